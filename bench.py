@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: bases/s k-mer-counted (k=31) on MI355X — BASELINE.json `metric`.
+
+One step = one pass of the hot path over one batch of synthetic input with
+the batch already resident in HBM: extraction + canonicalisation + key-range
+partitioning + LDS counting + sorted (key, count) table on the device
+(count.rs:23-38 + :106-119), and for N>1 the owner-partitioned RCCL merge of
+the per-GPU tables (okm/dist.py).
+
+Workload (configs[1]): k=31, 1 GiB synthetic FASTQ of 150 bp reads =
+3,355,443 reads = 503,316,450 bases per GPU, sampled from a seeded 100 Mbp
+random genome (0.1 % substitutions, 0.01 % N).  With
+--gpus N every rank counts its own 3,355,443 reads of the same genome (weak
+scaling) and the tables are merged.
+
+Prints ONE JSON line on rank 0 (the driver's contract), including `roofline`
+for the dominant kernel (HIP events on the engine's own stream) and
+`cpu_baseline` (the oracle, oracle/okm_oracle.c, on a bounded sample, rank 0
+at N=1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orion-kmer_amd"))
+
+import numpy as np  # noqa: E402
+
+import okm  # noqa: E402
+from okm import _lib  # noqa: E402
+
+# Load the engine (and the HIP runtime it links) before torch, so the process
+# has exactly one HIP runtime.
+_lib.load()
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "bases/sec k-mer-counted (k=31) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+K = 31
+READS_PER_GPU = 3_355_443
+READ_LEN = 150
+GENOME_BP = 100_000_000
+GENOME_SEED = 2
+READ_SEED = 2
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=READS_PER_GPU, help="reads per GPU")
+    ap.add_argument("--cpu-sample-reads", type=int, default=300_000,
+                    help="reads in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    device = local
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+
+    # ---- synthetic batch for this rank, made resident in HBM ---------------
+    t0 = time.time()
+    first = rank * args.reads
+    batch = okm.synth_reads(args.reads, READ_LEN, genome_len=GENOME_BP, genome_seed=GENOME_SEED, seed=READ_SEED,
+                            first_read=first, sub_rate=0.001, n_rate=0.0001)
+    bases = args.reads * READ_LEN
+    dbuf = okm.DeviceBuffer(len(batch), device)
+    dbuf.upload(batch)
+    log(f"[rank {rank}] synthetic batch: {args.reads} reads, {bases} bases, {len(batch)} bytes "
+        f"({time.time() - t0:.1f}s)")
+
+    ctr = okm.KmerCounter(K, "count", device)
+    merger = okm.KmerCounter(K, "count", device) if world > 1 else None
+    if world > 1:
+        from okm import dist as okm_dist
+
+    def step():
+        ctr.reset()
+        ctr.add_device_batch(dbuf.address, len(batch))
+        n = ctr.count()
+        if world == 1:
+            return n
+        keys = torch.empty(n, dtype=torch.int64, device="cuda")
+        counts = torch.empty(n, dtype=torch.int64, device="cuda")
+        ctr.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
+        rk, rc, _ = okm_dist.exchange(keys, counts, K)
+        torch.cuda.synchronize()
+        merger.reset()
+        if rk.numel():
+            merger.add_pairs_device(rk.data_ptr(), rc.data_ptr(), rk.numel())
+        return merger.count()
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        ctr.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctr.set_timing(not args.no_timing)
+    barrier_sync()
+    t_start = time.perf_counter()
+    n_owned = 0
+    for _ in range(args.steps):
+        n_owned = step()
+    barrier_sync()
+    dt = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    stats = ctr.kernel_stats() if not args.no_timing else {}
+    info = ctr.engine_info()
+
+    # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) -------
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle import OracleCounter
+        m = min(args.cpu_sample_reads, args.reads)
+        sample = batch[:m * (READ_LEN + 1)]
+        oc = OracleCounter(K)
+        tc = time.perf_counter()
+        oc.add_separated(sample)
+        keys_c, counts_c = oc.result(1)
+        tcpu = time.perf_counter() - tc
+        cpu = {"value": m * READ_LEN / tcpu, "unit": "bases/s", "cores": 1, "kind": "port",
+               "sample": f"first {m} reads ({m * READ_LEN} bases) of the same batch, k=31, "
+                         f"oracle/okm_oracle.c (faithful O(k) encode+rc per window, 1 thread, "
+                         f"count.rs is single-threaded), {tcpu:.1f} s incl. filter+sort"}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    value = world * bases * args.steps / dt
+    # dominant kernel by device time in the timed region
+    roof = None
+    kernels = {}
+    if stats:
+        for name, s in stats.items():
+            if s["launches"]:
+                avg = s["total_ms"] / s["launches"]
+                per = s["alg_bytes"] / s["launches"]
+                kernels[name] = {"launches": s["launches"], "avg_ms": round(avg, 4),
+                                 "alg_bytes_per_launch": per,
+                                 "achieved_GBs": round(per / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
+        dom = max(kernels, key=lambda n: stats[n]["total_ms"])
+        dk = kernels[dom]
+        ach = dk["achieved_GBs"]
+        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
+                "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"]}
+        tot_ms = sum(s["total_ms"] for s in stats.values())
+        tot_bytes = sum(s["alg_bytes"] for s in stats.values())
+        roof["path_achieved_GBs"] = round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1) if tot_ms > 0 else None
+        roof["path_alg_bytes_per_base"] = round(tot_bytes / (bases * args.steps), 2)
+    # SURVEY §8(d) whole-path roofline: 1 B/base + 16 B per k-mer instance
+    kmers = info["kmers"]
+    surv_bytes = bases + 16.0 * kmers
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "bases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1000, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded reads from a random genome, device-resident)",
+        "config": {"workload": "BASELINE configs[1]: k=31, 1 GiB synthetic 150 bp FASTQ per GPU "
+                               f"({args.reads} reads, {bases} bases), single MI355X; N>1: same shard "
+                               "per GPU + RCCL owner-partitioned table merge",
+                   "k": K, "reads_per_gpu": args.reads, "read_len": READ_LEN, "genome_bp": GENOME_BP,
+                   "distinct_kmers": int(info["distinct"]) if world == 1 else None,
+                   "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,
+                            "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
+                            "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
+                            "input_stream_frac": round(bases * args.steps / dt / 8e12, 5)},
+        "kernels": kernels,
+        "engine": info,
+    }
+    if world > 1:
+        out["config"]["owned_distinct_rank0"] = int(n_owned)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    dbuf.free()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,266 @@
+/*
+ * orion_kmer.h — C ABI of the MI355X-native k-mer engine (liborion_kmer.so).
+ *
+ * This is the drop-in boundary for orion-kmer's data-parallel hot path
+ * (reference: motroy/orion-kmer, Rust crate `orion-kmer/`).  Everything is
+ * `extern "C"`, plain pointers and sizes; no C++ types, exceptions or torch
+ * types cross it.  Each entry point names the reference interface it
+ * replaces (paths relative to the reference's `orion-kmer/` directory).
+ *
+ * The reference has no FFI of its own: its seam is the private
+ *   fn process_sequence_chunk(seq: &[u8], k: u8, map: &DashMap<u64, AtomicUsize>)
+ * (src/commands/count.rs:23), driven record by record from run_count's
+ * `while let Some(record) = reader.next()` loop (count.rs:68-72), plus the
+ * DashMap's drain/filter/sort at count.rs:106-119.  A Rust maintainer binds
+ * this header with `extern "C"` declarations.
+ *
+ * Conventions
+ *  - Every fallible call returns okm_status; nothing aborts across the ABI.
+ *  - Caller owns inputs; results returned through `**` out-pointers are
+ *    library-allocated host memory released with okm_free_result().
+ *  - A context is used by one host thread at a time (the reference's `count`
+ *    is single-threaded, count.rs:6,68-79).  Internally it owns one HIP
+ *    stream on one device; results are complete when a call returns.
+ *  - k in 1..=32 (u64 keys, kmer.rs:37-43).  Anything else is
+ *    OKM_E_INVALID_K, which the CLI prints as the reference's
+ *    "Invalid K-mer size: {k}. Must be between 1 and 32." (errors.rs:6).
+ *  - The library has NO CPU fallback: without a usable gfx950 device every
+ *    compute entry point fails with OKM_E_DEVICE.
+ */
+#ifndef ORION_KMER_H
+#define ORION_KMER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OKM_ABI_VERSION 1
+
+/* Byte that separates records in the device batch layout: any byte that is
+ * not A/C/G/T/U (either case) kills every window containing it, so windows
+ * never cross records (count.rs:23-38 is per record). */
+#define OKM_RECORD_SEPARATOR ((uint8_t)'\n')
+
+typedef struct okm_ctx okm_ctx;
+typedef struct okm_reader okm_reader;
+
+typedef enum okm_status {
+    OKM_OK = 0,
+    OKM_E_INVALID_K = 1,   /* errors.rs:6 InvalidKmerSize */
+    OKM_E_NOMEM = 2,       /* host or device allocation failed */
+    OKM_E_DEVICE = 3,      /* no usable GPU / HIP runtime error */
+    OKM_E_COMM = 4,        /* reserved (multi-GPU exchange) */
+    OKM_E_ARG = 5,         /* bad argument (null pointer, bad length ...) */
+    OKM_E_OVERFLOW = 6,    /* capacity exceeded (caller buffer too small) */
+    OKM_E_IO = 7,          /* file open/read/write failed */
+    OKM_E_PARSE = 8,       /* not FASTA/FASTQ (first byte), empty file */
+    OKM_E_RECORD = 9,      /* malformed record */
+    OKM_E_STATE = 10,      /* call out of order (e.g. fetch before count) */
+    OKM_E_FORMAT = 11      /* bad KmerDbV2 bytes */
+} okm_status;
+
+typedef enum okm_mode {
+    OKM_MODE_COUNT = 0,    /* count.rs: DashMap<u64, AtomicUsize> */
+    OKM_MODE_SET = 1       /* build.rs:50-58: DashSet<u64> */
+} okm_mode;
+
+/* ------------------------------------------------------------------------
+ * Library / device
+ * ---------------------------------------------------------------------- */
+
+int okm_abi_version(void);
+const char *okm_status_string(okm_status s);
+/* Number of visible HIP devices (0 when none; never an error). */
+int okm_device_count(void);
+/* Name of the device's ISA ("gfx950"), or "" when unavailable. */
+const char *okm_device_arch(int device);
+/* Thread-local message of the last failing call on this thread. */
+const char *okm_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Counting context — replaces DashMap::new() (count.rs:48) / DashSet::new()
+ * (build.rs:95) and everything process_sequence_chunk (count.rs:23-38) does
+ * to it.
+ * ---------------------------------------------------------------------- */
+
+/* device: HIP ordinal.  distinct_hint: expected distinct k-mers (0 = unknown);
+ * sizing only, never correctness. */
+okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint);
+void okm_destroy(okm_ctx *ctx);
+/* Forget all input and results; keep device allocations for reuse. */
+okm_status okm_reset(okm_ctx *ctx);
+
+/* Append one batch of records held in HOST memory.  Record r is
+ * seq[offsets[r] .. offsets[r+1]) (offsets has n_records+1 entries).
+ * normalized=0: the bytes are raw sequence bytes and the library applies
+ * needletail normalize(false) semantics (case fold, U->T, whitespace and
+ * line breaks removed, anything else kills the window) — the call at
+ * count.rs:71.  normalized=1: caller already normalised (whitespace-free).
+ * Replaces the record loop count.rs:68-72. */
+okm_status okm_add_batch(okm_ctx *ctx, const uint8_t *seq, const uint64_t *offsets,
+                         uint64_t n_records, int normalized);
+
+/* Append a batch already resident in DEVICE memory in the batch layout:
+ * whitespace-free records joined by OKM_RECORD_SEPARATOR.  The bytes are
+ * consumed (k-mers extracted) before the call returns; the caller may reuse
+ * the buffer afterwards.  This is the zero-copy hot path. */
+okm_status okm_add_batch_device(okm_ctx *ctx, const uint8_t *d_seq, uint64_t n_bytes);
+
+/* Append (canonical key, count) pairs in DEVICE memory, e.g. partial tables
+ * received from other GPUs.  Counts add (the AtomicUsize fetch_add of
+ * count.rs:31-34 generalised to a weight). */
+okm_status okm_add_pairs_device(okm_ctx *ctx, const uint64_t *d_keys, const uint64_t *d_counts,
+                                uint64_t n);
+/* Same, from HOST memory. */
+okm_status okm_add_pairs(okm_ctx *ctx, const uint64_t *keys, const uint64_t *counts, uint64_t n);
+
+/* Run the counting over everything added so far; *n_distinct receives the
+ * number of distinct canonical k-mers (DashMap::len()).  Idempotent until the
+ * next add. */
+okm_status okm_count(okm_ctx *ctx, uint64_t *n_distinct);
+
+/* Copy the counted table, filtered to count >= min_count and sorted
+ * ascending by key (count.rs:106-119), into caller buffers of capacity
+ * `cap` entries.  dst_on_device!=0: keys/counts are device pointers (counts
+ * may be NULL).  *n receives the number of entries written. */
+okm_status okm_fetch_counts(okm_ctx *ctx, uint64_t min_count, uint64_t *keys, uint64_t *counts,
+                            uint64_t cap, uint64_t *n, int dst_on_device);
+/* Number of entries okm_fetch_counts would return for min_count. */
+okm_status okm_result_size(okm_ctx *ctx, uint64_t min_count, uint64_t *n);
+
+/* count + fetch into library-allocated host arrays (free with okm_free_result). */
+okm_status okm_finish_counts(okm_ctx *ctx, uint64_t min_count, uint64_t **keys, uint64_t **counts,
+                             uint64_t *n);
+/* Set mode result (build.rs:104): sorted unique canonical k-mers. */
+okm_status okm_finish_set(okm_ctx *ctx, uint64_t **keys, uint64_t *n);
+void okm_free_result(void *p);
+
+/* Device pointers to the counted, sorted, unfiltered table (valid until the
+ * next add/reset/destroy). */
+okm_status okm_result_device(okm_ctx *ctx, const uint64_t **d_keys, const uint64_t **d_counts,
+                             uint64_t *n);
+
+/* |A ∩ B| of two sorted unique key arrays in host memory, computed on the
+ * device (compare.rs:58 HashSet::intersection().count()). */
+okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint64_t *b,
+                                     uint64_t nb, int device, uint64_t *out);
+
+/* ------------------------------------------------------------------------
+ * Instrumentation (bench.py measures kernels with HIP events on the
+ * context's own stream).
+ * ---------------------------------------------------------------------- */
+okm_status okm_synchronize(okm_ctx *ctx);
+okm_status okm_set_timing(okm_ctx *ctx, int enable);
+/* Per-kernel stats accumulated since okm_set_timing(ctx,1): fills up to
+ * `cap` entries; *n receives the number of kernels.  name[i] points into
+ * library storage. */
+typedef struct okm_kernel_stat {
+    const char *name;
+    uint64_t launches;
+    double total_ms;        /* sum of HIP-event durations */
+    double alg_bytes;       /* algorithmic HBM bytes moved */
+} okm_kernel_stat;
+okm_status okm_kernel_stats(okm_ctx *ctx, okm_kernel_stat *stats, int cap, int *n);
+/* Engine counters of the last okm_count (partition levels, max partition,...) */
+typedef struct okm_engine_info {
+    uint64_t kmers;          /* valid windows (sum of counts) */
+    uint64_t distinct;
+    uint32_t l1_bits;        /* first-level key-range partition bits */
+    uint32_t l2_bits;        /* second-level bits (0 = not needed) */
+    uint32_t levels;         /* partition passes over keys */
+    uint32_t work_items;     /* partitions counted in LDS */
+    uint64_t max_partition;  /* largest partition (instances) */
+    uint64_t device_bytes;   /* device memory held */
+} okm_engine_info;
+okm_status okm_engine_info_get(okm_ctx *ctx, okm_engine_info *info);
+
+/* Device memory helpers (so a host program without a GPU framework can stage
+ * device-resident batches). */
+okm_status okm_device_alloc(int device, uint64_t bytes, void **d_ptr);
+okm_status okm_device_free(void *d_ptr);
+okm_status okm_memcpy_h2d(void *d_dst, const void *src, uint64_t bytes);
+okm_status okm_memcpy_d2h(void *dst, const void *d_src, uint64_t bytes);
+
+/* ------------------------------------------------------------------------
+ * k-mer codec parity surface — kmer.rs pub fns (CPU; for tests and hosts).
+ * ---------------------------------------------------------------------- */
+/* kmer.rs:37-57 seq_to_u64: returns 1 and writes *out for Some, 0 for None. */
+int okm_seq_to_u64(const uint8_t *seq, size_t len, uint8_t k, uint64_t *out);
+/* kmer.rs:61-75 u64_to_seq: writes k bytes; returns 0 (reference panics) for bad k. */
+int okm_u64_to_seq(uint64_t v, uint8_t k, char *out);
+/* kmer.rs:79-94; returns 0 (reference panics) for bad k. */
+uint64_t okm_reverse_complement_u64(uint64_t v, uint8_t k);
+/* kmer.rs:99-106 */
+uint64_t okm_canonical_u64(uint64_t v, uint8_t k);
+
+/* ------------------------------------------------------------------------
+ * Host record source — replaces needletail parse_fastx_reader + record
+ * normalize (count.rs:59-72) and the extension-based decompression of
+ * utils.rs:125-152.  Produces normalised batches in the layout okm_add_batch
+ * takes.
+ * ---------------------------------------------------------------------- */
+/* decompress_by_extension=1: count/query behaviour (utils.rs:125-152:
+ * .gz/.xz/.zst/.zstd by lower-cased extension); 0: build/classify behaviour
+ * (utils.rs:157-161, raw bytes).  needletail's own gzip/bzip2/xz magic
+ * sniffing is applied after that in both cases. */
+okm_status okm_reader_open(okm_reader **out, const char *path, int decompress_by_extension);
+/* Next batch of at most ~max_bytes sequence bytes (at least one record).
+ * Pointers stay valid until the next call.  *n_records == 0 at end. */
+okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **seq,
+                           const uint64_t **offsets, uint64_t *n_records);
+uint64_t okm_reader_records(const okm_reader *r);
+void okm_reader_close(okm_reader *r);
+/* Parse a whole in-memory FASTA/FASTQ buffer (after sniffing compression). */
+okm_status okm_parse_buffer(const uint8_t *data, uint64_t n, uint8_t **seq, uint64_t **offsets,
+                            uint64_t *n_records);
+
+/* ------------------------------------------------------------------------
+ * Output codecs — utils.rs:167-198 get_output_writer (.gz/.xz/.zst by
+ * extension, else plain) and the TSV of count.rs:127-135.
+ * ---------------------------------------------------------------------- */
+/* Writes "KMER\tCOUNT\n" lines for sorted (keys, counts). */
+okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *keys,
+                                const uint64_t *counts, uint64_t n);
+/* Writes `n` raw bytes through the extension-selected compressor. */
+okm_status okm_write_file(const char *path, const uint8_t *data, uint64_t n);
+/* Reads a whole file, decompressing by extension (utils.rs:125-152). */
+okm_status okm_read_file(const char *path, int decompress_by_extension, uint8_t **data, uint64_t *n);
+
+/* ------------------------------------------------------------------------
+ * KmerDbV2 (db_types.rs:7-14) bincode 1.3 codec — build.rs:141-146 writer,
+ * utils.rs:37-55 reader.  Layout: u8 k; u64 n_refs; per ref: u64 len, name
+ * bytes, u64 n_keys, n_keys × u64 (all little-endian).
+ * ---------------------------------------------------------------------- */
+typedef struct okm_db okm_db;
+okm_status okm_db_new(okm_db **out, uint8_t k);
+/* db_types.rs:38-40 add_reference: a duplicate name overwrites. `keys` are
+ * copied. */
+okm_status okm_db_add_reference(okm_db *db, const char *name, const uint64_t *keys, uint64_t n);
+okm_status okm_db_write(const okm_db *db, const char *path);
+okm_status okm_db_read(okm_db **out, const char *path);
+uint8_t okm_db_k(const okm_db *db);
+uint64_t okm_db_num_references(const okm_db *db);
+/* Reference i: name (NUL-terminated, library storage), keys (library storage). */
+okm_status okm_db_reference(const okm_db *db, uint64_t i, const char **name, const uint64_t **keys,
+                            uint64_t *n);
+void okm_db_free(okm_db *db);
+
+/* ------------------------------------------------------------------------
+ * Seeded synthetic reads (bench / tests; SURVEY.md §8(d) generator).
+ * Reads of `read_len` bases sampled from a random genome of `genome_len`
+ * bases (genome drawn from genome_seed), strand 50/50, substitution rate
+ * sub_rate, N rate n_rate, per-read draws keyed by (seed, read index).
+ * Output: n_reads records in the device batch layout, each followed by
+ * OKM_RECORD_SEPARATOR: out must hold n_reads*(read_len+1) bytes.
+ * ---------------------------------------------------------------------- */
+okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t seed,
+                           uint64_t first_read, uint64_t n_reads, uint32_t read_len,
+                           double sub_rate, double n_rate, uint8_t *out, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORION_KMER_H */

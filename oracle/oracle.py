@@ -1,0 +1,119 @@
+"""ctypes binding of the C restatement (oracle/okm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — the checker for tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.  Builds oracle/build/liboracle.so on demand with
+gcc (oracle/Makefile).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint64, c_void_p
+from typing import Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "okm_oracle.c")):
+        build()
+    lib = ctypes.CDLL(LIB)
+    lib.oracle_seq_to_u64.restype = c_int
+    lib.oracle_seq_to_u64.argtypes = [c_char_p, c_size_t, c_uint8, POINTER(c_uint64)]
+    lib.oracle_reverse_complement_u64.restype = c_uint64
+    lib.oracle_reverse_complement_u64.argtypes = [c_uint64, c_uint8]
+    lib.oracle_canonical_u64.restype = c_uint64
+    lib.oracle_canonical_u64.argtypes = [c_uint64, c_uint8]
+    lib.oracle_u64_to_seq.restype = c_int
+    lib.oracle_u64_to_seq.argtypes = [c_uint64, c_uint8, c_char_p]
+    lib.oracle_normalize.restype = c_size_t
+    lib.oracle_normalize.argtypes = [c_char_p, c_size_t, c_char_p]
+    lib.oracle_counter_new.restype = c_void_p
+    lib.oracle_counter_new.argtypes = [c_uint8]
+    lib.oracle_counter_free.argtypes = [c_void_p]
+    lib.oracle_counter_add_record.argtypes = [c_void_p, c_char_p, c_size_t, c_int]
+    lib.oracle_counter_add_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int]
+    lib.oracle_counter_add_pairs.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64]
+    lib.oracle_counter_distinct.restype = c_uint64
+    lib.oracle_counter_distinct.argtypes = [c_void_p]
+    lib.oracle_counter_windows.restype = c_uint64
+    lib.oracle_counter_windows.argtypes = [c_void_p]
+    lib.oracle_counter_result.restype = c_uint64
+    lib.oracle_counter_result.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]
+    _lib = lib
+    return lib
+
+
+class OracleCounter:
+    """count.rs:23-38 + :106-119 restated in C (O(k) per window, one core)."""
+
+    def __init__(self, k: int):
+        self.k = k
+        self.h = load().oracle_counter_new(k)
+        if not self.h:
+            raise ValueError(f"Invalid K-mer size: {k}. Must be between 1 and 32.")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            load().oracle_counter_free(self.h)
+            self.h = None
+
+    def add_records(self, seqs: Sequence[bytes], normalized: bool = False) -> None:
+        for s in seqs:
+            load().oracle_counter_add_record(self.h, s, len(s), 1 if normalized else 0)
+
+    def add_batch(self, data: np.ndarray, offsets: np.ndarray, normalized: bool = False) -> None:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        load().oracle_counter_add_batch(self.h, data.ctypes.data, offsets.ctypes.data, len(offsets) - 1,
+                                        1 if normalized else 0)
+
+    def add_separated(self, data: np.ndarray, sep: int = ord("\n")) -> None:
+        """A batch in the device layout (records joined by `sep`)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        cut = np.flatnonzero(data == sep)
+        starts = np.concatenate([[0], cut + 1]).astype(np.uint64)
+        ends = np.concatenate([cut, [len(data)]]).astype(np.uint64)
+        keep = ends > starts
+        # records are [start, end); express them as an offsets array over a
+        # separator-free copy
+        lens = (ends - starts)[keep]
+        body = np.delete(data, cut) if len(cut) else data
+        offs = np.zeros(len(lens) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens)
+        self.add_batch(body, offs, normalized=False)
+
+    def add_pairs(self, keys: np.ndarray, counts: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        counts = np.ascontiguousarray(counts, dtype=np.uint64)
+        load().oracle_counter_add_pairs(self.h, keys.ctypes.data, counts.ctypes.data, len(keys))
+
+    @property
+    def distinct(self) -> int:
+        return int(load().oracle_counter_distinct(self.h))
+
+    @property
+    def windows(self) -> int:
+        return int(load().oracle_counter_windows(self.h))
+
+    def result(self, min_count: int = 1) -> Tuple[np.ndarray, np.ndarray]:
+        n = self.distinct
+        keys = np.empty(max(n, 1), dtype=np.uint64)
+        counts = np.empty(max(n, 1), dtype=np.uint64)
+        m = load().oracle_counter_result(self.h, min_count, keys.ctypes.data, counts.ctypes.data, n)
+        return keys[:m].copy(), counts[:m].copy()

@@ -1,0 +1,1016 @@
+// okm_engine.hip — host side of the counting context (C ABI in orion_kmer.h).
+//
+// One okm_ctx = one device + one HIP stream.  Work per okm_count():
+//
+//   add_batch*:  L1 pass per batch (extract_hist -> host offsets ->
+//                extract_scatter): the batch's canonical k-mers land in 2^l1
+//                key-range partitions ("runs"; one run per batch).
+//   okm_count:   split every partition whose size could exceed the LDS table
+//                (rounds of part_hist/part_scatter, each consuming more key
+//                bits, per-partition bit budget), then count_items (LDS table
+//                + sort per partition), then compact to one dense sorted
+//                (key, count) table.
+//
+// Replaces run_count's map (count.rs:48), its per-record fill
+// (count.rs:68-72 -> process_sequence_chunk count.rs:23-38) and its
+// drain/filter/sort (count.rs:106-119).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "okm_internal.h"
+
+namespace okm {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+okm_status fail(okm_status s, const std::string &msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail(e_ == hipErrorOutOfMemory ? OKM_E_NOMEM : OKM_E_DEVICE,                  \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                      \
+    } while (0)
+
+#define OKM_TRY(expr)                    \
+    do {                                 \
+        okm_status s_ = (expr);          \
+        if (s_ != OKM_OK) return s_;     \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Device memory pool (best-fit free list; GB-sized buffers are reused across
+// okm_count calls instead of hipMalloc/hipFree in the hot loop).
+// ---------------------------------------------------------------------------
+struct DevPool {
+    std::multimap<size_t, void *> free_;
+    std::map<void *, size_t> size_;
+    size_t held = 0;
+
+    okm_status get(size_t bytes, void **out) {
+        bytes = (bytes + 255) & ~size_t(255);
+        if (bytes == 0) bytes = 256;
+        auto it = free_.lower_bound(bytes);
+        if (it != free_.end() && it->first <= bytes * 2) {
+            *out = it->second;
+            free_.erase(it);
+            return OKM_OK;
+        }
+        void *p = nullptr;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            // release cached blocks and retry once
+            trim();
+            (void)hipGetLastError();
+            e = hipMalloc(&p, bytes);
+            if (e != hipSuccess)
+                return fail(OKM_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+        }
+        size_[p] = bytes;
+        held += bytes;
+        *out = p;
+        return OKM_OK;
+    }
+    void put(void *p) {
+        if (!p) return;
+        auto it = size_.find(p);
+        if (it == size_.end()) return;
+        free_.emplace(it->second, p);
+    }
+    void trim() {
+        for (auto &kv : free_) {
+            (void)hipFree(kv.second);
+            held -= size_[kv.second];
+            size_.erase(kv.second);
+        }
+        free_.clear();
+    }
+    void release_all() {
+        for (auto &kv : size_) (void)hipFree(kv.first);
+        size_.clear();
+        free_.clear();
+        held = 0;
+    }
+};
+
+template <typename T>
+static okm_status pool_get(DevPool &pool, size_t n, T **out) {
+    void *p = nullptr;
+    OKM_TRY(pool.get(n * sizeof(T), &p));
+    *out = static_cast<T *>(p);
+    return OKM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// HIP-event kernel timing (okm_set_timing / okm_kernel_stats)
+// ---------------------------------------------------------------------------
+struct KernelTimer {
+    bool on = false;
+    struct Pending {
+        int id;
+        hipEvent_t a, b;
+        double bytes;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> spare;
+    std::vector<std::string> names;
+    std::vector<okm_kernel_stat> stats;
+    hipEvent_t cur_a = nullptr;
+
+    int id_of(const char *name) {
+        for (size_t i = 0; i < names.size(); ++i)
+            if (names[i] == name) return (int)i;
+        names.emplace_back(name);
+        okm_kernel_stat st{};
+        stats.push_back(st);
+        return (int)names.size() - 1;
+    }
+    hipEvent_t ev() {
+        if (!spare.empty()) {
+            hipEvent_t e = spare.back();
+            spare.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void begin(hipStream_t s) {
+        if (!on) return;
+        cur_a = ev();
+        (void)hipEventRecord(cur_a, s);
+    }
+    void end(hipStream_t s, const char *name, double bytes) {
+        if (!on) return;
+        hipEvent_t b = ev();
+        (void)hipEventRecord(b, s);
+        pending.push_back({id_of(name), cur_a, b, bytes});
+    }
+    // call after the stream is synchronised
+    void flush() {
+        for (auto &p : pending) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, p.a, p.b);
+            stats[p.id].launches += 1;
+            stats[p.id].total_ms += ms;
+            stats[p.id].alg_bytes += p.bytes;
+            spare.push_back(p.a);
+            spare.push_back(p.b);
+        }
+        pending.clear();
+    }
+    void reset() {
+        flush();
+        for (auto &s : stats) s = okm_kernel_stat{};
+    }
+    void destroy() {
+        flush();
+        for (auto e : spare) (void)hipEventDestroy(e);
+        spare.clear();
+    }
+};
+
+// L1-partitioned keys of one batch (or one add_pairs call).
+struct Run {
+    uint64_t *keys = nullptr;
+    uint64_t *counts = nullptr;  // null: every key weighs 1
+    std::vector<uint64_t> off;   // nbins + 1 offsets
+};
+
+}  // namespace okm
+
+using namespace okm;
+
+struct okm_ctx {
+    int device = 0;
+    uint8_t k = 0;
+    okm_mode mode = OKM_MODE_COUNT;
+    hipStream_t stream = nullptr;
+    uint32_t l1_bits = 0, nbins = 1, shift1 = 64;
+
+    DevPool pool;
+    std::vector<Run> runs;
+    KernelTimer timer;
+
+    // small persistent scratch
+    uint32_t *HC = nullptr;
+    size_t HC_cap = 0;
+    unsigned long long *Hg = nullptr, *cursor = nullptr;
+    size_t Hg_cap = 0;
+    unsigned long long *flag = nullptr;  // overflow word
+    uint8_t *staging = nullptr;          // device copy of a host batch
+    size_t staging_cap = 0;
+    uint8_t *pinned = nullptr;           // pinned host staging
+    size_t pinned_cap = 0;
+
+    // result
+    bool counted = false;
+    uint64_t *res_keys = nullptr, *res_counts = nullptr;
+    uint64_t n_res = 0;
+    okm_engine_info info{};
+};
+
+namespace okm {
+
+static okm_status ensure_hc(okm_ctx *c, size_t n_u32) {
+    if (n_u32 <= c->HC_cap) return OKM_OK;
+    if (c->HC) (void)hipFree(c->HC);
+    c->HC = nullptr;
+    size_t cap = std::max(n_u32, size_t(1) << 20);
+    HIP_TRY(hipMalloc(&c->HC, cap * sizeof(uint32_t)));
+    c->HC_cap = cap;
+    return OKM_OK;
+}
+
+static okm_status ensure_hg(okm_ctx *c, size_t n) {
+    if (n <= c->Hg_cap) return OKM_OK;
+    if (c->Hg) (void)hipFree(c->Hg);
+    if (c->cursor) (void)hipFree(c->cursor);
+    c->Hg = c->cursor = nullptr;
+    size_t cap = std::max(n, size_t(1) << 16);
+    HIP_TRY(hipMalloc(&c->Hg, cap * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&c->cursor, cap * sizeof(unsigned long long)));
+    c->Hg_cap = cap;
+    return OKM_OK;
+}
+
+static okm_status ensure_pinned(okm_ctx *c, size_t bytes) {
+    if (bytes <= c->pinned_cap) return OKM_OK;
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    size_t cap = std::max(bytes, size_t(1) << 20);
+    HIP_TRY(hipHostMalloc(&c->pinned, cap, hipHostMallocDefault));
+    c->pinned_cap = cap;
+    return OKM_OK;
+}
+
+static okm_status ensure_staging(okm_ctx *c, size_t bytes) {
+    if (bytes <= c->staging_cap) return OKM_OK;
+    if (c->staging) (void)hipFree(c->staging);
+    c->staging = nullptr;
+    size_t cap = std::max(bytes + 64, size_t(1) << 20);
+    HIP_TRY(hipMalloc(&c->staging, cap));
+    c->staging_cap = cap;
+    return OKM_OK;
+}
+
+static void invalidate_result(okm_ctx *c) {
+    if (c->res_keys) c->pool.put(c->res_keys);
+    if (c->res_counts) c->pool.put(c->res_counts);
+    c->res_keys = c->res_counts = nullptr;
+    c->n_res = 0;
+    c->counted = false;
+}
+
+static okm_status sync(okm_ctx *c) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipGetLastError());
+    c->timer.flush();
+    return OKM_OK;
+}
+
+// Host prefix sum of a device histogram -> offsets (host) and device cursor.
+static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &off) {
+    std::vector<unsigned long long> h(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), c->Hg, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    off.assign(nb + 1, 0);
+    for (size_t b = 0; b < nb; ++b) off[b + 1] = off[b] + h[b];
+    HIP_TRY(hipMemcpyAsync(c->cursor, off.data(), nb * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
+    return OKM_OK;
+}
+
+// L1 pass over a device-resident batch (whitespace-free records joined by
+// OKM_RECORD_SEPARATOR, 16-byte aligned).
+static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
+    if (n == 0) return OKM_OK;
+    const uint64_t tile = extract_tile();
+    uint64_t tiles = (n + tile - 1) / tile;
+    uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, 2048);
+    uint64_t chunk = ((tiles + nblocks - 1) / nblocks) * tile;
+    nblocks = (uint32_t)((n + chunk - 1) / chunk);
+    ExtractGeom g{n, c->k, c->shift1, c->nbins, nblocks, chunk};
+
+    OKM_TRY(ensure_hc(c, (size_t)nblocks * c->nbins));
+    OKM_TRY(ensure_hg(c, c->nbins));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, c->nbins * sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_extract_hist(c->stream, d_seq, g, c->HC, c->Hg);
+    c->timer.end(c->stream, "extract_hist", (double)n);
+    HIP_TRY(hipGetLastError());
+
+    Run run;
+    OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
+    const uint64_t total = run.off.back();
+    if (total == 0) return OKM_OK;
+    OKM_TRY(pool_get(c->pool, total, &run.keys));
+    c->timer.begin(c->stream);
+    launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys);
+    c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * (double)total);
+    HIP_TRY(hipGetLastError());
+    c->runs.push_back(std::move(run));
+    c->info.kmers += total;
+    return OKM_OK;
+}
+
+struct Part {
+    uint32_t seg_begin, seg_count;  // into the host segment table
+    uint64_t len;
+    uint64_t prefix;                // absolute key prefix at `consumed` bits
+    uint32_t consumed;
+};
+
+static const uint64_t kChunkKeys = 1u << 16;
+
+// One partition pass: split every part in `todo` by its own number of bits.
+// Segments of the parts are read; the result is a new level array whose bins
+// become the children (in key order) of each part.
+static okm_status split_round(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts,
+                              const std::vector<uint32_t> &todo, const std::vector<uint32_t> &bits,
+                              bool weighted, std::vector<void *> &level_bufs) {
+    const uint32_t twok = 2u * c->k;
+    std::vector<DevSeg> psegs;      // pass segments (one per input segment)
+    std::vector<DevChunk> chunks;
+    std::vector<uint32_t> out_base(todo.size());
+    uint32_t nout = 0, max_local = 1;
+    uint64_t total = 0;
+    for (size_t t = 0; t < todo.size(); ++t) {
+        const Part &p = parts[todo[t]];
+        const uint32_t b = bits[t];
+        const uint32_t nl = 1u << b;
+        out_base[t] = nout;
+        nout += nl;
+        max_local = std::max(max_local, nl);
+        for (uint32_t s = 0; s < p.seg_count; ++s) {
+            DevSeg d = segtab[p.seg_begin + s];
+            d.shift = twok - p.consumed - b;
+            d.key_base = p.prefix << b;
+            d.out_base = out_base[t];
+            d.nlocal = nl;
+            const uint32_t sid = (uint32_t)psegs.size();
+            psegs.push_back(d);
+            for (uint64_t o = 0; o < d.len; o += kChunkKeys)
+                chunks.push_back(DevChunk{sid, 0, o, std::min(kChunkKeys, d.len - o)});
+        }
+        total += p.len;
+    }
+    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)max_local));
+    OKM_TRY(ensure_hg(c, nout));
+    DevSeg *d_segs;
+    DevChunk *d_chunks;
+    OKM_TRY(pool_get(c->pool, psegs.size(), &d_segs));
+    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    level_bufs.push_back(d_segs);
+    level_bufs.push_back(d_chunks);
+    HIP_TRY(hipMemcpyAsync(d_segs, psegs.data(), psegs.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, nout * sizeof(unsigned long long), c->stream));
+    const double kb = weighted ? 16.0 : 8.0;
+    c->timer.begin(c->stream);
+    launch_part_hist(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->Hg);
+    c->timer.end(c->stream, "part_hist", 8.0 * (double)total);
+    HIP_TRY(hipGetLastError());
+    std::vector<uint64_t> off;
+    OKM_TRY(hist_to_offsets(c, nout, off));
+    uint64_t *lk = nullptr, *lc = nullptr;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &lk));
+    level_bufs.push_back(lk);
+    if (weighted) {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &lc));
+        level_bufs.push_back(lc);
+    }
+    c->timer.begin(c->stream);
+    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->cursor, lk, lc);
+    c->timer.end(c->stream, "part_scatter", 2.0 * kb * (double)total);
+    HIP_TRY(hipGetLastError());
+    c->info.levels += 1;
+
+    // replace each split part by its children
+    std::vector<Part> next;
+    next.reserve(parts.size() + nout);
+    size_t t = 0;
+    for (uint32_t i = 0; i < parts.size(); ++i) {
+        if (t < todo.size() && todo[t] == i) {
+            const Part &p = parts[i];
+            const uint32_t b = bits[t];
+            for (uint32_t l = 0; l < (1u << b); ++l) {
+                const uint32_t ob = out_base[t] + l;
+                const uint64_t len = off[ob + 1] - off[ob];
+                if (!len) continue;
+                DevSeg d{};
+                d.keys = lk + off[ob];
+                d.counts = lc ? lc + off[ob] : nullptr;
+                d.len = len;
+                d.shift = 64;
+                d.nlocal = 1;
+                Part ch{(uint32_t)segtab.size(), 1, len, (p.prefix << b) | l, p.consumed + b};
+                segtab.push_back(d);
+                next.push_back(ch);
+            }
+            ++t;
+        } else {
+            next.push_back(parts[i]);
+        }
+    }
+    parts.swap(next);
+    return OKM_OK;
+}
+
+static uint32_t log2_floor(uint64_t x) {
+    uint32_t r = 0;
+    while (x > 1) {
+        x >>= 1;
+        ++r;
+    }
+    return r;
+}
+
+static okm_status do_count(okm_ctx *c) {
+    if (c->counted) return OKM_OK;
+    invalidate_result(c);
+    const uint32_t twok = 2u * c->k;
+    const uint64_t cap = count_item_capacity();        // distinct per item
+    const uint32_t capbits = log2_floor(cap);          // 2^capbits <= cap
+    const uint64_t target = cap * 3 / 4;               // aim below cap after a split
+
+    // initial parts: the L1 bins, each a list of per-run segments
+    std::vector<DevSeg> segtab;
+    std::vector<Part> parts;
+    bool weighted = false;
+    for (auto &r : c->runs) weighted |= (r.counts != nullptr);
+    for (uint32_t b = 0; b < c->nbins; ++b) {
+        Part p{(uint32_t)segtab.size(), 0, 0, b, c->l1_bits};
+        for (auto &r : c->runs) {
+            const uint64_t len = r.off[b + 1] - r.off[b];
+            if (!len) continue;
+            DevSeg d{};
+            d.keys = r.keys + r.off[b];
+            d.counts = r.counts ? r.counts + r.off[b] : nullptr;
+            d.len = len;
+            d.shift = 64;
+            d.nlocal = 1;
+            segtab.push_back(d);
+            p.seg_count++;
+            p.len += len;
+        }
+        if (p.len) parts.push_back(p);
+    }
+    c->info.l1_bits = c->l1_bits;
+    c->info.l2_bits = 0;
+    c->info.levels = 0;
+
+    // split rounds until every part is countable in one LDS table
+    std::vector<void *> level_bufs;
+    for (int round = 0; round < 64; ++round) {
+        std::vector<uint32_t> todo, bits;
+        for (uint32_t i = 0; i < parts.size(); ++i) {
+            const Part &p = parts[i];
+            const uint32_t rem = twok - p.consumed;
+            if (p.len <= cap || rem <= capbits) continue;
+            uint32_t b = 1;
+            while (b < 12 && (p.len >> b) > target) ++b;
+            b = std::min(b, rem);
+            todo.push_back(i);
+            bits.push_back(b);
+        }
+        if (todo.empty()) break;
+        if (round == 0) c->info.l2_bits = bits.empty() ? 0 : *std::max_element(bits.begin(), bits.end());
+        OKM_TRY(split_round(c, segtab, parts, todo, bits, weighted, level_bufs));
+    }
+
+    // count every part in LDS
+    const uint32_t nitems = (uint32_t)parts.size();
+    c->info.work_items = nitems;
+    c->info.max_partition = 0;
+    std::vector<DevItem> items(nitems);
+    uint64_t out_total = 0, in_total = 0;
+    for (uint32_t i = 0; i < nitems; ++i) {
+        items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total};
+        out_total += std::min<uint64_t>(parts[i].len, cap);
+        in_total += parts[i].len;
+        c->info.max_partition = std::max(c->info.max_partition, parts[i].len);
+    }
+    if (nitems == 0) {
+        for (void *p : level_bufs) c->pool.put(p);
+        c->counted = true;
+        c->n_res = 0;
+        c->info.distinct = 0;
+        return OKM_OK;
+    }
+    DevSeg *d_segs;
+    DevItem *d_items;
+    uint64_t *sk, *sc;
+    unsigned long long *n_out, *dense_off, *scan_tmp;
+    OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
+    OKM_TRY(pool_get(c->pool, nitems, &d_items));
+    OKM_TRY(pool_get(c->pool, out_total, &sk));
+    OKM_TRY(pool_get(c->pool, out_total, &sc));
+    OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
+    OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_items, items.data(), nitems * sizeof(DevItem), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->flag, 0, sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag);
+    c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
+    HIP_TRY(hipGetLastError());
+    launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
+    HIP_TRY(hipGetLastError());
+    unsigned long long hv[2];
+    HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    if (hv[1]) return fail(OKM_E_OVERFLOW, "LDS count table overflow (partition sizing invariant broken)");
+    const uint64_t nd = hv[0];
+    if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    c->timer.begin(c->stream);
+    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts);
+    c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(sync(c));
+    for (void *p : level_bufs) c->pool.put(p);
+    c->pool.put(d_segs);
+    c->pool.put(d_items);
+    c->pool.put(sk);
+    c->pool.put(sc);
+    c->pool.put(n_out);
+    c->pool.put(dense_off);
+    c->pool.put(scan_tmp);
+    c->n_res = nd;
+    c->info.distinct = nd;
+    c->counted = true;
+    return OKM_OK;
+}
+
+static bool device_ok(int device, std::string *why) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        *why = "no HIP device visible (the engine has no CPU fallback)";
+        return false;
+    }
+    if (device < 0 || device >= n) {
+        *why = "device ordinal " + std::to_string(device) + " out of range (" + std::to_string(n) + " visible)";
+        return false;
+    }
+    return true;
+}
+
+}  // namespace okm
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int okm_abi_version(void) { return OKM_ABI_VERSION; }
+
+const char *okm_status_string(okm_status s) {
+    switch (s) {
+    case OKM_OK: return "ok";
+    case OKM_E_INVALID_K: return "invalid k";
+    case OKM_E_NOMEM: return "out of memory";
+    case OKM_E_DEVICE: return "device error";
+    case OKM_E_COMM: return "communication error";
+    case OKM_E_ARG: return "invalid argument";
+    case OKM_E_OVERFLOW: return "capacity exceeded";
+    case OKM_E_IO: return "i/o error";
+    case OKM_E_PARSE: return "parse error";
+    case OKM_E_RECORD: return "record error";
+    case OKM_E_STATE: return "invalid state";
+    case OKM_E_FORMAT: return "format error";
+    }
+    return "unknown";
+}
+
+const char *okm_last_error(void) { return okm::g_last_error.c_str(); }
+
+int okm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+const char *okm_device_arch(int device) {
+    static thread_local char buf[64];
+    buf[0] = 0;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return buf;
+    }
+    std::snprintf(buf, sizeof(buf), "%s", p.gcnArchName);
+    char *colon = std::strchr(buf, ':');
+    if (colon) *colon = 0;
+    return buf;
+}
+
+okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint) {
+    (void)distinct_hint;
+    if (!out) return fail(OKM_E_ARG, "okm_create: out is NULL");
+    *out = nullptr;
+    if (k == 0 || k > 32)
+        return fail(OKM_E_INVALID_K, "Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and 32.");
+    if (mode != OKM_MODE_COUNT && mode != OKM_MODE_SET) return fail(OKM_E_ARG, "okm_create: bad mode");
+    std::string why;
+    if (!device_ok(device, &why)) return fail(OKM_E_DEVICE, why);
+    HIP_TRY(hipSetDevice(device));
+    okm_ctx *c = new okm_ctx();
+    c->device = device;
+    c->k = k;
+    c->mode = mode;
+    c->l1_bits = std::min<uint32_t>(10u, 2u * k);
+    c->nbins = 1u << c->l1_bits;
+    c->shift1 = 2u * k - c->l1_bits;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->flag, sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
+    }
+    *out = c;
+    return OKM_OK;
+}
+
+void okm_destroy(okm_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->timer.destroy();
+    c->pool.release_all();
+    if (c->HC) (void)hipFree(c->HC);
+    if (c->Hg) (void)hipFree(c->Hg);
+    if (c->cursor) (void)hipFree(c->cursor);
+    if (c->flag) (void)hipFree(c->flag);
+    if (c->staging) (void)hipFree(c->staging);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+okm_status okm_reset(okm_ctx *c) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    OKM_TRY(sync(c));
+    invalidate_result(c);
+    for (auto &r : c->runs) {
+        c->pool.put(r.keys);
+        c->pool.put(r.counts);
+    }
+    c->runs.clear();
+    c->info = okm_engine_info{};
+    return OKM_OK;
+}
+
+static bool is_ws(uint8_t ch) { return ch == ' ' || ch == '\t' || ch == '\r' || ch == '\n'; }
+
+okm_status okm_add_batch(okm_ctx *c, const uint8_t *seq, const uint64_t *offsets, uint64_t n_records,
+                         int normalized) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    if (n_records == 0) return OKM_OK;
+    if (!seq || !offsets) return fail(OKM_E_ARG, "okm_add_batch: null seq/offsets");
+    HIP_TRY(hipSetDevice(c->device));
+    const uint64_t total = offsets[n_records] - offsets[0];
+    OKM_TRY(sync(c));  // pinned buffer reuse
+    OKM_TRY(ensure_pinned(c, total + n_records + 16));
+    // device batch layout: whitespace-free records + separator
+    uint8_t *dst = c->pinned;
+    uint64_t o = 0;
+    for (uint64_t r = 0; r < n_records; ++r) {
+        const uint8_t *s = seq + offsets[r];
+        const uint64_t len = offsets[r + 1] - offsets[r];
+        if (normalized) {
+            std::memcpy(dst + o, s, len);
+            o += len;
+        } else {
+            for (uint64_t i = 0; i < len; ++i)
+                if (!is_ws(s[i])) dst[o++] = s[i];
+        }
+        dst[o++] = OKM_RECORD_SEPARATOR;
+    }
+    OKM_TRY(ensure_staging(c, o));
+    HIP_TRY(hipMemcpyAsync(c->staging, dst, o, hipMemcpyHostToDevice, c->stream));
+    invalidate_result(c);
+    return l1_batch(c, c->staging, o);
+}
+
+okm_status okm_add_batch_device(okm_ctx *c, const uint8_t *d_seq, uint64_t n_bytes) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    if (n_bytes == 0) return OKM_OK;
+    if (!d_seq) return fail(OKM_E_ARG, "okm_add_batch_device: null pointer");
+    HIP_TRY(hipSetDevice(c->device));
+    invalidate_result(c);
+    if ((reinterpret_cast<uintptr_t>(d_seq) & 15u) != 0) {
+        OKM_TRY(ensure_staging(c, n_bytes));
+        HIP_TRY(hipMemcpyAsync(c->staging, d_seq, n_bytes, hipMemcpyDeviceToDevice, c->stream));
+        return l1_batch(c, c->staging, n_bytes);
+    }
+    return l1_batch(c, d_seq, n_bytes);
+}
+
+okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64_t *d_counts, uint64_t n) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    if (n == 0) return OKM_OK;
+    if (!d_keys) return fail(OKM_E_ARG, "okm_add_pairs_device: null keys");
+    HIP_TRY(hipSetDevice(c->device));
+    invalidate_result(c);
+    // L1-partition the pairs with the generic pass (one segment, 2^l1 bins)
+    DevSeg s{};
+    s.keys = d_keys;
+    s.counts = d_counts;
+    s.len = n;
+    s.key_base = 0;
+    s.out_base = 0;
+    s.shift = c->shift1;
+    s.nlocal = c->nbins;
+    std::vector<DevChunk> chunks;
+    for (uint64_t o = 0; o < n; o += kChunkKeys) chunks.push_back(DevChunk{0, 0, o, std::min(kChunkKeys, n - o)});
+    DevSeg *d_seg;
+    DevChunk *d_chunks;
+    OKM_TRY(pool_get(c->pool, 1, &d_seg));
+    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    HIP_TRY(hipMemcpyAsync(d_seg, &s, sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)c->nbins));
+    OKM_TRY(ensure_hg(c, c->nbins));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, c->nbins * sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_part_hist(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->Hg);
+    c->timer.end(c->stream, "part_hist", 8.0 * (double)n);
+    HIP_TRY(hipGetLastError());
+    Run run;
+    OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
+    OKM_TRY(pool_get(c->pool, n, &run.keys));
+    OKM_TRY(pool_get(c->pool, n, &run.counts));
+    c->timer.begin(c->stream);
+    launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys, run.counts);
+    c->timer.end(c->stream, "part_scatter", 32.0 * (double)n);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(sync(c));
+    c->pool.put(d_seg);
+    c->pool.put(d_chunks);
+    c->runs.push_back(std::move(run));
+    return OKM_OK;
+}
+
+okm_status okm_add_pairs(okm_ctx *c, const uint64_t *keys, const uint64_t *counts, uint64_t n) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    if (n == 0) return OKM_OK;
+    if (!keys) return fail(OKM_E_ARG, "okm_add_pairs: null keys");
+    HIP_TRY(hipSetDevice(c->device));
+    uint64_t *dk = nullptr, *dc = nullptr;
+    OKM_TRY(pool_get(c->pool, n, &dk));
+    if (counts) OKM_TRY(pool_get(c->pool, n, &dc));
+    HIP_TRY(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (counts) HIP_TRY(hipMemcpyAsync(dc, counts, n * 8, hipMemcpyHostToDevice, c->stream));
+    okm_status s = okm_add_pairs_device(c, dk, dc, n);
+    c->pool.put(dk);
+    c->pool.put(dc);
+    return s;
+}
+
+okm_status okm_count(okm_ctx *c, uint64_t *n_distinct) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    OKM_TRY(do_count(c));
+    if (n_distinct) *n_distinct = c->n_res;
+    return OKM_OK;
+}
+
+okm_status okm_result_device(okm_ctx *c, const uint64_t **d_keys, const uint64_t **d_counts, uint64_t *n) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    OKM_TRY(okm_count(c, nullptr));
+    if (d_keys) *d_keys = c->res_keys;
+    if (d_counts) *d_counts = c->res_counts;
+    if (n) *n = c->n_res;
+    return OKM_OK;
+}
+
+okm_status okm_result_size(okm_ctx *c, uint64_t min_count, uint64_t *n) {
+    if (!c || !n) return fail(OKM_E_ARG, "null argument");
+    OKM_TRY(okm_count(c, nullptr));
+    if (min_count <= 1 || c->n_res == 0) {
+        *n = c->n_res;
+        return OKM_OK;
+    }
+    const uint32_t nb = filter_blocks(c->n_res);
+    unsigned long long *bc;
+    OKM_TRY(pool_get(c->pool, nb + 1, &bc));
+    HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
+    launch_filter_count(c->stream, c->res_counts, c->n_res, min_count, bc, nb);
+    std::vector<unsigned long long> h(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), bc, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    c->pool.put(bc);
+    uint64_t t = 0;
+    for (auto v : h) t += v;
+    *n = t;
+    return OKM_OK;
+}
+
+okm_status okm_fetch_counts(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint64_t *counts, uint64_t cap,
+                            uint64_t *n, int dst_on_device) {
+    if (!c || !n) return fail(OKM_E_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    OKM_TRY(okm_count(c, nullptr));
+    *n = 0;
+    if (c->n_res == 0) return OKM_OK;
+    const uint64_t *src_k = c->res_keys, *src_c = c->res_counts;
+    uint64_t m = c->n_res;
+    uint64_t *tk = nullptr, *tc = nullptr;
+    if (min_count > 1) {
+        const uint32_t nb = filter_blocks(c->n_res);
+        unsigned long long *bc, *bo, *tmp;
+        OKM_TRY(pool_get(c->pool, nb + 1, &bc));
+        OKM_TRY(pool_get(c->pool, nb + 1, &bo));
+        OKM_TRY(pool_get(c->pool, scan_tmp_elems(nb + 1), &tmp));
+        HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
+        launch_filter_count(c->stream, c->res_counts, c->n_res, min_count, bc, nb);
+        launch_exclusive_scan(c->stream, bc, bo, nb + 1, tmp);
+        unsigned long long tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, bo + nb, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
+        OKM_TRY(sync(c));
+        m = tot;
+        if (m > cap) {
+            c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+            return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
+        }
+        if (m) {
+            OKM_TRY(pool_get(c->pool, m, &tk));
+            OKM_TRY(pool_get(c->pool, m, &tc));
+            launch_filter_scatter(c->stream, c->res_keys, c->res_counts, c->n_res, min_count, bo, tk, tc);
+            HIP_TRY(hipGetLastError());
+        }
+        c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+        src_k = tk;
+        src_c = tc;
+    } else if (m > cap) {
+        return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
+    }
+    if (m) {
+        const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        if (keys) HIP_TRY(hipMemcpyAsync(keys, src_k, m * 8, kind, c->stream));
+        if (counts) HIP_TRY(hipMemcpyAsync(counts, src_c, m * 8, kind, c->stream));
+    }
+    OKM_TRY(sync(c));
+    if (tk) c->pool.put(tk);
+    if (tc) c->pool.put(tc);
+    *n = m;
+    return OKM_OK;
+}
+
+okm_status okm_finish_counts(okm_ctx *c, uint64_t min_count, uint64_t **keys, uint64_t **counts, uint64_t *n) {
+    if (!c || !keys || !n) return fail(OKM_E_ARG, "null argument");
+    *keys = nullptr;
+    if (counts) *counts = nullptr;
+    uint64_t m = 0;
+    OKM_TRY(okm_result_size(c, min_count, &m));
+    uint64_t *hk = (uint64_t *)std::malloc(std::max<uint64_t>(m, 1) * 8);
+    uint64_t *hc = counts ? (uint64_t *)std::malloc(std::max<uint64_t>(m, 1) * 8) : nullptr;
+    if (!hk || (counts && !hc)) {
+        std::free(hk);
+        std::free(hc);
+        return fail(OKM_E_NOMEM, "okm_finish_counts: host allocation");
+    }
+    okm_status s = okm_fetch_counts(c, min_count, hk, hc, m, n, 0);
+    if (s != OKM_OK) {
+        std::free(hk);
+        std::free(hc);
+        return s;
+    }
+    *keys = hk;
+    if (counts) *counts = hc;
+    return OKM_OK;
+}
+
+okm_status okm_finish_set(okm_ctx *c, uint64_t **keys, uint64_t *n) {
+    return okm_finish_counts(c, 1, keys, nullptr, n);
+}
+
+void okm_free_result(void *p) { std::free(p); }
+
+okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb, int device,
+                                     uint64_t *out) {
+    if (!out) return fail(OKM_E_ARG, "null out");
+    *out = 0;
+    if (na == 0 || nb == 0) return OKM_OK;
+    if (!a || !b) return fail(OKM_E_ARG, "null input");
+    std::string why;
+    if (!device_ok(device, &why)) return fail(OKM_E_DEVICE, why);
+    HIP_TRY(hipSetDevice(device));
+    uint64_t *da = nullptr, *db = nullptr;
+    unsigned long long *dout = nullptr;
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    okm_status status = OKM_OK;
+    do {
+        if (hipMalloc(&da, na * 8) != hipSuccess || hipMalloc(&db, nb * 8) != hipSuccess ||
+            hipMalloc(&dout, 8) != hipSuccess) {
+            status = fail(OKM_E_NOMEM, "okm_set_intersection_size: device allocation");
+            break;
+        }
+        // probe the smaller set into the larger (compare.rs:58)
+        const bool swap = na > nb;
+        const uint64_t *sa = swap ? b : a, *sb = swap ? a : b;
+        const uint64_t sna = swap ? nb : na, snb = swap ? na : nb;
+        if (hipMemcpyAsync(da, sa, sna * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(db, sb, snb * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemsetAsync(dout, 0, 8, st) != hipSuccess) {
+            status = fail(OKM_E_DEVICE, "okm_set_intersection_size: copy");
+            break;
+        }
+        launch_intersect_count(st, da, sna, db, snb, dout);
+        unsigned long long h = 0;
+        if (hipMemcpyAsync(&h, dout, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            status = fail(OKM_E_DEVICE, "okm_set_intersection_size: kernel");
+            break;
+        }
+        *out = h;
+    } while (0);
+    (void)hipGetLastError();
+    if (da) (void)hipFree(da);
+    if (db) (void)hipFree(db);
+    if (dout) (void)hipFree(dout);
+    (void)hipStreamDestroy(st);
+    return status;
+}
+
+okm_status okm_synchronize(okm_ctx *c) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    return sync(c);
+}
+
+okm_status okm_set_timing(okm_ctx *c, int enable) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    OKM_TRY(sync(c));
+    c->timer.on = enable != 0;
+    c->timer.reset();
+    return OKM_OK;
+}
+
+okm_status okm_kernel_stats(okm_ctx *c, okm_kernel_stat *stats, int cap, int *n) {
+    if (!c || !n) return fail(OKM_E_ARG, "null argument");
+    OKM_TRY(sync(c));
+    const int m = (int)c->timer.stats.size();
+    for (int i = 0; i < m && i < cap; ++i) {
+        stats[i] = c->timer.stats[i];
+        stats[i].name = c->timer.names[i].c_str();
+    }
+    *n = m;
+    return OKM_OK;
+}
+
+okm_status okm_engine_info_get(okm_ctx *c, okm_engine_info *info) {
+    if (!c || !info) return fail(OKM_E_ARG, "null argument");
+    *info = c->info;
+    info->device_bytes = c->pool.held + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    return OKM_OK;
+}
+
+okm_status okm_device_alloc(int device, uint64_t bytes, void **d_ptr) {
+    if (!d_ptr) return fail(OKM_E_ARG, "null out");
+    std::string why;
+    if (!device_ok(device, &why)) return fail(OKM_E_DEVICE, why);
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(d_ptr, bytes ? bytes : 1));
+    return OKM_OK;
+}
+
+okm_status okm_device_free(void *d_ptr) {
+    if (d_ptr) HIP_TRY(hipFree(d_ptr));
+    return OKM_OK;
+}
+
+okm_status okm_memcpy_h2d(void *d_dst, const void *src, uint64_t bytes) {
+    if (bytes) HIP_TRY(hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice));
+    return OKM_OK;
+}
+
+okm_status okm_memcpy_d2h(void *dst, const void *d_src, uint64_t bytes) {
+    if (bytes) HIP_TRY(hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost));
+    return OKM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// okm_internal.h — internal declarations shared by the library's translation
+// units (not part of the C ABI).
+#pragma once
+
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include <vector>
+
+#include "orion_kmer.h"
+
+namespace okm {
+
+// thread-local last error (okm_last_error)
+void set_error(const std::string &msg);
+okm_status fail(okm_status s, const std::string &msg);
+
+constexpr uint64_t kEmptyKey = ~0ull;  // never a canonical key
+
+// ----------------------------------------------------------------------------
+// Device-side launchers (okm_device.hip).  All take a hipStream_t as void*.
+// ----------------------------------------------------------------------------
+
+// A run of keys in device memory (optionally weighted).
+struct DevSeg {
+    const uint64_t *keys;
+    const uint64_t *counts;  // nullptr => every key weighs 1
+    uint64_t len;
+    uint64_t key_base;       // (key >> shift) - key_base = local bin in [0, nlocal)
+    uint32_t out_base;       // first output bin of this segment (compact numbering)
+    uint32_t shift;          // 64 => a single bin
+    uint32_t nlocal;         // bins this segment splits into (<= pass maximum)
+    uint32_t pad;
+};
+
+// One unit of partition-pass work: a slice of a segment.
+struct DevChunk {
+    uint32_t seg;
+    uint32_t pad;
+    uint64_t begin;
+    uint64_t len;
+};
+
+// One partition to count in LDS: segs[seg_begin, seg_begin + seg_count).
+struct DevItem {
+    uint32_t seg_begin;
+    uint32_t seg_count;
+    uint64_t out_off;        // where its sorted distinct entries go (scratch)
+};
+
+struct ExtractGeom {
+    uint64_t n;        // bytes in the batch
+    uint32_t k;
+    uint32_t shift;    // bin = key >> shift (64 => single bin)
+    uint32_t nbins;    // 1 << l1 bits
+    uint32_t nblocks;  // persistent blocks (chunks)
+    uint64_t chunk;    // window starts per block (multiple of the tile)
+};
+
+// L1: k-mer extraction from a batch, histogram by top key bits.
+void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g, uint32_t *HC,
+                         unsigned long long *Hg);
+// L1: k-mer extraction + scatter into key-range partitions (exact placement).
+void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
+                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys);
+
+// Generic key-range partition pass over a chunk list.  max_local bounds every
+// segment's nlocal; HC is nchunks x max_local.
+void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
+                      uint32_t max_local, uint32_t *HC, unsigned long long *Hg);
+void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks,
+                         uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
+                         unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts);
+uint32_t extract_tile();
+
+// Exclusive scan of n u64 values (in -> out, out may equal in); tmp >= scan_tmp_elems(n).
+size_t scan_tmp_elems(uint64_t n);
+void launch_exclusive_scan(void *stream, const unsigned long long *in, unsigned long long *out,
+                           uint64_t n, unsigned long long *tmp);
+
+// LDS counting of partitions; writes sorted distinct (key,count) at out_off and
+// n_out[item].  Returns the max distinct capacity per item.
+uint32_t count_item_capacity();
+void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
+                        uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
+                        unsigned long long *overflow);
+
+// Gather the per-item results into dense arrays given exclusive offsets.
+void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
+                          const unsigned long long *n_out, const unsigned long long *dense_off,
+                          const uint64_t *src_keys, const uint64_t *src_counts,
+                          uint64_t *dst_keys, uint64_t *dst_counts);
+
+// Filter (count >= min) with order preserved; flags/scan in tmp.
+void launch_filter_count(void *stream, const uint64_t *counts, uint64_t n, uint64_t min_count,
+                         unsigned long long *block_counts, uint32_t nblocks_hint);
+void launch_filter_scatter(void *stream, const uint64_t *keys, const uint64_t *counts, uint64_t n,
+                           uint64_t min_count, const unsigned long long *block_offsets,
+                           uint64_t *dst_keys, uint64_t *dst_counts);
+uint32_t filter_blocks(uint64_t n);
+
+// |A ∩ B| of sorted unique arrays (merge-path style binary search per element).
+void launch_intersect_count(void *stream, const uint64_t *a, uint64_t na, const uint64_t *b,
+                            uint64_t nb, unsigned long long *out);
+
+}  // namespace okm

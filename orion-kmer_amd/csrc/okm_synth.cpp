@@ -1,0 +1,105 @@
+// okm_synth.cpp — seeded synthetic reads for the benchmark and the tests
+// (reads sampled uniformly from a random genome, strand
+// 50/50, substitution errors, N bases).  Counter-based: every read is a pure
+// function of (seed, read index), so any thread count, any shard of read
+// indices and any machine produce identical bytes.
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "okm_internal.h"
+
+namespace okm {
+
+static inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Genome {
+    uint64_t seed = 0, len = 0;
+    std::vector<uint8_t> codes;  // one 2-bit code per byte
+};
+
+static std::mutex g_mu;
+static Genome g_genome;
+
+static const Genome &genome(uint64_t seed, uint64_t len) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_genome.seed == seed && g_genome.len == len && !g_genome.codes.empty()) return g_genome;
+    g_genome.seed = seed;
+    g_genome.len = len;
+    g_genome.codes.resize(len);
+    // 32 bases per splitmix64 draw
+    for (uint64_t i = 0; i < len; i += 32) {
+        uint64_t r = splitmix64(seed * 0xD1B54A32D192ED03ull + i / 32);
+        const uint64_t m = std::min<uint64_t>(32, len - i);
+        for (uint64_t j = 0; j < m; ++j) {
+            g_genome.codes[i + j] = (uint8_t)(r & 3);
+            r >>= 2;
+        }
+    }
+    return g_genome;
+}
+
+}  // namespace okm
+
+using namespace okm;
+
+extern "C" okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t seed, uint64_t first_read,
+                                      uint64_t n_reads, uint32_t read_len, double sub_rate, double n_rate,
+                                      uint8_t *out, int threads) {
+    if (!out || read_len == 0 || genome_len < read_len) return fail(OKM_E_ARG, "okm_synth_reads: bad arguments");
+    const Genome &G = genome(genome_seed, genome_len);
+    const uint8_t *g = G.codes.data();
+    const uint64_t npos = genome_len - read_len + 1;
+    // per-base draw: 32-bit uniform u; u < t_sub => substitution, t_sub <= u < t_sub + t_n => N
+    const uint64_t t_sub = (uint64_t)(sub_rate * 4294967296.0);
+    const uint64_t t_n = (uint64_t)(n_rate * 4294967296.0);
+    const size_t stride = (size_t)read_len + 1;
+    auto work = [&](uint64_t a, uint64_t b) {
+        for (uint64_t i = a; i < b; ++i) {
+            const uint64_t r = first_read + i;
+            const uint64_t h = splitmix64(seed ^ splitmix64(r));
+            const uint64_t pos = h % npos;
+            const bool rev = (splitmix64(h) >> 63) != 0;
+            uint8_t *o = out + i * stride;
+            uint64_t draw = 0;
+            for (uint32_t j = 0; j < read_len; ++j) {
+                if ((j & 1) == 0) draw = splitmix64(h + 0x632BE59BD9B4E019ull * (j + 1));
+                const uint64_t u = (j & 1) ? (draw >> 32) : (draw & 0xFFFFFFFFull);
+                uint32_t code = rev ? 3u - g[pos + read_len - 1 - j] : g[pos + j];
+                uint8_t ch;
+                if (u < t_sub) {
+                    code = (code + 1 + (uint32_t)(u % 3)) & 3u;
+                    ch = "ACGT"[code];
+                } else if (u < t_sub + t_n) {
+                    ch = 'N';
+                } else {
+                    ch = "ACGT"[code];
+                }
+                o[j] = ch;
+            }
+            o[read_len] = OKM_RECORD_SEPARATOR;
+        }
+    };
+    int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::min<uint64_t>((uint64_t)nt, std::max<uint64_t>(1, n_reads / 4096));
+    if (nt <= 1) {
+        work(0, n_reads);
+        return OKM_OK;
+    }
+    std::vector<std::thread> ts;
+    const uint64_t per = (n_reads + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const uint64_t a = std::min<uint64_t>(n_reads, t * per), b = std::min<uint64_t>(n_reads, a + per);
+        ts.emplace_back(work, a, b);
+    }
+    for (auto &t : ts) t.join();
+    return OKM_OK;
+}

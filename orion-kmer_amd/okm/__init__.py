@@ -1,0 +1,412 @@
+"""okm — Python host layer over the MI355X k-mer engine (liborion_kmer.so).
+
+Mirrors the reference's library surface (``orion_kmer::kmer`` pub fns,
+``kmer.rs:37-106``) and its ``count``/``build``/``compare`` drivers
+(``commands/count.rs:40-141``, ``build.rs:80-160``, ``compare.rs:29-97``) so
+tests read like the reference's own.  All compute goes through the C ABI; the
+engine itself is HIP on gfx950 and has no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_char_p, c_int, c_uint64, c_void_p
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import (OKM_E_DEVICE, OKM_E_INVALID_K, OKM_E_IO, OKM_E_PARSE, OKM_E_RECORD,
+                   OKM_MODE_COUNT, OKM_MODE_SET, OKM_OK, RECORD_SEPARATOR, OkmError, check)
+
+__all__ = [
+    "seq_to_u64", "u64_to_seq", "reverse_complement_u64", "canonical_u64",
+    "KmerCounter", "DeviceBuffer", "device_count", "device_arch", "pack_records",
+    "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads",
+    "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
+]
+
+
+def lib():
+    return _lib.load()
+
+
+# ---------------------------------------------------------------------------
+# kmer.rs pub fns (CPU parity surface)
+# ---------------------------------------------------------------------------
+
+def seq_to_u64(seq: bytes, k: int) -> Optional[int]:
+    """kmer.rs:37-57."""
+    out = c_uint64(0)
+    if k < 0 or k > 255:
+        return None
+    ok = lib().okm_seq_to_u64(bytes(seq), len(seq), k, byref(out))
+    return out.value if ok else None
+
+
+def u64_to_seq(v: int, k: int) -> bytes:
+    """kmer.rs:61-75 (raises ValueError where the reference panics)."""
+    if k <= 0 or k > 32:
+        raise ValueError(f"Invalid k-mer length for decoding: {k}")
+    buf = ctypes.create_string_buffer(k)
+    lib().okm_u64_to_seq(v, k, buf)
+    return buf.raw
+
+
+def reverse_complement_u64(v: int, k: int) -> int:
+    """kmer.rs:79-94 (raises ValueError where the reference panics)."""
+    if k <= 0 or k > 32:
+        raise ValueError(f"Invalid k-mer length for reverse complement: {k}")
+    return int(lib().okm_reverse_complement_u64(v, k))
+
+
+def canonical_u64(v: int, k: int) -> int:
+    """kmer.rs:99-106."""
+    if k <= 0 or k > 32:
+        raise ValueError(f"Invalid k-mer length for reverse complement: {k}")
+    return int(lib().okm_canonical_u64(v, k))
+
+
+# ---------------------------------------------------------------------------
+# device
+# ---------------------------------------------------------------------------
+
+def device_count() -> int:
+    return int(lib().okm_device_count())
+
+
+def device_arch(device: int = 0) -> str:
+    return (lib().okm_device_arch(device) or b"").decode()
+
+
+class DeviceBuffer:
+    """Raw device allocation owned by Python (for device-resident batches)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.ptr = c_void_p()
+        self.nbytes = int(nbytes)
+        check(lib().okm_device_alloc(device, self.nbytes, byref(self.ptr)), "okm_device_alloc")
+
+    def upload(self, host: np.ndarray) -> None:
+        host = np.ascontiguousarray(host)
+        assert host.nbytes <= self.nbytes
+        check(lib().okm_memcpy_h2d(self.ptr, host.ctypes.data, host.nbytes), "okm_memcpy_h2d")
+
+    def download(self, host: np.ndarray) -> None:
+        assert host.flags.c_contiguous and host.nbytes <= self.nbytes
+        check(lib().okm_memcpy_d2h(host.ctypes.data, self.ptr, host.nbytes), "okm_memcpy_d2h")
+
+    @property
+    def address(self) -> int:
+        return int(self.ptr.value or 0)
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().okm_device_free(self.ptr)
+            self.ptr = c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# record batches
+# ---------------------------------------------------------------------------
+
+def pack_records(seqs: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """(bytes, offsets[n+1]) for okm_add_batch."""
+    offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    if seqs:
+        offs[1:] = np.cumsum([len(s) for s in seqs], dtype=np.uint64)
+    data = np.frombuffer(b"".join(seqs), dtype=np.uint8) if seqs else np.zeros(0, np.uint8)
+    return data.copy(), offs
+
+
+def parse_fastx(data: bytes) -> List[bytes]:
+    """Normalised sequences of a FASTA/FASTQ buffer (needletail semantics)."""
+    seq = c_void_p()
+    off = c_void_p()
+    n = c_uint64()
+    check(lib().okm_parse_buffer(data, len(data), byref(seq), byref(off), byref(n)), "okm_parse_buffer")
+    try:
+        offs = np.ctypeslib.as_array(ctypes.cast(off, POINTER(c_uint64)), shape=(n.value + 1,)).copy()
+        total = int(offs[-1])
+        raw = ctypes.string_at(seq, total) if total else b""
+        return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n.value)]
+    finally:
+        lib().okm_free_result(seq)
+        lib().okm_free_result(off)
+
+
+def read_fastx_file(path: str, decompress_by_extension: bool = True) -> List[bytes]:
+    """All normalised records of a file via the C reader (count: True, build: False)."""
+    r = c_void_p()
+    check(lib().okm_reader_open(byref(r), path.encode(), 1 if decompress_by_extension else 0),
+          f"okm_reader_open({path})")
+    out: List[bytes] = []
+    try:
+        while True:
+            seq = c_void_p()
+            off = c_void_p()
+            n = c_uint64()
+            check(lib().okm_reader_next(r, 64 << 20, byref(seq), byref(off), byref(n)), "okm_reader_next")
+            if n.value == 0:
+                break
+            offs = np.ctypeslib.as_array(ctypes.cast(off, POINTER(c_uint64)), shape=(n.value + 1,)).copy()
+            raw = ctypes.string_at(seq, int(offs[-1])) if int(offs[-1]) else b""
+            out.extend(raw[int(offs[i]):int(offs[i + 1])] for i in range(n.value))
+    finally:
+        lib().okm_reader_close(r)
+    return out
+
+
+def write_counts_tsv(path: str, k: int, keys: np.ndarray, counts: np.ndarray) -> None:
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    check(lib().okm_write_counts_tsv(path.encode(), k, keys.ctypes.data, counts.ctypes.data, len(keys)),
+          "okm_write_counts_tsv")
+
+
+def synth_reads(n_reads: int, read_len: int = 150, genome_len: int = 100_000_000, genome_seed: int = 2,
+                seed: int = 2, first_read: int = 0, sub_rate: float = 0.001, n_rate: float = 0.0001,
+                threads: int = 0) -> np.ndarray:
+    """Seeded reads in the device batch layout (each read + '\\n')."""
+    out = np.empty(n_reads * (read_len + 1), dtype=np.uint8)
+    check(lib().okm_synth_reads(genome_seed, genome_len, seed, first_read, n_reads, read_len, sub_rate,
+                                n_rate, out.ctypes.data, threads), "okm_synth_reads")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# counting context
+# ---------------------------------------------------------------------------
+
+class KmerCounter:
+    """The GPU replacement of ``DashMap<u64, AtomicUsize>`` (count.rs:48) and
+    of process_sequence_chunk (count.rs:23-38).  mode='set' mirrors build.rs's
+    DashSet."""
+
+    def __init__(self, k: int, mode: str = "count", device: int = 0, distinct_hint: int = 0):
+        self.k = k
+        self.ctx = c_void_p()
+        m = OKM_MODE_SET if mode == "set" else OKM_MODE_COUNT
+        check(lib().okm_create(byref(self.ctx), k, m, device, distinct_hint), "okm_create")
+
+    def close(self) -> None:
+        if self.ctx:
+            lib().okm_destroy(self.ctx)
+            self.ctx = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self) -> None:
+        check(lib().okm_reset(self.ctx), "okm_reset")
+
+    def add_records(self, seqs: Sequence[bytes], normalized: bool = False) -> None:
+        data, offs = pack_records(list(seqs))
+        self.add_batch(data, offs, normalized)
+
+    def add_batch(self, data: np.ndarray, offsets: np.ndarray, normalized: bool = False) -> None:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        if n <= 0:
+            return
+        check(lib().okm_add_batch(self.ctx, data.ctypes.data, offsets.ctypes.data, n, 1 if normalized else 0),
+              "okm_add_batch")
+
+    def add_device_batch(self, d_ptr: int, nbytes: int) -> None:
+        check(lib().okm_add_batch_device(self.ctx, c_void_p(d_ptr), nbytes), "okm_add_batch_device")
+
+    def add_pairs(self, keys: np.ndarray, counts: Optional[np.ndarray] = None) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        if counts is not None:
+            counts = np.ascontiguousarray(counts, dtype=np.uint64)
+        check(lib().okm_add_pairs(self.ctx, keys.ctypes.data,
+                                  counts.ctypes.data if counts is not None else None, len(keys)),
+              "okm_add_pairs")
+
+    def add_pairs_device(self, d_keys: int, d_counts: Optional[int], n: int) -> None:
+        check(lib().okm_add_pairs_device(self.ctx, c_void_p(d_keys), c_void_p(d_counts) if d_counts else None, n),
+              "okm_add_pairs_device")
+
+    def count(self) -> int:
+        n = c_uint64()
+        check(lib().okm_count(self.ctx, byref(n)), "okm_count")
+        return n.value
+
+    def result(self, min_count: int = 1) -> Tuple[np.ndarray, np.ndarray]:
+        """Sorted (keys, counts) with count >= min_count (count.rs:106-119)."""
+        n = c_uint64()
+        check(lib().okm_result_size(self.ctx, min_count, byref(n)), "okm_result_size")
+        keys = np.empty(n.value, dtype=np.uint64)
+        counts = np.empty(n.value, dtype=np.uint64)
+        got = c_uint64()
+        check(lib().okm_fetch_counts(self.ctx, min_count, keys.ctypes.data, counts.ctypes.data, n.value,
+                                     byref(got), 0), "okm_fetch_counts")
+        return keys[:got.value], counts[:got.value]
+
+    def result_device(self) -> Tuple[int, int, int]:
+        k = c_void_p()
+        c = c_void_p()
+        n = c_uint64()
+        check(lib().okm_result_device(self.ctx, byref(k), byref(c), byref(n)), "okm_result_device")
+        return int(k.value or 0), int(c.value or 0), n.value
+
+    def fetch_into_device(self, d_keys: int, d_counts: int, cap: int, min_count: int = 1) -> int:
+        got = c_uint64()
+        check(lib().okm_fetch_counts(self.ctx, min_count, c_void_p(d_keys), c_void_p(d_counts), cap, byref(got), 1),
+              "okm_fetch_counts(device)")
+        return got.value
+
+    def synchronize(self) -> None:
+        check(lib().okm_synchronize(self.ctx), "okm_synchronize")
+
+    def set_timing(self, on: bool) -> None:
+        check(lib().okm_set_timing(self.ctx, 1 if on else 0), "okm_set_timing")
+
+    def kernel_stats(self) -> Dict[str, Dict[str, float]]:
+        arr = (_lib.KernelStat * 64)()
+        n = c_int()
+        check(lib().okm_kernel_stats(self.ctx, arr, 64, byref(n)), "okm_kernel_stats")
+        out = {}
+        for i in range(min(n.value, 64)):
+            s = arr[i]
+            out[s.name.decode()] = {"launches": int(s.launches), "total_ms": float(s.total_ms),
+                                    "alg_bytes": float(s.alg_bytes)}
+        return out
+
+    def engine_info(self) -> Dict[str, int]:
+        info = _lib.EngineInfo()
+        check(lib().okm_engine_info_get(self.ctx, byref(info)), "okm_engine_info_get")
+        return {f: int(getattr(info, f)) for f, _ in _lib.EngineInfo._fields_}
+
+
+def set_intersection_size(a: np.ndarray, b: np.ndarray, device: int = 0) -> int:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = c_uint64()
+    check(lib().okm_set_intersection_size(a.ctypes.data, len(a), b.ctypes.data, len(b), device, byref(out)),
+          "okm_set_intersection_size")
+    return out.value
+
+
+# ---------------------------------------------------------------------------
+# KmerDbV2 (db_types.rs:7-14)
+# ---------------------------------------------------------------------------
+
+class KmerDb:
+    def __init__(self, k: int, references: Optional[Dict[str, np.ndarray]] = None):
+        self.k = k
+        self.references: Dict[str, np.ndarray] = dict(references or {})
+
+    def add_reference(self, name: str, keys: np.ndarray) -> None:
+        self.references[name] = np.asarray(keys, dtype=np.uint64)
+
+    def write(self, path: str) -> None:
+        db = c_void_p()
+        check(lib().okm_db_new(byref(db), self.k), "okm_db_new")
+        try:
+            for name, keys in self.references.items():
+                keys = np.ascontiguousarray(keys, dtype=np.uint64)
+                check(lib().okm_db_add_reference(db, name.encode(), keys.ctypes.data, len(keys)),
+                      "okm_db_add_reference")
+            check(lib().okm_db_write(db, path.encode()), "okm_db_write")
+        finally:
+            lib().okm_db_free(db)
+
+    @classmethod
+    def read(cls, path: str) -> "KmerDb":
+        db = c_void_p()
+        check(lib().okm_db_read(byref(db), path.encode()), "okm_db_read")
+        try:
+            out = cls(int(lib().okm_db_k(db)))
+            for i in range(int(lib().okm_db_num_references(db))):
+                name = c_char_p()
+                keys = c_void_p()
+                n = c_uint64()
+                check(lib().okm_db_reference(db, i, byref(name), byref(keys), byref(n)), "okm_db_reference")
+                arr = np.ctypeslib.as_array(ctypes.cast(keys, POINTER(c_uint64)), shape=(n.value,)).copy() \
+                    if n.value else np.zeros(0, np.uint64)
+                out.references[name.value.decode()] = arr
+            return out
+        finally:
+            lib().okm_db_free(db)
+
+    def get_all_kmers_unified(self) -> set:
+        s: set = set()
+        for v in self.references.values():
+            s.update(int(x) for x in v)
+        return s
+
+
+# ---------------------------------------------------------------------------
+# drivers (the reference's commands, through the engine)
+# ---------------------------------------------------------------------------
+
+def run_count(k: int, input_files: Iterable[str], output_file: Optional[str] = None, min_count: int = 1,
+              device: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """count.rs:40-141: every file in order into one table, filter, sort, TSV."""
+    if k == 0 or k > 32:
+        raise OkmError(OKM_E_INVALID_K, f"Invalid K-mer size: {k}. Must be between 1 and 32.")
+    with KmerCounter(k, "count", device) as c:
+        for p in input_files:
+            c.add_records(read_fastx_file(p, True), normalized=True)
+        keys, counts = c.result(min_count)
+    if output_file:
+        write_counts_tsv(output_file, k, keys, counts)
+    return keys, counts
+
+
+def run_build(k: int, genome_files: Iterable[str], output_file: Optional[str] = None,
+              device: int = 0) -> KmerDb:
+    """build.rs:80-160: per-file canonical k-mer sets under the basename."""
+    if k == 0 or k > 32:
+        raise OkmError(OKM_E_INVALID_K, f"Invalid K-mer size: {k}. Must be between 1 and 32.")
+    db = KmerDb(k)
+    with KmerCounter(k, "set", device) as c:
+        for p in genome_files:
+            c.reset()
+            c.add_records(read_fastx_file(p, False), normalized=True)
+            keys, _ = c.result(1)
+            db.add_reference(os.path.basename(p) or p, keys)
+    if output_file:
+        db.write(output_file)
+    return db
+
+
+def run_compare(db1: KmerDb, db2: KmerDb, device: int = 0) -> Dict[str, object]:
+    """compare.rs:29-97 on the device (union per DB, |A∩B|, Jaccard)."""
+    if db1.k != db2.k:
+        raise OkmError(OKM_E_INVALID_K, "K-mer databases have incompatible k-mer sizes (overall comparison): "
+                                        f"{db1.k} vs {db2.k}")
+
+    def unified(db: KmerDb) -> np.ndarray:
+        arrs = [v for v in db.references.values() if len(v)]
+        if not arrs:
+            return np.zeros(0, np.uint64)
+        with KmerCounter(db.k, "set", device) as c:
+            for v in arrs:
+                c.add_pairs(v)
+            return c.result(1)[0]
+
+    a, b = unified(db1), unified(db2)
+    inter = set_intersection_size(a, b, device) if len(a) and len(b) else 0
+    union = len(a) + len(b) - inter
+    return {"kmer_size": db1.k, "db1_total_unique_kmers_across_references": len(a),
+            "db2_total_unique_kmers_across_references": len(b), "intersection_size": inter,
+            "union_size": union, "jaccard_index": 0.0 if union == 0 else inter / union}

@@ -1,0 +1,142 @@
+"""ctypes binding of liborion_kmer.so (include/orion_kmer.h).
+
+The shared library is built in-tree (``orion-kmer_amd/build/``) by
+``__graft_entry__.build()`` / ``make -C orion-kmer_amd``.  Loading fails
+loudly when it is missing: there is no Python or CPU fallback for the engine.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_size_t,
+                    c_uint8, c_uint32, c_uint64, c_void_p)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+AMD_DIR = os.path.dirname(PKG_DIR)
+BUILD_DIR = os.path.join(AMD_DIR, "build")
+LIB_PATH = os.path.join(BUILD_DIR, "liborion_kmer.so")
+CLI_PATH = os.path.join(BUILD_DIR, "orion-kmer")
+HEADER_PATH = os.path.join(os.path.dirname(AMD_DIR), "include", "orion_kmer.h")
+
+OKM_OK = 0
+OKM_E_INVALID_K = 1
+OKM_E_NOMEM = 2
+OKM_E_DEVICE = 3
+OKM_E_COMM = 4
+OKM_E_ARG = 5
+OKM_E_OVERFLOW = 6
+OKM_E_IO = 7
+OKM_E_PARSE = 8
+OKM_E_RECORD = 9
+OKM_E_STATE = 10
+OKM_E_FORMAT = 11
+
+OKM_MODE_COUNT = 0
+OKM_MODE_SET = 1
+RECORD_SEPARATOR = ord("\n")
+
+
+class OkmError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[{status}] {msg}")
+        self.status = status
+
+
+class KernelStat(Structure):
+    _fields_ = [("name", c_char_p), ("launches", c_uint64), ("total_ms", c_double),
+                ("alg_bytes", c_double)]
+
+
+class EngineInfo(Structure):
+    _fields_ = [("kmers", c_uint64), ("distinct", c_uint64), ("l1_bits", c_uint32),
+                ("l2_bits", c_uint32), ("levels", c_uint32), ("work_items", c_uint32),
+                ("max_partition", c_uint64), ("device_bytes", c_uint64)]
+
+
+_P64 = POINTER(c_uint64)
+_PP64 = POINTER(POINTER(c_uint64))
+
+# name -> (restype, argtypes)
+PROTOTYPES = {
+    "okm_abi_version": (c_int, []),
+    "okm_status_string": (c_char_p, [c_int]),
+    "okm_device_count": (c_int, []),
+    "okm_device_arch": (c_char_p, [c_int]),
+    "okm_last_error": (c_char_p, []),
+    "okm_create": (c_int, [POINTER(c_void_p), c_uint8, c_int, c_int, c_uint64]),
+    "okm_destroy": (None, [c_void_p]),
+    "okm_reset": (c_int, [c_void_p]),
+    "okm_add_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int]),
+    "okm_add_batch_device": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "okm_add_pairs_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
+    "okm_add_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
+    "okm_count": (c_int, [c_void_p, _P64]),
+    "okm_fetch_counts": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, _P64, c_int]),
+    "okm_result_size": (c_int, [c_void_p, c_uint64, _P64]),
+    "okm_finish_counts": (c_int, [c_void_p, c_uint64, _PP64, _PP64, _P64]),
+    "okm_finish_set": (c_int, [c_void_p, _PP64, _P64]),
+    "okm_free_result": (None, [c_void_p]),
+    "okm_result_device": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), _P64]),
+    "okm_set_intersection_size": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_int, _P64]),
+    "okm_synchronize": (c_int, [c_void_p]),
+    "okm_set_timing": (c_int, [c_void_p, c_int]),
+    "okm_kernel_stats": (c_int, [c_void_p, POINTER(KernelStat), c_int, POINTER(c_int)]),
+    "okm_engine_info_get": (c_int, [c_void_p, POINTER(EngineInfo)]),
+    "okm_device_alloc": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),
+    "okm_device_free": (c_int, [c_void_p]),
+    "okm_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "okm_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "okm_seq_to_u64": (c_int, [c_char_p, c_size_t, c_uint8, _P64]),
+    "okm_u64_to_seq": (c_int, [c_uint64, c_uint8, POINTER(c_char)]),
+    "okm_reverse_complement_u64": (c_uint64, [c_uint64, c_uint8]),
+    "okm_canonical_u64": (c_uint64, [c_uint64, c_uint8]),
+    "okm_reader_open": (c_int, [POINTER(c_void_p), c_char_p, c_int]),
+    "okm_reader_next": (c_int, [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_void_p), _P64]),
+    "okm_reader_records": (c_uint64, [c_void_p]),
+    "okm_reader_close": (None, [c_void_p]),
+    "okm_parse_buffer": (c_int, [c_char_p, c_uint64, POINTER(c_void_p), POINTER(c_void_p), _P64]),
+    "okm_write_counts_tsv": (c_int, [c_char_p, c_uint8, c_void_p, c_void_p, c_uint64]),
+    "okm_write_file": (c_int, [c_char_p, c_char_p, c_uint64]),
+    "okm_read_file": (c_int, [c_char_p, c_int, POINTER(c_void_p), _P64]),
+    "okm_db_new": (c_int, [POINTER(c_void_p), c_uint8]),
+    "okm_db_add_reference": (c_int, [c_void_p, c_char_p, c_void_p, c_uint64]),
+    "okm_db_write": (c_int, [c_void_p, c_char_p]),
+    "okm_db_read": (c_int, [POINTER(c_void_p), c_char_p]),
+    "okm_db_k": (c_uint8, [c_void_p]),
+    "okm_db_num_references": (c_uint64, [c_void_p]),
+    "okm_db_reference": (c_int, [c_void_p, c_uint64, POINTER(c_char_p), POINTER(c_void_p), _P64]),
+    "okm_db_free": (None, [c_void_p]),
+    "okm_synth_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
+                                c_double, c_void_p, c_int]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load liborion_kmer.so (RTLD_GLOBAL, so a HIP runtime it brings in is the
+    one every later HIP user in the process binds to)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OkmError(OKM_E_DEVICE, f"{LIB_PATH} is missing: build it with "
+                                     f"`python -c 'import __graft_entry__ as g; g.build()'` "
+                                     f"or `make -C orion-kmer_amd` (there is no fallback)")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return (load().okm_last_error() or b"").decode(errors="replace")
+
+
+def check(status: int, what: str = "") -> None:
+    if status != OKM_OK:
+        raise OkmError(status, f"{what}: {last_error()}" if what else last_error())

@@ -1,0 +1,138 @@
+"""Owner-partitioned merge of per-GPU count tables.
+
+Reads shard naturally across GPUs (count.rs:23-38 is per record), so every
+rank counts its own shard with no communication.  The only exchange step
+is the merge:
+
+  1. each rank holds its local table, sorted by key (okm_count's output);
+  2. a 2^B-bin histogram of the top key bits is summed over ranks
+     (all_reduce) and cut into contiguous, count-balanced key ranges, one per
+     rank (value-range ownership: canonical k-mers are skewed ~7:5:3:1 by
+     first base, so equal-width ranges would not balance);
+  3. every rank's sorted table splits into contiguous per-owner slices
+     (searchsorted on the range boundaries) and one all_to_all_single moves
+     sizes, then one moves keys and one moves counts;
+  4. each owner adds the received (key, count) runs into a fresh counter
+     (weights add, exactly the AtomicUsize fetch_add of count.rs:31-34) and
+     re-counts, giving its range sorted.
+
+The global table is the concatenation of the owners' ranges in rank order,
+so no final merge is needed.  The same code runs over gloo with CPU tensors
+(tests) and over RCCL ("nccl") with device tensors (bench.py on MI355X).
+"""
+
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HIST_BITS = 16
+
+MergeFn = Callable[[torch.Tensor, torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]
+
+
+def key_bins(keys: torch.Tensor, k: int, bits: int) -> torch.Tensor:
+    """Top `bits` bits of the 2k-bit keys (int64 view of u64 keys)."""
+    shift = 2 * k - bits
+    b = keys >> shift if shift > 0 else keys
+    return b & ((1 << bits) - 1)
+
+
+def hist_bits(k: int) -> int:
+    return min(HIST_BITS, 2 * k)
+
+
+def local_histogram(keys: torch.Tensor, k: int) -> torch.Tensor:
+    bits = hist_bits(k)
+    if keys.numel() == 0:
+        return torch.zeros(1 << bits, dtype=torch.int64, device=keys.device)
+    return torch.bincount(key_bins(keys, k, bits), minlength=1 << bits).to(torch.int64)
+
+
+def owner_ranges(hist: np.ndarray, world: int) -> List[int]:
+    """Bin boundaries b_0=0 <= b_1 <= ... <= b_world=len(hist): rank r owns
+    bins [b_r, b_{r+1}); cuts at the cumulative count closest to r/world."""
+    cum = np.cumsum(hist, dtype=np.float64)
+    total = cum[-1] if len(cum) else 0.0
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        b = int(np.searchsorted(cum, target, side="left")) + 1
+        b = max(bounds[-1], min(b, len(hist)))
+        bounds.append(b)
+    bounds.append(len(hist))
+    return bounds
+
+
+def _order_view(keys: torch.Tensor, k: int) -> torch.Tensor:
+    """int64 values whose signed order equals the keys' unsigned order."""
+    if k < 32:
+        return keys
+    return keys ^ torch.tensor(-(1 << 63), dtype=torch.int64, device=keys.device)
+
+
+def exchange(keys: torch.Tensor, counts: torch.Tensor, k: int,
+             group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor, List[int]]:
+    """Move every (key, count) of this rank's sorted table to the owner of its
+    key range; returns the received concatenated runs and the bin bounds."""
+    world = dist.get_world_size(group)
+    dev = keys.device
+    hist = local_histogram(keys, k)
+    dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    bounds = owner_ranges(hist.cpu().numpy(), world)
+    bits = hist_bits(k)
+    shift = 2 * k - bits
+    # key boundaries of the owners' ranges (first key of each range)
+    kb = []
+    for b in bounds[1:-1]:
+        v = b << shift
+        if v >= 1 << 63:
+            v -= 1 << 64
+        kb.append(v)
+    kb_t = torch.tensor(kb, dtype=torch.int64, device=dev)
+    cuts = torch.searchsorted(_order_view(keys, k), _order_view(kb_t, k), right=False) if world > 1 \
+        else torch.zeros(0, dtype=torch.int64, device=dev)
+    edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts,
+                       torch.tensor([keys.numel()], dtype=torch.int64, device=dev)])
+    send_sizes = (edges[1:] - edges[:-1]).to(torch.int64)
+    recv_sizes = torch.empty_like(send_sizes)
+    dist.all_to_all_single(recv_sizes, send_sizes, group=group)
+    ss = send_sizes.cpu().tolist()
+    rs = recv_sizes.cpu().tolist()
+    rk = torch.empty(sum(rs), dtype=torch.int64, device=dev)
+    rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rk, keys.contiguous(), rs, ss, group=group)
+    dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
+    return rk, rc, bounds
+
+
+def distributed_merge(keys: torch.Tensor, counts: torch.Tensor, k: int, merge: MergeFn,
+                      group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Steps 2-4 above; returns this rank's owned range of the global table."""
+    rk, rc, _ = exchange(keys, counts, k, group)
+    return merge(rk, rc)
+
+
+def gather_global(keys: torch.Tensor, counts: torch.Tensor,
+                  group: Optional[dist.ProcessGroup] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate every owner's range in rank order on every rank (tests and
+    small outputs only; a CLI writes each range in order instead)."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    mx = int(max(int(x.item()) for x in ns))
+    pk = torch.zeros(mx, dtype=torch.int64, device=keys.device)
+    pc = torch.zeros(mx, dtype=torch.int64, device=keys.device)
+    pk[:keys.numel()] = keys
+    pc[:counts.numel()] = counts
+    gk = [torch.empty_like(pk) for _ in range(world)]
+    gc = [torch.empty_like(pc) for _ in range(world)]
+    dist.all_gather(gk, pk, group=group)
+    dist.all_gather(gc, pc, group=group)
+    ok = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gk, ns)]).view(np.uint64)
+    oc = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gc, ns)]).view(np.uint64)
+    return ok, oc

@@ -1,0 +1,336 @@
+"""Parity of the HIP engine (through the C ABI) with the oracle.
+
+- golden cases (reference test contents, reference fixture files,
+  restatement-defined edge cases): byte-identical TSV / sets / JSON, via the
+  Python host layer and via the orion-kmer CLI;
+- seeded random batches at MB scale: exact (key, count) equality with the C
+  restatement (oracle/okm_oracle.c);
+- full BASELINE-size batches: size-independent properties (sum of counts ==
+  valid windows, strictly sorted unique keys, every key canonical,
+  determinism, batch-split and pairs-merge invariance).
+Integer work: the bar is bit-exact.
+"""
+
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import okm
+import restate as R
+from conftest import case_file_bytes, materialize
+from okm import _lib
+from oracle import OracleCounter
+
+pytestmark = pytest.mark.gpu
+
+
+def counts_dict(keys, counts):
+    return dict(zip(keys.tolist(), counts.tolist()))
+
+
+def np_revcomp(v: np.ndarray, k: int) -> np.ndarray:
+    x = ~v.astype(np.uint64)
+    for s, m in ((2, 0x3333333333333333), (4, 0x0F0F0F0F0F0F0F0F), (8, 0x00FF00FF00FF00FF),
+                 (16, 0x0000FFFF0000FFFF)):
+        m = np.uint64(m)
+        x = ((x >> np.uint64(s)) & m) | ((x & m) << np.uint64(s))
+    x = (x >> np.uint64(32)) | (x << np.uint64(32))
+    return x >> np.uint64(64 - 2 * k)
+
+
+def valid_windows(batch: np.ndarray, k: int) -> int:
+    """Number of k-windows of all-ACGT bytes in a separator-joined batch
+    (count.rs:28-36: every window that seq_to_u64 accepts)."""
+    total = 0
+    step = 1 << 26
+    valid_set = np.zeros(256, bool)
+    valid_set[list(b"ACGTacgtUu")] = True
+    for o in range(0, len(batch), step):
+        seg = batch[o:o + step + k - 1]  # windows starting in [o, o + step)
+        if len(seg) < k:
+            break
+        bad = ~valid_set[seg]
+        c = np.concatenate([[0], np.cumsum(bad, dtype=np.int64)])
+        total += int(((c[k:] - c[:-k]) == 0).sum())
+    return total
+
+
+def assert_table_invariants(keys, counts, k):
+    assert keys.dtype == np.uint64
+    if len(keys) > 1:
+        assert (keys[1:] > keys[:-1]).all(), "keys must be strictly increasing (count.rs:119)"
+    assert (counts >= 1).all()
+    if k < 32:
+        assert (keys < np.uint64(1) << np.uint64(2 * k)).all()
+    assert (keys <= np_revcomp(keys, k)).all(), "every key must be canonical (kmer.rs:99-106)"
+
+
+# ---------------------------------------------------------------------------
+# goldens
+# ---------------------------------------------------------------------------
+
+def test_device_visible():
+    assert okm.device_count() >= 1
+    assert okm.device_arch(0) == "gfx950"
+
+
+def test_golden_count_cases_engine(golden_cases):
+    for c in golden_cases["count"]:
+        with okm.KmerCounter(c["k"]) as ctr:
+            for f in c["files"]:
+                raw = R.decompress_by_extension(f["name"], case_file_bytes(f))
+                ctr.add_records(okm.parse_fastx(raw), normalized=True)
+            keys, counts = ctr.result(c["min_count"])
+        tsv = "".join(f"{R.u64_to_seq(int(a), c['k']).decode()}\t{int(b)}\n" for a, b in zip(keys, counts))
+        assert tsv == c["expected_tsv"], c["name"]
+
+
+def test_golden_count_cases_raw_records(golden_cases):
+    """Un-normalised record bytes: the device LUT applies normalize()."""
+    for c in golden_cases["count"]:
+        recs = []
+        for f in c["files"]:
+            raw = R.decompress_by_extension(f["name"], case_file_bytes(f))
+            recs += [s for _, s in R.parse_fastx(raw)]
+        with okm.KmerCounter(c["k"]) as ctr:
+            ctr.add_records(recs, normalized=False)
+            keys, counts = ctr.result(c["min_count"])
+        exp = R.count_records(recs, c["k"])
+        exp = {a: b for a, b in exp.items() if b >= c["min_count"]}
+        assert counts_dict(keys, counts) == exp, c["name"]
+
+
+def test_golden_count_cases_cli(golden_cases, tmp_path):
+    for i, c in enumerate(golden_cases["count"]):
+        paths = materialize(tmp_path, c["files"], f"c{i}")
+        out = tmp_path / f"c{i}.tsv"
+        args = [_lib.CLI_PATH, "count", "-k", str(c["k"]), "-o", str(out), "-m", str(c["min_count"])]
+        for p in paths:
+            args += ["-i", p]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (c["name"], r.stderr)
+        assert out.read_text() == c["expected_tsv"], c["name"]
+
+
+@pytest.mark.parametrize("ext", ["gz", "xz", "zst"])
+def test_cli_compressed_output(golden_cases, tmp_path, ext):
+    c = golden_cases["count"][0]
+    paths = materialize(tmp_path, c["files"])
+    out = tmp_path / f"o.tsv.{ext}"
+    r = subprocess.run([_lib.CLI_PATH, "count", "-k", str(c["k"]), "-i", *paths, "-o", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert R.decompress_by_extension(str(out), out.read_bytes()).decode() == c["expected_tsv"]
+
+
+def test_cli_error_contexts(tmp_path):
+    empty = tmp_path / "empty.fa"
+    empty.write_bytes(b"")
+    r = subprocess.run([_lib.CLI_PATH, "count", "-k", "5", "-i", str(empty), "-o", str(tmp_path / "o")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and f"Failed to parse FASTA/Q content from: {empty}" in r.stderr
+    missing = tmp_path / "missing.fa"
+    r = subprocess.run([_lib.CLI_PATH, "count", "-k", "5", "-i", str(missing), "-o", str(tmp_path / "o")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and f"Failed to get input reader for file: {missing}" in r.stderr
+    bad = tmp_path / "bad.fq"
+    bad.write_bytes(b"@r\nACGT\n+\nII\n")
+    r = subprocess.run([_lib.CLI_PATH, "count", "-k", "3", "-i", str(bad), "-o", str(tmp_path / "o")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and f"Error reading record from {bad}" in r.stderr
+
+
+def test_golden_build_cases_cli(golden_cases, tmp_path):
+    for i, c in enumerate(golden_cases["build"]):
+        paths = materialize(tmp_path, c["files"], f"b{i}")
+        out = tmp_path / f"b{i}.db"
+        args = [_lib.CLI_PATH, "build", "-k", str(c["k"]), "-o", str(out)]
+        for p in paths:
+            args += ["-g", p]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (c["name"], r.stderr)
+        db = okm.KmerDb.read(str(out))
+        assert db.k == c["k"]
+        assert {n: v.tolist() for n, v in db.references.items()} == c["expected"], c["name"]
+
+
+def test_golden_compare_cases_cli(golden_cases, tmp_path):
+    for i, c in enumerate(golden_cases["compare"]):
+        dbs = []
+        for j, (k, files) in enumerate(((c["k1"], c["files1"]), (c["k2"], c["files2"]))):
+            paths = materialize(tmp_path, files, f"m{i}_{j}")
+            out = tmp_path / f"m{i}_{j}.db"
+            args = [_lib.CLI_PATH, "build", "-k", str(k), "-o", str(out)]
+            for p in paths:
+                args += ["-g", p]
+            assert subprocess.run(args, capture_output=True, timeout=120).returncode == 0
+            dbs.append(str(out))
+        js = tmp_path / f"m{i}.json"
+        r = subprocess.run([_lib.CLI_PATH, "compare", "--db1", dbs[0], "--db2", dbs[1], "-o", str(js)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (c["name"], r.stderr)
+        exp = c["expected_json"].replace('"DB1"', json.dumps(dbs[0])).replace('"DB2"', json.dumps(dbs[1]))
+        assert js.read_text() == exp, c["name"]
+
+
+def test_compare_k_mismatch_cli(tmp_path):
+    a = tmp_path / "a.fa"
+    a.write_text(">s\nACGTACGT\n")
+    for k in (3, 4):
+        subprocess.run([_lib.CLI_PATH, "build", "-k", str(k), "-g", str(a), "-o", str(tmp_path / f"k{k}.db")],
+                       check=True, capture_output=True, timeout=120)
+    r = subprocess.run([_lib.CLI_PATH, "compare", "--db1", str(tmp_path / "k3.db"), "--db2", str(tmp_path / "k4.db"),
+                        "-o", str(tmp_path / "x.json")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1
+    assert "K-mer databases have incompatible k-mer sizes (overall comparison): 3 vs 4" in r.stderr
+
+
+# ---------------------------------------------------------------------------
+# seeded random batches vs the C oracle (exact)
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("k,n_reads,read_len,genome", [
+    (31, 40_000, 150, 2_000_000), (21, 40_000, 150, 500_000), (32, 20_000, 150, 1_000_000),
+    (15, 30_000, 100, 300_000), (5, 5_000, 150, 100_000), (1, 2_000, 50, 10_000), (2, 2_000, 50, 10_000),
+    (11, 20_000, 150, 50_000), (31, 2_000, 5_000, 1_000_000),
+])
+def test_random_vs_oracle(k, n_reads, read_len, genome):
+    batch = okm.synth_reads(n_reads, read_len, genome_len=genome, genome_seed=k, seed=100 + k,
+                            sub_rate=0.01, n_rate=0.001)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    with okm.KmerCounter(k) as ctr:
+        body = batch.reshape(n_reads, read_len + 1)[:, :read_len]
+        offs = np.arange(0, (n_reads + 1) * read_len, read_len, dtype=np.uint64)
+        ctr.add_batch(np.ascontiguousarray(body).reshape(-1), offs)
+        gk, gc = ctr.result(1)
+        info = ctr.engine_info()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["kmers"] == oc.windows
+
+
+def test_device_batch_matches_host_batch_and_alignment():
+    k = 25
+    batch = okm.synth_reads(30_000, 150, genome_len=400_000, seed=9, sub_rate=0.02)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    buf = okm.DeviceBuffer(len(batch) + 64)
+    padded = np.zeros(len(batch) + 64, np.uint8)
+    for off in (0, 3):  # 16-B aligned and unaligned device pointers
+        padded[off:off + len(batch)] = batch
+        buf.upload(padded)
+        with okm.KmerCounter(k) as ctr:
+            ctr.add_device_batch(buf.address + off, len(batch))
+            gk, gc = ctr.result(1)
+        assert np.array_equal(gk, ek) and np.array_equal(gc, ec), off
+    buf.free()
+
+
+def test_multi_batch_multi_run_and_min_count():
+    k = 27
+    batch = okm.synth_reads(60_000, 150, genome_len=300_000, seed=4)
+    recs = batch.reshape(60_000, 151)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    with okm.KmerCounter(k) as ctr:
+        for part in np.array_split(recs, 7):
+            body = np.ascontiguousarray(part[:, :150]).reshape(-1)
+            offs = np.arange(0, (len(part) + 1) * 150, 150, dtype=np.uint64)
+            ctr.add_batch(body, offs, normalized=True)
+        for m in (1, 2, 5, 40):
+            gk, gc = ctr.result(m)
+            ek, ec = oc.result(m)
+            assert np.array_equal(gk, ek) and np.array_equal(gc, ec), m
+
+
+def test_pairs_merge_equals_whole():
+    k = 31
+    batch = okm.synth_reads(50_000, 150, genome_len=200_000, seed=8)
+    half = (50_000 // 2) * 151
+    parts = []
+    for sl in (batch[:half], batch[half:]):
+        with okm.KmerCounter(k) as c:
+            c.add_records([bytes(r) for r in sl.tobytes().split(b"\n") if r], normalized=True)
+            parts.append(c.result(1))
+    with okm.KmerCounter(k) as whole:
+        whole.add_records([bytes(r) for r in batch.tobytes().split(b"\n") if r], normalized=True)
+        wk, wc = whole.result(1)
+    with okm.KmerCounter(k) as m:
+        for pk, pc in parts:
+            m.add_pairs(pk, pc)
+        mk, mc = m.result(1)
+    assert np.array_equal(mk, wk) and np.array_equal(mc, wc)
+
+
+def test_hot_key_and_long_record():
+    # poly-A reads: every window is key 0 -> one partition holds everything and
+    # must be split down to a small remainder (multi-level path)
+    k = 31
+    recs = [b"A" * 150] * 20_000 + [b"ACGT" * 50_000]  # + one 200 kb record
+    oc = OracleCounter(k)
+    oc.add_records(recs)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records(recs)
+        gk, gc = ctr.result(1)
+        info = ctr.engine_info()
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["levels"] >= 2
+
+
+def test_empty_inputs():
+    with okm.KmerCounter(21) as ctr:
+        ctr.add_records([])
+        ctr.add_records([b"", b"ACG", b"NNNNNNNNNNNNNNNNNNNNNNNNNNNNNN"])
+        assert ctr.count() == 0
+        k, c = ctr.result(1)
+        assert len(k) == 0 and len(c) == 0
+    with okm.KmerCounter(5, "set") as ctr:
+        assert ctr.count() == 0
+
+
+def test_set_intersection():
+    rng = np.random.default_rng(3)
+    a = np.unique(rng.integers(0, 1 << 40, 200_000, dtype=np.uint64))
+    b = np.unique(np.concatenate([a[::3], rng.integers(0, 1 << 40, 100_000, dtype=np.uint64)]))
+    assert okm.set_intersection_size(a, b) == len(np.intersect1d(a, b))
+    assert okm.set_intersection_size(a, np.zeros(0, np.uint64)) == 0
+
+
+# ---------------------------------------------------------------------------
+# BASELINE-size properties (configs[1]: 1 GiB FASTQ-equivalent, k=31)
+# ---------------------------------------------------------------------------
+
+def test_full_size_properties():
+    k = 31
+    n_reads = 3_355_443
+    batch = okm.synth_reads(n_reads, 150, genome_len=100_000_000, genome_seed=2, seed=2)
+    buf = okm.DeviceBuffer(len(batch))
+    buf.upload(batch)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_device_batch(buf.address, len(batch))
+        n = ctr.count()
+        keys, counts = ctr.result(1)
+        info = ctr.engine_info()
+        ctr.reset()
+        ctr.add_device_batch(buf.address, len(batch))
+        k2, c2 = ctr.result(1)
+    buf.free()
+    assert n == len(keys) and info["distinct"] == n
+    assert int(counts.sum()) == valid_windows(batch, k) == info["kmers"]
+    assert_table_invariants(keys, counts, k)
+    assert np.array_equal(keys, k2) and np.array_equal(counts, c2), "determinism"
+    # exact parity on a prefix sample against the oracle
+    m = 150_000
+    oc = OracleCounter(k)
+    oc.add_separated(batch[:m * 151])
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records([bytes(r) for r in batch[:m * 151].tobytes().split(b"\n") if r], normalized=True)
+        gk, gc = ctr.result(1)
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)

@@ -1,0 +1,201 @@
+"""C-ABI library on the host (no GPU compute): every symbol in
+include/orion_kmer.h is exported; the CPU parts of the boundary (codec parity
+surface, FASTA/FASTQ record source, output codecs, KmerDbV2, synthetic reads)
+match the oracle; and the engine refuses to run without a device."""
+
+import gzip
+import lzma
+import os
+import random
+import re
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import okm
+import restate as R
+from conftest import GOLDEN, case_file_bytes, has_gpu
+from okm import _lib
+
+
+def header_symbols():
+    with open(_lib.HEADER_PATH) as fh:
+        txt = fh.read()
+    return sorted(set(re.findall(r"\b(okm_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 45
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the ctypes prototypes cover the whole header
+    assert set(syms) == set(_lib.PROTOTYPES), set(syms) ^ set(_lib.PROTOTYPES)
+    assert lib.okm_abi_version() == 1
+
+
+def test_cli_links_only_the_c_abi():
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.CLI_PATH], capture_output=True, text=True).stdout
+    used = set(re.findall(r"\b(okm_[a-z0-9_]+)\b", out))
+    assert used and used <= set(header_symbols())
+
+
+def test_codec_kats(reference_expectations):
+    for c in reference_expectations["seq_to_u64"]:
+        assert okm.seq_to_u64(c["seq"].encode(), c["k"]) == c["value"], c["src"]
+    for c in reference_expectations["u64_to_seq"]:
+        assert okm.u64_to_seq(c["value"], c["k"]).decode() == c["seq"], c["src"]
+    for c in reference_expectations["reverse_complement"]:
+        k = len(c["seq"])
+        assert okm.reverse_complement_u64(okm.seq_to_u64(c["seq"].encode(), k), k) == \
+            okm.seq_to_u64(c["rc"].encode(), k)
+    for c in reference_expectations["canonical"]:
+        k = len(c["seq"])
+        assert okm.canonical_u64(okm.seq_to_u64(c["seq"].encode(), k), k) == okm.seq_to_u64(c["canon"].encode(), k)
+    for bad in (0, 33):
+        with pytest.raises(ValueError):
+            okm.u64_to_seq(0, bad)
+        with pytest.raises(ValueError):
+            okm.reverse_complement_u64(0, bad)
+
+
+def test_codec_random_vs_restate():
+    rng = random.Random(3)
+    for _ in range(5000):
+        k = rng.randint(1, 32)
+        v = rng.getrandbits(2 * k)
+        assert okm.reverse_complement_u64(v, k) == R.reverse_complement_u64(v, k)
+        assert okm.canonical_u64(v, k) == R.canonical_u64(v, k)
+        assert okm.u64_to_seq(v, k) == R.u64_to_seq(v, k)
+        s = bytes(rng.choice(b"ACGTacgtNX") for _ in range(k))
+        assert okm.seq_to_u64(s, k) == R.seq_to_u64(s, k)
+
+
+def test_parse_buffer_matches_restate(golden_cases):
+    for c in golden_cases["count"]:
+        for f in c["files"]:
+            raw = R.decompress_by_extension(f["name"], case_file_bytes(f))
+            exp = [R.normalize(s) for _, s in R.parse_fastx(raw)]
+            assert okm.parse_fastx(raw) == exp, (c["name"], f["name"])
+
+
+def test_parse_errors():
+    for bad in (b"", b"This is not fasta content\nACGT", b"ACGT\n"):
+        with pytest.raises(okm.OkmError) as ei:
+            okm.parse_fastx(bad)
+        assert ei.value.status == _lib.OKM_E_PARSE
+    for bad in (b"@r\nACGT\n+\nIII\n", b"@r\nACGT\n+\n", b"@r\nACGT\nIIII\nIIII\n"):
+        with pytest.raises(okm.OkmError) as ei:
+            okm.parse_fastx(bad)
+        assert ei.value.status == _lib.OKM_E_RECORD
+    # headers-only FASTA is valid with empty records (build_tests.rs:239-251)
+    assert okm.parse_fastx(b">h1\n>h2\n") == [b"", b""]
+
+
+def test_reader_fixture_files(reference_expectations):
+    fx = reference_expectations["fixture_files"]
+    d = os.path.join(GOLDEN, "data")
+    for ext in ("gz", "xz", "zst"):
+        for base in ("test_input1.fasta", "test_input2.fastq"):
+            path = os.path.join(d, f"{base}.{ext}")
+            exp = [R.normalize(s) for _, s in R.parse_fastx(fx[base].encode())]
+            assert okm.read_fastx_file(path, True) == exp
+            if ext != "zst":  # build path: needletail sniffs gz/xz magic itself
+                assert okm.read_fastx_file(path, False) == exp
+    # needletail 0.5.1 has no zstd: the raw (build) reader rejects .zst content
+    with pytest.raises(okm.OkmError):
+        okm.read_fastx_file(os.path.join(d, "test_input1.fasta.zst"), False)
+
+
+def test_reader_missing_file():
+    with pytest.raises(okm.OkmError) as ei:
+        okm.read_fastx_file("/nonexistent/file.fa")
+    assert ei.value.status == _lib.OKM_E_IO
+
+
+@pytest.mark.parametrize("ext", ["tsv", "gz", "xz", "zst", "zstd", "GZ"])
+def test_tsv_writer_and_output_codecs(tmp_path, ext):
+    rng = np.random.default_rng(1)
+    k = 21
+    keys = np.sort(rng.integers(0, 1 << 42, 1000, dtype=np.uint64))
+    counts = rng.integers(1, 10 ** 12, 1000, dtype=np.uint64)
+    p = str(tmp_path / f"out.{ext}")
+    okm.write_counts_tsv(p, k, keys, counts)
+    raw = open(p, "rb").read()
+    e = ext.lower()
+    if e == "gz":
+        raw = gzip.decompress(raw)
+    elif e == "xz":
+        raw = lzma.decompress(raw)
+    elif e in ("zst", "zstd"):
+        raw = R._zstd_decompress(raw)
+    exp = "".join(f"{R.u64_to_seq(int(a), k).decode()}\t{int(b)}\n" for a, b in zip(keys, counts))
+    assert raw.decode() == exp
+
+
+def test_empty_tsv(tmp_path):
+    p = str(tmp_path / "e.tsv")
+    okm.write_counts_tsv(p, 5, np.zeros(0, np.uint64), np.zeros(0, np.uint64))
+    assert open(p, "rb").read() == b""
+
+
+def test_kmerdb_roundtrip_and_bincode_layout(tmp_path):
+    db = okm.KmerDb(4)
+    db.add_reference("a.fa", np.array([1, 5, 9], np.uint64))
+    db.add_reference("b.fa", np.array([], np.uint64))
+    db.add_reference("a.fa", np.array([2, 3], np.uint64))  # overwrite (db_types.rs:38-40)
+    p = str(tmp_path / "x.db")
+    db.write(p)
+    raw = open(p, "rb").read()
+    # bincode 1.3 default: u8 k, u64 len-prefixed map/string/set, LE fixed ints
+    exp = bytes([4]) + struct.pack("<Q", 2)
+    exp += struct.pack("<Q", 4) + b"a.fa" + struct.pack("<Q", 2) + struct.pack("<QQ", 2, 3)
+    exp += struct.pack("<Q", 4) + b"b.fa" + struct.pack("<Q", 0)
+    assert raw == exp
+    back = okm.KmerDb.read(p)
+    assert back.k == 4 and list(back.references) == ["a.fa", "b.fa"]
+    assert back.references["a.fa"].tolist() == [2, 3]
+    for ext in ("gz", "xz", "zst"):
+        q = str(tmp_path / f"x.db.{ext}")
+        db.write(q)
+        assert okm.KmerDb.read(q).references["a.fa"].tolist() == [2, 3]
+    open(str(tmp_path / "bad.db"), "wb").write(raw[:10])
+    with pytest.raises(okm.OkmError) as ei:
+        okm.KmerDb.read(str(tmp_path / "bad.db"))
+    assert ei.value.status == _lib.OKM_E_FORMAT
+
+
+def test_synth_reads_deterministic_and_shardable():
+    a = okm.synth_reads(5000, 150, genome_len=1_000_000, threads=1)
+    b = okm.synth_reads(5000, 150, genome_len=1_000_000, threads=8)
+    assert np.array_equal(a, b)
+    c = okm.synth_reads(2000, 150, genome_len=1_000_000, first_read=3000, threads=3)
+    assert np.array_equal(a[3000 * 151:], c)
+    recs = a.reshape(5000, 151)
+    assert (recs[:, 150] == ord("\n")).all()
+    body = recs[:, :150]
+    assert set(np.unique(body).tolist()) <= set(b"ACGTN")
+    # error rates near the requested ones (0.1 % substitutions, 0.01 % N)
+    n_frac = (body == ord("N")).mean()
+    assert 0.00002 < n_frac < 0.0005
+
+
+@pytest.mark.skipif(has_gpu(), reason="a HIP device is visible")
+def test_engine_fails_loudly_without_device():
+    with pytest.raises(okm.OkmError) as ei:
+        okm.KmerCounter(21)
+    assert ei.value.status == _lib.OKM_E_DEVICE
+    assert "no CPU fallback" in str(ei.value)
+    with pytest.raises(okm.OkmError):
+        okm.set_intersection_size(np.array([1], np.uint64), np.array([1], np.uint64))
+
+
+def test_invalid_k_rejected_before_device():
+    for k in (0, 33):
+        with pytest.raises(okm.OkmError) as ei:
+            okm.KmerCounter(k)
+        assert ei.value.status == _lib.OKM_E_INVALID_K
+        assert f"Invalid K-mer size: {k}. Must be between 1 and 32." in str(ei.value)

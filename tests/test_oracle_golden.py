@@ -1,0 +1,158 @@
+"""Pin the oracle: the Python and C restatements against the reference's own
+test expectations (tests/golden/reference_expectations.json, transcribed from
+orion-kmer/src/kmer.rs:108-341 and orion-kmer/tests/*.rs) and against the
+committed goldens (tests/golden/cases.json).  CPU only."""
+
+import random
+
+import numpy as np
+import pytest
+
+import restate as R
+from conftest import case_file_bytes
+from oracle import OracleCounter, load as oracle_load
+
+
+def test_restate_codec_kats(reference_expectations):
+    E = reference_expectations
+    for c in E["seq_to_u64"]:
+        assert R.seq_to_u64(c["seq"].encode(), c["k"]) == c["value"], c["src"]
+    for c in E["u64_to_seq"]:
+        assert R.u64_to_seq(c["value"], c["k"]).decode() == c["seq"], c["src"]
+    for c in E["reverse_complement"]:
+        k = len(c["seq"])
+        assert R.reverse_complement_u64(R.seq_to_u64(c["seq"].encode(), k), k) == R.seq_to_u64(c["rc"].encode(), k)
+    for c in E["canonical"]:
+        k = len(c["seq"])
+        assert R.canonical_u64(R.seq_to_u64(c["seq"].encode(), k), k) == R.seq_to_u64(c["canon"].encode(), k)
+    with pytest.raises(ValueError):
+        R.u64_to_seq(0, 0)
+    with pytest.raises(ValueError):
+        R.u64_to_seq(0, 33)
+    with pytest.raises(ValueError):
+        R.reverse_complement_u64(0, 0)
+    with pytest.raises(ValueError):
+        R.u64_to_dna_base(4)
+
+
+def test_restate_count_matches_reference_tests(reference_expectations):
+    for c in reference_expectations["count"]:
+        tsv = R.run_count_bytes([(n, t.encode()) for n, t in c["files"]], c["k"], c["min_count"])
+        assert sorted(tsv.strip().splitlines()) == c["expected_sorted_lines"], c["src"]
+
+
+def test_restate_count_errors(reference_expectations):
+    for c in reference_expectations["count_errors"]:
+        with pytest.raises(R.OracleError) as ei:
+            R.run_count_bytes([("x.fa", b">a\nACGT\n")], c["k"])
+        assert c["stderr_contains"] in str(ei.value)
+
+
+def test_restate_build_matches_reference_tests(reference_expectations):
+    for c in reference_expectations["build"]:
+        k = c["k"]
+        refs = R.build_sets([(n, t.encode()) for n, t in c["files"]], k)
+        exp = {n: {R.canonical_u64(R.seq_to_u64(s.encode(), k), k) for s in v} for n, v in c["expected"].items()}
+        assert refs == exp, c["src"]
+        assert len(set().union(*refs.values())) == c["total_unique"]
+
+
+def test_restate_compare_matches_reference_tests(reference_expectations):
+    for c in reference_expectations["compare"]:
+        k = c["k"]
+        r1 = R.build_sets([(n, t.encode()) for n, t in c["db1"]], k)
+        r2 = R.build_sets([(n, t.encode()) for n, t in c["db2"]], k)
+        res = R.compare_sets(k, r1, k, r2)
+        assert res["db1_total_unique_kmers_across_references"] == c["db1_total"], c["src"]
+        assert res["db2_total_unique_kmers_across_references"] == c["db2_total"]
+        assert res["intersection_size"] == c["intersection"]
+        assert res["union_size"] == c["union"]
+        assert abs(res["jaccard_index"] - c["intersection"] / c["union"]) < 1e-12
+    for c in reference_expectations["compare_errors"]:
+        with pytest.raises(R.OracleError) as ei:
+            R.compare_sets(c["k1"], {}, c["k2"], {})
+        assert c["stderr_contains"] in str(ei.value)
+
+
+def test_fixture_files_decode_to_transcribed_bytes(reference_expectations):
+    fx = reference_expectations["fixture_files"]
+    for ext in ("gz", "xz", "zst"):
+        for base in ("test_input1.fasta", "test_input2.fastq"):
+            raw = case_file_bytes({"fixture": f"{base}.{ext}"})
+            assert R.decompress_by_extension(f"{base}.{ext}", raw).decode() == fx[base]
+
+
+def test_golden_cases_regenerate(golden_cases):
+    """cases.json is exactly what the pinned restatement produces."""
+    for c in golden_cases["count"]:
+        tsv = R.run_count_bytes([(f["name"], case_file_bytes(f)) for f in c["files"]], c["k"], c["min_count"])
+        assert tsv == c["expected_tsv"], c["name"]
+
+
+# ---------------------------------------------------------------------------
+# C restatement
+# ---------------------------------------------------------------------------
+
+def test_c_oracle_codec_kats(reference_expectations):
+    import ctypes
+    lib = oracle_load()
+    for c in reference_expectations["seq_to_u64"]:
+        out = ctypes.c_uint64()
+        ok = lib.oracle_seq_to_u64(c["seq"].encode(), len(c["seq"]), c["k"], ctypes.byref(out))
+        assert (out.value if ok else None) == c["value"], c["src"]
+    rng = random.Random(7)
+    for _ in range(2000):
+        k = rng.randint(1, 32)
+        v = rng.getrandbits(2 * k)
+        assert lib.oracle_reverse_complement_u64(v, k) == R.reverse_complement_u64(v, k)
+        assert lib.oracle_canonical_u64(v, k) == R.canonical_u64(v, k)
+
+
+def _records_of(files):
+    recs = []
+    for f in files:
+        data = R.decompress_by_extension(f["name"], case_file_bytes(f))
+        recs.extend(s for _, s in R.parse_fastx(data))
+    return recs
+
+
+def test_c_oracle_matches_goldens(golden_cases):
+    for c in golden_cases["count"]:
+        oc = OracleCounter(c["k"])
+        oc.add_records(_records_of(c["files"]), normalized=False)
+        keys, counts = oc.result(c["min_count"])
+        tsv = R.format_counts(dict(zip(keys.tolist(), counts.tolist())), c["k"], c["min_count"])
+        assert tsv == c["expected_tsv"], c["name"]
+
+
+def test_c_oracle_matches_restate_random():
+    rng = random.Random(99)
+    for trial in range(30):
+        k = rng.choice([1, 2, 3, 5, 8, 13, 21, 31, 32])
+        seqs = [bytes(rng.choice(b"ACGTacgtNNU-") for _ in range(rng.randint(0, 120))) for _ in range(rng.randint(1, 12))]
+        exp = R.count_records(seqs, k)
+        oc = OracleCounter(k)
+        oc.add_records(seqs)
+        keys, counts = oc.result(1)
+        assert dict(zip(keys.tolist(), counts.tolist())) == exp
+        assert oc.windows == sum(exp.values())
+
+
+def test_c_oracle_separated_layout_equals_records():
+    rng = random.Random(5)
+    seqs = [bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 60))) for _ in range(50)]
+    a = OracleCounter(11)
+    a.add_records(seqs)
+    b = OracleCounter(11)
+    b.add_separated(np.frombuffer(b"\n".join(seqs), dtype=np.uint8))
+    ka, ca = a.result()
+    kb, cb = b.result()
+    assert np.array_equal(ka, kb) and np.array_equal(ca, cb)
+
+
+def test_c_oracle_pairs_merge():
+    a = OracleCounter(7)
+    a.add_pairs(np.array([5, 3, 5], np.uint64), np.array([1, 2, 10], np.uint64))
+    k, c = a.result(1)
+    assert k.tolist() == [3, 5] and c.tolist() == [2, 11]
+    assert a.result(3)[0].tolist() == [5]
