@@ -688,9 +688,11 @@ okm_status okm_add_batch(okm_ctx *c, const uint8_t *seq, const uint64_t *offsets
                          int normalized) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     if (n_records == 0) return OKM_OK;
-    if (!seq || !offsets) return fail(OKM_E_ARG, "okm_add_batch: null seq/offsets");
-    HIP_TRY(hipSetDevice(c->device));
+    if (!offsets) return fail(OKM_E_ARG, "okm_add_batch: null offsets");
     const uint64_t total = offsets[n_records] - offsets[0];
+    if (total == 0) return OKM_OK;  // only empty records (e.g. header-only FASTA)
+    if (!seq) return fail(OKM_E_ARG, "okm_add_batch: null seq");
+    HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(sync(c));  // pinned buffer reuse
     OKM_TRY(ensure_pinned(c, total + n_records + 16));
     // device batch layout: whitespace-free records + separator
@@ -924,15 +926,15 @@ okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint6
     HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     okm_status status = OKM_OK;
     do {
-        if (hipMalloc(&da, na * 8) != hipSuccess || hipMalloc(&db, nb * 8) != hipSuccess ||
-            hipMalloc(&dout, 8) != hipSuccess) {
-            status = fail(OKM_E_NOMEM, "okm_set_intersection_size: device allocation");
-            break;
-        }
         // probe the smaller set into the larger (compare.rs:58)
         const bool swap = na > nb;
         const uint64_t *sa = swap ? b : a, *sb = swap ? a : b;
         const uint64_t sna = swap ? nb : na, snb = swap ? na : nb;
+        if (hipMalloc(&da, sna * 8) != hipSuccess || hipMalloc(&db, snb * 8) != hipSuccess ||
+            hipMalloc(&dout, 8) != hipSuccess) {
+            status = fail(OKM_E_NOMEM, "okm_set_intersection_size: device allocation");
+            break;
+        }
         if (hipMemcpyAsync(da, sa, sna * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemcpyAsync(db, sb, snb * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemsetAsync(dout, 0, 8, st) != hipSuccess) {
