@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,6 +64,11 @@ struct DevPool {
     okm_status get(size_t bytes, void **out) {
         bytes = (bytes + 255) & ~size_t(255);
         if (bytes == 0) bytes = 256;
+        if (bytes > (64u << 20)) {  // big buffers: 1/16 size classes, so run-to-run size jitter reuses blocks
+            size_t g = 1;
+            while ((g << 5) <= bytes) g <<= 1;
+            bytes = (bytes + g - 1) & ~(g - 1);
+        }
         auto it = free_.lower_bound(bytes);
         if (it != free_.end() && it->first <= bytes * 2) {
             *out = it->second;
@@ -82,6 +88,8 @@ struct DevPool {
         size_[p] = bytes;
         held += bytes;
         *out = p;
+        if (getenv("OKM_PROFILE_HOST"))
+            fprintf(stderr, "[okm pool] hipMalloc %zu bytes (held %zu, free blocks %zu)\n", bytes, held, free_.size());
         return OKM_OK;
     }
     void put(void *p) {
@@ -113,6 +121,47 @@ static okm_status pool_get(DevPool &pool, size_t n, T **out) {
     *out = static_cast<T *>(p);
     return OKM_OK;
 }
+
+static bool debug_sync() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("OKM_DEBUG_SYNC");
+        v = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// OKM_PROFILE_HOST=1: wall time of host phases (incl. the syncs inside them),
+// printed to stderr by okm_count.
+struct HostProf {
+    bool on = false;
+    std::vector<std::pair<std::string, double>> acc;
+    std::chrono::steady_clock::time_point last;
+    HostProf() {
+        const char *e = getenv("OKM_PROFILE_HOST");
+        on = e && *e && *e != '0';
+        last = std::chrono::steady_clock::now();
+    }
+    void mark(const char *name) {
+        if (!on) return;
+        auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - last).count();
+        last = now;
+        for (auto &kv : acc)
+            if (kv.first == name) {
+                kv.second += ms;
+                return;
+            }
+        acc.emplace_back(name, ms);
+    }
+    void dump(const char *tag) {
+        if (!on) return;
+        fprintf(stderr, "[okm host %s]", tag);
+        for (auto &kv : acc) fprintf(stderr, " %s=%.3f", kv.first.c_str(), kv.second);
+        fprintf(stderr, "\n");
+        acc.clear();
+    }
+};
 
 // ---------------------------------------------------------------------------
 // HIP-event kernel timing (okm_set_timing / okm_kernel_stats)
@@ -154,6 +203,10 @@ struct KernelTimer {
         (void)hipEventRecord(cur_a, s);
     }
     void end(hipStream_t s, const char *name, double bytes) {
+        if (debug_sync()) {  // OKM_DEBUG_SYNC=1: serialise and name every kernel
+            hipError_t e = hipStreamSynchronize(s);
+            fprintf(stderr, "[okm] %s done: %s\n", name, hipGetErrorString(e));
+        }
         if (!on) return;
         hipEvent_t b = ev();
         (void)hipEventRecord(b, s);
@@ -204,6 +257,7 @@ struct okm_ctx {
     DevPool pool;
     std::vector<Run> runs;
     KernelTimer timer;
+    HostProf hprof;
 
     // small persistent scratch
     uint32_t *HC = nullptr;
@@ -297,6 +351,7 @@ static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &
 // OKM_RECORD_SEPARATOR, 16-byte aligned).
 static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     if (n == 0) return OKM_OK;
+    c->hprof.mark("idle");
     const uint64_t tile = extract_tile();
     uint64_t tiles = (n + tile - 1) / tile;
     uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, 2048);
@@ -314,6 +369,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
 
     Run run;
     OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
+    c->hprof.mark("l1.hist+sync");
     const uint64_t total = run.off.back();
     if (total == 0) return OKM_OK;
     OKM_TRY(pool_get(c->pool, total, &run.keys));
@@ -323,6 +379,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     HIP_TRY(hipGetLastError());
     c->runs.push_back(std::move(run));
     c->info.kmers += total;
+    c->hprof.mark("l1.scatter_launch");
     return OKM_OK;
 }
 
@@ -335,30 +392,39 @@ struct Part {
 
 static const uint64_t kChunkKeys = 1u << 16;
 
-// One partition pass: split every part in `todo` by its own number of bits.
-// Segments of the parts are read; the result is a new level array whose bins
-// become the children (in key order) of each part.
-static okm_status split_round(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts,
-                              const std::vector<uint32_t> &todo, const std::vector<uint32_t> &bits,
-                              bool weighted, std::vector<void *> &level_bufs) {
+// Output of one partition pass: a level array whose bins are the children, in
+// key order, of the parts that took part (offsets stay on the device).
+struct Level {
+    unsigned long long *d_offs = nullptr;  // nout + 1 exclusive offsets (line padded)
+    uint64_t *lk = nullptr, *lc = nullptr;
+    uint32_t nout = 0;
+    uint64_t padded = 0;
+    std::vector<uint32_t> out_base;        // first output bin of each participating part
+};
+
+// One partition pass: split every part in `todo` by its own number of bits
+// (0 bits = gather the part as one bin).
+static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, const std::vector<Part> &parts,
+                               const std::vector<uint32_t> &todo, const std::vector<uint32_t> &bits, bool weighted,
+                               std::vector<void *> &level_bufs, Level &L) {
     const uint32_t twok = 2u * c->k;
     std::vector<DevSeg> psegs;      // pass segments (one per input segment)
     std::vector<DevChunk> chunks;
-    std::vector<uint32_t> out_base(todo.size());
+    L.out_base.assign(todo.size(), 0);
     uint32_t nout = 0, max_local = 1;
     uint64_t total = 0;
     for (size_t t = 0; t < todo.size(); ++t) {
         const Part &p = parts[todo[t]];
         const uint32_t b = bits[t];
         const uint32_t nl = 1u << b;
-        out_base[t] = nout;
+        L.out_base[t] = nout;
         nout += nl;
         max_local = std::max(max_local, nl);
         for (uint32_t s = 0; s < p.seg_count; ++s) {
             DevSeg d = segtab[p.seg_begin + s];
             d.shift = twok - p.consumed - b;
             d.key_base = p.prefix << b;
-            d.out_base = out_base[t];
+            d.out_base = L.out_base[t];
             d.nlocal = nl;
             const uint32_t sid = (uint32_t)psegs.size();
             psegs.push_back(d);
@@ -367,52 +433,73 @@ static okm_status split_round(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
         }
         total += p.len;
     }
+    L.nout = nout;
     OKM_TRY(ensure_hc(c, chunks.size() * (size_t)max_local));
-    OKM_TRY(ensure_hg(c, nout));
+    OKM_TRY(ensure_hg(c, nout + 1));
     DevSeg *d_segs;
     DevChunk *d_chunks;
+    unsigned long long *scan_tmp;
     OKM_TRY(pool_get(c->pool, psegs.size(), &d_segs));
     OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
     level_bufs.push_back(d_segs);
     level_bufs.push_back(d_chunks);
+    level_bufs.push_back(L.d_offs);
+    level_bufs.push_back(scan_tmp);
     HIP_TRY(hipMemcpyAsync(d_segs, psegs.data(), psegs.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(c->Hg, 0, nout * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
     const double kb = weighted ? 16.0 : 8.0;
     c->timer.begin(c->stream);
     launch_part_hist(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->Hg);
     c->timer.end(c->stream, "part_hist", 8.0 * (double)total);
     HIP_TRY(hipGetLastError());
-    std::vector<uint64_t> off;
-    OKM_TRY(hist_to_offsets(c, nout, off));
-    uint64_t *lk = nullptr, *lc = nullptr;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &lk));
-    level_bufs.push_back(lk);
+    // bin offsets on the device; only the total crosses to the host
+    launch_exclusive_scan(c->stream, c->Hg, L.d_offs, (uint64_t)nout + 1, scan_tmp);
+    HIP_TRY(hipMemcpyAsync(c->cursor, L.d_offs, (size_t)nout * sizeof(unsigned long long), hipMemcpyDeviceToDevice, c->stream));
+    unsigned long long padded = 0;
+    HIP_TRY(hipMemcpyAsync(&padded, L.d_offs + nout, sizeof(padded), hipMemcpyDeviceToHost, c->stream));
+    c->hprof.mark("split.prep+hist_launch");
+    OKM_TRY(sync(c));
+    c->hprof.mark("split.hist_sync");
+    L.padded = padded;  // bins start on 128-B lines (okm_partition.hip)
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1), &L.lk));
+    level_bufs.push_back(L.lk);
     if (weighted) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &lc));
-        level_bufs.push_back(lc);
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1), &L.lc));
+        level_bufs.push_back(L.lc);
     }
     c->timer.begin(c->stream);
-    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->cursor, lk, lc);
+    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->cursor, L.lk, L.lc);
     c->timer.end(c->stream, "part_scatter", 2.0 * kb * (double)total);
     HIP_TRY(hipGetLastError());
     c->info.levels += 1;
+    return OKM_OK;
+}
 
-    // replace each split part by its children
+// Host view of a level: replace each participating part by its non-empty
+// children (rare path: a child is still too big for one LDS item).
+static okm_status split_children_host(okm_ctx *c, const Level &L, std::vector<DevSeg> &segtab,
+                                      std::vector<Part> &parts, const std::vector<uint32_t> &todo,
+                                      const std::vector<uint32_t> &bits) {
+    std::vector<uint64_t> off((size_t)L.nout + 1);
+    HIP_TRY(hipMemcpyAsync(off.data(), L.d_offs, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
     std::vector<Part> next;
-    next.reserve(parts.size() + nout);
+    next.reserve(parts.size() + L.nout);
     size_t t = 0;
     for (uint32_t i = 0; i < parts.size(); ++i) {
         if (t < todo.size() && todo[t] == i) {
             const Part &p = parts[i];
             const uint32_t b = bits[t];
             for (uint32_t l = 0; l < (1u << b); ++l) {
-                const uint32_t ob = out_base[t] + l;
+                const uint32_t ob = L.out_base[t] + l;
                 const uint64_t len = off[ob + 1] - off[ob];
                 if (!len) continue;
                 DevSeg d{};
-                d.keys = lk + off[ob];
-                d.counts = lc ? lc + off[ob] : nullptr;
+                d.keys = L.lk + off[ob];
+                d.counts = L.lc ? L.lc + off[ob] : nullptr;
                 d.len = len;
                 d.shift = 64;
                 d.nlocal = 1;
@@ -442,15 +529,21 @@ static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
     invalidate_result(c);
     const uint32_t twok = 2u * c->k;
-    const uint64_t cap = count_item_capacity();        // distinct per item
-    const uint32_t capbits = log2_floor(cap);          // 2^capbits <= cap
-    const uint64_t target = cap * 3 / 4;               // aim below cap after a split
+    const uint64_t cap = count_item_capacity();        // distinct keys per LDS pass
+    const uint32_t capbits = log2_floor(cap);          // 2^capbits <= cap: never needs a 2nd pass
+    // Items are sized in instances, assuming some duplication (reads cover
+    // the genome several times); an item with more distinct keys than one
+    // pass holds is still counted exactly, in several passes (okm_count.hip).
+    const uint64_t item_max = cap * 2;                 // split parts larger than this
+    const uint64_t target = item_max * 3 / 4;          // aim below it after a split
+    bool weighted = false;
+    for (auto &r : c->runs) weighted |= (r.counts != nullptr);
+    const uint32_t maxb = log2_floor(part_max_bins(weighted));  // bits one pass can split
+    c->hprof.mark("pre_count");
 
     // initial parts: the L1 bins, each a list of per-run segments
     std::vector<DevSeg> segtab;
     std::vector<Part> parts;
-    bool weighted = false;
-    for (auto &r : c->runs) weighted |= (r.counts != nullptr);
     for (uint32_t b = 0; b < c->nbins; ++b) {
         Part p{(uint32_t)segtab.size(), 0, 0, b, c->l1_bits};
         for (auto &r : c->runs) {
@@ -471,38 +564,107 @@ static okm_status do_count(okm_ctx *c) {
     c->info.l1_bits = c->l1_bits;
     c->info.l2_bits = 0;
     c->info.levels = 0;
+    c->info.max_partition = 0;
 
-    // split rounds until every part is countable in one LDS table
+    auto plan = [&](uint32_t i) -> uint32_t {  // bits to split part i by (0: keep)
+        const Part &p = parts[i];
+        const uint32_t rem = twok - p.consumed;
+        if (p.len <= item_max || rem <= capbits) return 0;
+        uint32_t b = 1;
+        while (b < maxb && (p.len >> b) > target) ++b;
+        return std::min(b, rem);
+    };
+
     std::vector<void *> level_bufs;
-    for (int round = 0; round < 64; ++round) {
+    DevItem *d_items = nullptr;
+    DevSeg *d_segs = nullptr;
+    uint32_t nitems = 0;
+    uint64_t out_total = 0, in_total = 0;
+    bool device_items = false;
+
+    // Round 0 on the device: every part takes part (0 bits = gathered as one
+    // bin), so the level's bins are the count work list in key order and are
+    // turned into items without the offsets ever reaching the host.
+    {
+        std::vector<uint32_t> all, bits;
+        bool any = false;
+        for (uint32_t i = 0; i < parts.size(); ++i) {
+            all.push_back(i);
+            bits.push_back(plan(i));
+            any |= bits.back() != 0;
+        }
+        if (any) {
+            c->info.l2_bits = *std::max_element(bits.begin(), bits.end());
+            c->hprof.mark("split.plan");
+            Level L;
+            OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L));
+            std::vector<DevParent> par(parts.size());
+            for (uint32_t i = 0; i < parts.size(); ++i) par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
+            DevParent *d_par;
+            unsigned long long *flags;
+            OKM_TRY(pool_get(c->pool, par.size(), &d_par));
+            OKM_TRY(pool_get(c->pool, 2, &flags));
+            OKM_TRY(pool_get(c->pool, L.nout, &d_items));
+            OKM_TRY(pool_get(c->pool, L.nout, &d_segs));
+            level_bufs.push_back(d_par);
+            level_bufs.push_back(flags);
+            HIP_TRY(hipMemcpyAsync(d_par, par.data(), par.size() * sizeof(DevParent), hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
+            launch_make_items(c->stream, L.d_offs, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc, d_items, d_segs,
+                              item_max, capbits, flags);
+            HIP_TRY(hipGetLastError());
+            unsigned long long hf[2];
+            HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
+            OKM_TRY(sync(c));
+            c->hprof.mark("split.round");
+            if (hf[0] == 0) {
+                device_items = true;
+                nitems = L.nout;
+                out_total = in_total = L.padded;
+                c->info.max_partition = hf[1];
+                if (hf[1] >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
+            } else {
+                c->pool.put(d_items);
+                c->pool.put(d_segs);
+                d_items = nullptr;
+                d_segs = nullptr;
+                OKM_TRY(split_children_host(c, L, segtab, parts, all, bits));
+            }
+        }
+    }
+
+    // Further rounds on the host view (only when a child is still too big:
+    // skewed or adversarial key distributions).
+    for (int round = 1; !device_items && round < 64; ++round) {
         std::vector<uint32_t> todo, bits;
         for (uint32_t i = 0; i < parts.size(); ++i) {
-            const Part &p = parts[i];
-            const uint32_t rem = twok - p.consumed;
-            if (p.len <= cap || rem <= capbits) continue;
-            uint32_t b = 1;
-            while (b < 12 && (p.len >> b) > target) ++b;
-            b = std::min(b, rem);
+            const uint32_t b = plan(i);
+            if (!b) continue;
             todo.push_back(i);
             bits.push_back(b);
         }
         if (todo.empty()) break;
-        if (round == 0) c->info.l2_bits = bits.empty() ? 0 : *std::max_element(bits.begin(), bits.end());
-        OKM_TRY(split_round(c, segtab, parts, todo, bits, weighted, level_bufs));
+        Level L;
+        OKM_TRY(split_launch(c, segtab, parts, todo, bits, weighted, level_bufs, L));
+        OKM_TRY(split_children_host(c, L, segtab, parts, todo, bits));
     }
 
-    // count every part in LDS
-    const uint32_t nitems = (uint32_t)parts.size();
-    c->info.work_items = nitems;
-    c->info.max_partition = 0;
-    std::vector<DevItem> items(nitems);
-    uint64_t out_total = 0, in_total = 0;
-    for (uint32_t i = 0; i < nitems; ++i) {
-        items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total};
-        out_total += std::min<uint64_t>(parts[i].len, cap);
-        in_total += parts[i].len;
-        c->info.max_partition = std::max(c->info.max_partition, parts[i].len);
+    std::vector<DevItem> items;
+    if (!device_items) {
+        nitems = (uint32_t)parts.size();
+        items.resize(nitems);
+        for (uint32_t i = 0; i < nitems; ++i) {
+            // distinct <= instances, and <= 2^remaining-bits
+            const uint32_t rem = twok - parts[i].consumed;
+            const uint64_t bound = rem >= 63 ? parts[i].len : std::min<uint64_t>(parts[i].len, 1ull << rem);
+            items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total, rem, 0};
+            out_total += bound;
+            in_total += parts[i].len;
+            c->info.max_partition = std::max(c->info.max_partition, parts[i].len);
+            if (parts[i].len >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
+        }
     }
+    c->info.work_items = nitems;
     if (nitems == 0) {
         for (void *p : level_bufs) c->pool.put(p);
         c->counted = true;
@@ -510,23 +672,27 @@ static okm_status do_count(okm_ctx *c) {
         c->info.distinct = 0;
         return OKM_OK;
     }
-    DevSeg *d_segs;
-    DevItem *d_items;
     uint64_t *sk, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
-    OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
-    OKM_TRY(pool_get(c->pool, nitems, &d_items));
-    OKM_TRY(pool_get(c->pool, out_total, &sk));
-    OKM_TRY(pool_get(c->pool, out_total, &sc));
+    if (!device_items) {
+        OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
+        OKM_TRY(pool_get(c->pool, nitems, &d_items));
+    }
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sk));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
-    HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_items, items.data(), nitems * sizeof(DevItem), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(c->flag, 0, sizeof(unsigned long long), c->stream));
+    c->hprof.mark("items.build");
+    if (!device_items) {
+        HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_items, items.data(), nitems * sizeof(DevItem), hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag);
+    c->hprof.mark("items.h2d");
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, weighted);
     c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
@@ -535,7 +701,8 @@ static okm_status do_count(okm_ctx *c) {
     HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
-    if (hv[1]) return fail(OKM_E_OVERFLOW, "LDS count table overflow (partition sizing invariant broken)");
+    c->hprof.mark("count+scan+sync");
+    if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     const uint64_t nd = hv[0];
     if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_keys));
@@ -556,6 +723,8 @@ static okm_status do_count(okm_ctx *c) {
     c->n_res = nd;
     c->info.distinct = nd;
     c->counted = true;
+    c->hprof.mark("compact+sync");
+    c->hprof.dump("count");
     return OKM_OK;
 }
 
@@ -639,11 +808,11 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->device = device;
     c->k = k;
     c->mode = mode;
-    c->l1_bits = std::min<uint32_t>(10u, 2u * k);
+    c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins()), 2u * k);
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->flag, sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess) {
         (void)hipGetLastError();
         delete c;
         return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
@@ -679,6 +848,7 @@ okm_status okm_reset(okm_ctx *c) {
     }
     c->runs.clear();
     c->info = okm_engine_info{};
+    c->hprof.mark("reset");
     return OKM_OK;
 }
 
@@ -762,8 +932,8 @@ okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64
     HIP_TRY(hipGetLastError());
     Run run;
     OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
-    OKM_TRY(pool_get(c->pool, n, &run.keys));
-    OKM_TRY(pool_get(c->pool, n, &run.counts));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
     c->timer.begin(c->stream);
     launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys, run.counts);
     c->timer.end(c->stream, "part_scatter", 32.0 * (double)n);

@@ -1,0 +1,179 @@
+// okm_extract.hip — L1 pass: batch bytes -> canonical k-mers -> key-range bins.
+//
+// Restates on the device:
+//   kmer.rs:12-20   dna_base_to_u64      -> base_code / base_valid (+ U/u->T of
+//                                          needletail normalize, count.rs:71)
+//   kmer.rs:37-57   seq_to_u64           -> rolling forward word `fwd`
+//   kmer.rs:79-94   reverse_complement   -> rolling `rc`
+//   kmer.rs:99-106  canonical_u64        -> min(fwd, rc)
+//   count.rs:23-38  window loop          -> scan_segment + valid-run counter
+//
+// Two kernels per batch.  extract_hist counts, per persistent block, the keys
+// of each bin (top l1 bits of the 2k-bit key); the host turns the totals into
+// bin offsets.  extract_scatter recomputes the k-mers (ALU is cheap next to
+// HBM) and places them exactly: each block owns one contiguous slice per bin
+// (claimed with one returning atomic per (block, bin)), and every 8192-window
+// tile is counting-sorted by bin in LDS first so that each bin's keys leave
+// the CU as one contiguous run (~256 B at 256 bins) instead of 8-byte
+// scattered stores (which cost 3.5x the bytes in HBM writes).
+#include "okm_dev_common.h"
+
+namespace okm {
+
+// Valid bytes after needletail normalize(false) + dna_base_to_u64:
+// A/a C/c G/g T/t U/u (kmer.rs:14-17; U->T is normalize's).  c & 0xDF folds
+// case and has exactly {X, X|0x20} as preimages of an upper-case letter X.
+__device__ __forceinline__ bool base_valid(uint32_t c) {
+    const uint32_t u = c & 0xDFu;
+    return (u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'U');
+}
+// A=0 C=1 G=2 T=3 (and U=3) for either case: ((c>>1) ^ (c>>2)) & 3.
+__device__ __forceinline__ uint32_t base_code(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
+
+__device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
+    return shift >= 64 ? 0u : (uint32_t)(key >> shift);
+}
+
+constexpr int kSeg = 32;           // window starts per thread
+constexpr int kLoad = kSeg + 32;   // bytes per thread: covers kSeg + k - 1 for k <= 32
+constexpr int kExtractBlock = 256;
+constexpr int kTile = kExtractBlock * kSeg;
+constexpr int kMaxL1Bins = 256;
+
+uint32_t extract_tile() { return (uint32_t)kTile; }
+uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
+
+// Walk the windows starting in [w0, w0 + kSeg) of a batch of n bytes.  Every
+// window whose k bytes are all valid is canonicalised and handed to emit().
+// Bytes at or beyond n read as 0 (invalid), so windows never run off the end;
+// record separators are invalid bytes, so windows never cross records.
+template <typename Emit>
+__device__ __forceinline__ void scan_segment(const uint8_t *__restrict__ seq, uint64_t n,
+                                             uint64_t w0, uint32_t k, Emit &&emit) {
+    uint32_t w[kLoad / 4];
+    if (w0 + kLoad <= n) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
+#pragma unroll
+        for (int q = 0; q < kLoad / 16; ++q) {
+            const uint4 v = p[q];
+            w[4 * q + 0] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kLoad / 4; ++q) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t idx = w0 + 4 * q + b;
+                const uint32_t c = idx < n ? (uint32_t)seq[idx] : 0u;
+                x |= c << (8 * b);
+            }
+            w[q] = x;
+        }
+    }
+    const uint64_t kmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1ull);
+    const uint32_t rcs = 2 * k - 2;
+    uint64_t fwd = 0, rc = 0;
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < kLoad - 1; ++i) {
+        const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+        const uint32_t code = base_code(c);
+        fwd = ((fwd << 2) | code) & kmask;                    // kmer.rs:51, rolled
+        rc = (rc >> 2) | ((uint64_t)(code ^ 3u) << rcs);     // kmer.rs:87-91, rolled
+        run = base_valid(c) ? run + 1 : 0;
+        const int start = i - (int)k + 1;
+        if (run >= k && start >= 0 && start < kSeg) emit(fwd < rc ? fwd : rc);  // kmer.rs:101
+    }
+}
+
+__global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq,
+                                                                ExtractGeom g,
+                                                                uint32_t *__restrict__ HC,
+                                                                ull *__restrict__ Hg) {
+    __shared__ uint32_t lh[kMaxL1Bins];
+    for (uint32_t b = threadIdx.x; b < g.nbins; b += kExtractBlock) lh[b] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
+    const uint32_t shift = g.shift;
+    for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
+        const uint64_t w0 = t0 + (uint64_t)threadIdx.x * kSeg;
+        if (w0 < end)
+            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) { atomicAdd(&lh[bin_of(key, shift)], 1u); });
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < g.nbins; b += kExtractBlock) {
+        const uint32_t h = lh[b];
+        HC[(uint64_t)blockIdx.x * g.nbins + b] = h;
+        if (h) atomicAdd(&Hg[b], (ull)h);
+    }
+}
+
+__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t *__restrict__ seq,
+                                                                   ExtractGeom g,
+                                                                   const uint32_t *__restrict__ HC,
+                                                                   ull *__restrict__ cursor,
+                                                                   uint64_t *__restrict__ out) {
+    __shared__ ull stage[kTile];
+    __shared__ ull gcur[kMaxL1Bins];     // this block's next output index per bin
+    __shared__ uint32_t hist[kMaxL1Bins];
+    __shared__ uint32_t lofs[kMaxL1Bins];  // tile-local start of each bin in `stage`
+    __shared__ uint32_t lcur[kMaxL1Bins];
+    __shared__ ull wsum[kExtractBlock / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t nb = g.nbins;
+    if (t < nb) {
+        const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
+        gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
+    const uint32_t shift = g.shift;
+    for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
+        if (t < nb) hist[t] = 0;
+        __syncthreads();
+        const uint64_t w0 = t0 + (uint64_t)t * kSeg;
+        if (w0 < end)
+            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) { atomicAdd(&hist[bin_of(key, shift)], 1u); });
+        __syncthreads();
+        ull tile_n;
+        const uint32_t my = t < nb ? hist[t] : 0u;
+        const uint32_t off = (uint32_t)block_excl_scan<kExtractBlock>(my, wsum, &tile_n);
+        if (t < nb) {
+            lofs[t] = off;
+            lcur[t] = off;
+        }
+        __syncthreads();
+        if (w0 < end)
+            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) {
+                stage[atomicAdd(&lcur[bin_of(key, shift)], 1u)] = key;
+            });
+        __syncthreads();
+        // each bin's keys are contiguous in `stage` and go to a contiguous run
+        for (uint32_t j = t; j < (uint32_t)tile_n; j += kExtractBlock) {
+            const ull key = stage[j];
+            const uint32_t b = bin_of(key, shift);
+            out[gcur[b] + (j - lofs[b])] = key;
+        }
+        __syncthreads();
+        if (t < nb) gcur[t] += hist[t];
+    }
+}
+
+void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g, uint32_t *HC,
+                         unsigned long long *Hg) {
+    hipLaunchKernelGGL(k_extract_hist, dim3(g.nblocks), dim3(kExtractBlock), 0, (hipStream_t)stream, seq, g,
+                       HC, Hg);
+}
+
+void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
+                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys) {
+    hipLaunchKernelGGL(k_extract_scatter, dim3(g.nblocks), dim3(kExtractBlock), 0, (hipStream_t)stream, seq,
+                       g, HC, cursor, out_keys);
+}
+
+}  // namespace okm

@@ -46,6 +46,8 @@ struct DevItem {
     uint32_t seg_begin;
     uint32_t seg_count;
     uint64_t out_off;        // where its sorted distinct entries go (scratch)
+    uint32_t rem_bits;       // key bits below the item's common prefix
+    uint32_t pad;
 };
 
 struct ExtractGeom {
@@ -72,18 +74,36 @@ void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunk
                          uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
                          unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts);
 uint32_t extract_tile();
+uint32_t extract_max_bins();
+uint32_t part_max_bins(bool weighted);
 
 // Exclusive scan of n u64 values (in -> out, out may equal in); tmp >= scan_tmp_elems(n).
 size_t scan_tmp_elems(uint64_t n);
 void launch_exclusive_scan(void *stream, const unsigned long long *in, unsigned long long *out,
                            uint64_t n, unsigned long long *tmp);
 
-// LDS counting of partitions; writes sorted distinct (key,count) at out_off and
-// n_out[item].  Returns the max distinct capacity per item.
+// LDS counting of partitions (okm_count.hip); writes sorted distinct
+// (key,count) at out_off and n_out[item].  ctl[0] = error word, ctl[1] = item
+// queue (both zeroed before the launch).  count_item_capacity() = distinct
+// keys one LDS pass holds (bigger items take several passes).
 uint32_t count_item_capacity();
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *overflow);
+                        unsigned long long *ctl, bool weighted);
+
+// A part that took part in a device-side split round: its children are the
+// output bins [out_base, out_base + nlocal) of the round.
+struct DevParent {
+    uint32_t out_base;
+    uint32_t rem;            // key bits below the children's common prefix
+};
+
+// One item (and one segment) per output bin of a split round, straight from
+// the device offsets (nout + 1 entries).  flags[0] += children that are still
+// too big for one item; flags[1] = max child length.
+void launch_make_items(void *stream, const unsigned long long *offs, uint32_t nout, const DevParent *parents,
+                       uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
+                       uint64_t item_max, uint32_t capbits, unsigned long long *flags);
 
 // Gather the per-item results into dense arrays given exclusive offsets.
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
