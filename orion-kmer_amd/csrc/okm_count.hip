@@ -5,34 +5,85 @@
 // blockIdx stride; an LDS-broadcast dynamic queue deadlocked under hipcc's
 // structuriser).
 //
-// The LDS table is ORDER-PRESERVING: an item is a contiguous key range, so a
-// key's home slot is the next kHomeBits bits of the key below the item's
-// common prefix (monotone in the key), collisions probe forward only and the
-// table has a kCap-slot tail instead of wrapping.  Every key then sits in the
-// maximal run of occupied slots ("cluster") that contains its home, and
-// clusters appear in key order.  After inserting, a key's rank in the sorted
-// output is
-//     (ordinal of its slot among occupied slots) - (its offset in its cluster)
-//   + (number of keys in its cluster that are smaller),
-// which costs a few LDS reads per key at the table's load (<= 50 % of the
-// home range): no sort network at all.
+// An item is a contiguous key range whose keys share all bits above its
+// `rem_bits` remaining bits.  Its "home" is the next kHomeBits bits (monotone in
+// the key), so homes are key sub-ranges in order.  Three modes:
 //
-// An item whose distinct keys exceed one pass's capacity (kCap) is processed
-// as 2, 4, ... sub-ranges of its remaining key bits, in key order, so any
-// item size is correct; the host sizes items so that this is rare.
+//  tag mode (rem_bits > kHomeBits, at most kCapI instances — the planner
+//  guarantees it): every home has a TAG slot.  One 64-bit LDS CAS per
+//  instance: the first key to reach a home claims the tag, and every instance
+//  of the tag key just adds to the home's packed counter.  At 4x-coverage
+//  reads ~88 % of instances end there (a home holds 0.3 distinct keys on
+//  average).  Only the other ("rest") instances are counting-sorted by home
+//  into LDS; each thread then owns 4 consecutive homes, insertion-sorts its
+//  (small) rest slice and emits, per home in order, the rest keys merged with
+//  the tag key.  Two block scans (rest offsets, distinct counts) place
+//  everything.  Per-thread loops run over REST instances only, which is what
+//  keeps the wave's slowest lane — that a divergent loop waits for — short.
+//
+//  full mode (fallback: more rest instances than the rest buffer holds, e.g.
+//  inputs whose keys are all distinct): all instances counting-sorted by home,
+//  per-thread insertion sort + run-length encoding over the same LDS.
+//
+//  dense mode (rem_bits <= kHomeBits): the key IS its slot; direct-address
+//  counters in LDS take any number of instances (small k, or keys the planner
+//  could not split further).
 #include "okm_dev_common.h"
 
 namespace okm {
 
-constexpr int kCB = 512;                  // threads per workgroup
-constexpr int kHomeBits = 11;
-constexpr int kHomes = 1 << kHomeBits;    // home slots
-constexpr int kCap = 2048;                // distinct keys per pass
-constexpr int kSlots = kHomes + kCap;     // homes + forward-probe tail (never wraps)
-constexpr int kSlotsPer = kSlots / kCB;   // table slots ranked per thread (8)
-constexpr int kLoadU = 4;                 // independent key loads in flight per thread
+#ifndef OKM_COUNT_WPE
+#define OKM_COUNT_WPE 8  // waves per EU floor of the unweighted kernel: 4 blocks/CU (64 VGPRs)
+#endif
+#ifndef OKM_COUNT_PROF
+#define OKM_COUNT_PROF 0
+#endif
+// OKM_COUNT_PROF=1 builds: thread 0 of every block accumulates clock64()
+// deltas between phase marks (debug/tuning only; okm_debug_count_prof()).
+__device__ unsigned long long g_count_prof[16];
+__shared__ unsigned long long g_prof_last;
+#define PMARK(i)                                                        \
+    do {                                                                \
+        if (OKM_COUNT_PROF && threadIdx.x == 0) {                       \
+            const unsigned long long now_ = clock64();                  \
+            atomicAdd(&g_count_prof[i], now_ - g_prof_last);            \
+            g_prof_last = now_;                                         \
+        }                                                               \
+    } while (0)
 
-uint32_t count_item_capacity() { return kCap; }
+constexpr int kCB = 512;                  // threads per workgroup
+constexpr int kPer = 8;                   // instances per thread (tag / full modes)
+constexpr int kCapI = kCB * kPer;         // instances per tag/full-mode item (4096)
+constexpr int kHomeBits = 11;
+constexpr int kHomes = 1 << kHomeBits;    // 2048 homes
+constexpr int kHomesPer = kHomes / kCB;   // homes owned by one thread (4)
+constexpr int kDenseBits = kHomeBits;     // dense mode: rem_bits <= this
+constexpr int kLoadU = 4;                 // dense mode: loads in flight per thread
+
+// LDS carve-up (bytes).  Tag mode: tag[kHomes] u64, tag counts (u16 pairs /
+// u64), three u16-pair per-home arrays (rest counts -> rest offsets, rest
+// distinct -> output offsets, rest keys below the tag), then the rest buffer
+// (keys, weights, first-occurrence flags).  Unweighted: 40,896 + 32 B of scan
+// scratch, so that 3-4 workgroups fit in 160 KiB.
+constexpr int kTagBytes = kHomes * 8;
+constexpr int kPairBytes = kHomes * 2;  // one u16 per home, packed in pairs
+template <bool W> struct Lds {
+    static constexpr int kTcntBytes = W ? kHomes * 8 : kPairBytes;
+    static constexpr int kRc = kTagBytes + kTcntBytes;   // byte offsets of the u16-pair arrays
+    static constexpr int kHd = kRc + kPairBytes;
+    static constexpr int kLt = kHd + kPairBytes;
+    static constexpr int kFixed = kLt + kPairBytes;
+    static constexpr int kRestEntry = W ? 17 : 9;        // key (+ weight) + first flag
+    static constexpr int kFullBytes = kCapI * 8 * (W ? 2 : 1) + kPairBytes;  // full mode: keys (+w) + counters
+    static constexpr int kBytes = W ? kFixed + 2048 * kRestEntry : 40896;
+    static constexpr int kRest = ((kBytes - kFixed) / kRestEntry) & ~15;
+    static constexpr int kRestIters = (kRest + kCB - 1) / kCB;
+    static_assert(kFullBytes <= kBytes, "full mode must fit the carve-up");
+    static_assert(kHomes * 12 <= kBytes, "dense mode must fit the carve-up");
+};
+
+uint32_t count_item_capacity() { return kCapI; }
+uint32_t count_dense_bits() { return kDenseBits; }
 
 template <bool W>
 struct CountType {
@@ -43,143 +94,527 @@ struct CountType<true> {
     typedef ull T;
 };
 
-// Monotone home slot: the kHomeBits key bits below the top `lg` bits of the
-// item's `rem` remaining bits (fewer remaining bits are scaled up).
-__device__ __forceinline__ uint32_t home_of(uint64_t key, uint32_t r) {
-    if (r >= (uint32_t)kHomeBits) return (uint32_t)(key >> (r - kHomeBits)) & (kHomes - 1);
-    return ((uint32_t)key & ((1u << r) - 1u)) << (kHomeBits - r);
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
 }
 
-template <bool W>
-__global__ __launch_bounds__(kCB) void k_count_items(const DevItem *__restrict__ items, uint32_t nitems,
-                                                     const DevSeg *__restrict__ segs,
-                                                     uint64_t *__restrict__ out_keys,
-                                                     uint64_t *__restrict__ out_counts,
-                                                     ull *__restrict__ n_out, ull *__restrict__ ctl) {
-    typedef typename CountType<W>::T CT;
-    __shared__ ull tk[kSlots];
-    __shared__ CT tc[kSlots];
-    __shared__ ull wsum[kCB / 64];
-    __shared__ uint32_t s_distinct, s_ovf;
-
-    const uint32_t t = threadIdx.x;
-    // Block-uniform values that steer loops containing barriers are kept
-    // scalar (blockIdx, readfirstlane of LDS words): hipcc otherwise treats
-    // LDS loads as divergent and structurises those loops with exec masks.
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const DevItem it = items[item];
-        uint32_t lg = 0, sub = 0;  // current pass: sub-range `sub` of 2^lg
-        ull written = 0;
-        for (;;) {
-            for (int j = t; j < kSlots; j += kCB) {
-                tk[j] = kEmptyKey;
-                tc[j] = 0;
-            }
-            if (t == 0) {
-                s_distinct = 0;
-                s_ovf = 0;
-            }
-            __syncthreads();
-            const uint32_t r = it.rem_bits - lg;  // bits below the sub-range id
-            const uint64_t smask = (1ull << lg) - 1ull;
-            for (uint32_t sg = 0; sg < it.seg_count; ++sg) {
-                const DevSeg s = segs[it.seg_begin + sg];
-                for (uint64_t base = 0; base < s.len; base += (uint64_t)kCB * kLoadU) {
-                    ull kk[kLoadU];
-                    CT ww[kLoadU];
+// Block-wide exclusive scan (u32); returns the block total in *total.  Two barriers.
+__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan32(v);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
 #pragma unroll
-                    for (int u = 0; u < kLoadU; ++u) {
-                        const uint64_t idx = base + (uint64_t)u * kCB + t;
-                        kk[u] = idx < s.len ? s.keys[idx] : kEmptyKey;
-                        ww[u] = 1;
-                        if (W && idx < s.len && s.counts) ww[u] = (CT)s.counts[idx];
-                    }
-#pragma unroll
-                    for (int u = 0; u < kLoadU; ++u) {
-                        const ull key = kk[u];
-                        if (key == kEmptyKey) continue;
-                        if (lg && ((key >> r) & smask) != sub) continue;
-                        if (s_ovf) continue;
-                        // DashMap entry().or_insert().fetch_add() (count.rs:31-34)
-                        for (uint32_t h = home_of(key, r); h < (uint32_t)kSlots; ++h) {
-                            const ull old = atomicCAS(&tk[h], (ull)kEmptyKey, key);
-                            if (old == kEmptyKey) {
-                                if (atomicAdd(&s_distinct, 1u) >= (uint32_t)kCap) s_ovf = 1;
-                                atomicAdd(&tc[h], ww[u]);
-                                break;
-                            }
-                            if (old == key) {
-                                atomicAdd(&tc[h], ww[u]);
-                                break;
-                            }
-                            if (h == (uint32_t)kSlots - 1) s_ovf = 1;  // tail exhausted
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            const bool ovf = __builtin_amdgcn_readfirstlane(s_ovf) != 0;
-            __syncthreads();
-            if (ovf) {  // more than kCap distinct keys in this sub-range: halve it
-                ++lg;
-                sub <<= 1;
-                if (lg > it.rem_bits || lg > 40) {  // cannot happen: 2^11 keys always fit
-                    if (t == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);
-                    break;
-                }
-                continue;
-            }
-            // ordinal of every occupied slot (table order)
-            const uint32_t s0 = t * kSlotsPer;
-            ull rk[kSlotsPer];
-            uint32_t mine = 0;
-#pragma unroll
-            for (int j = 0; j < kSlotsPer; ++j) {
-                rk[j] = tk[s0 + j];
-                mine += rk[j] != kEmptyKey;
-            }
-            ull total;
-            uint32_t ord = (uint32_t)block_excl_scan<kCB>(mine, wsum, &total);
-            const uint32_t D = __builtin_amdgcn_readfirstlane((uint32_t)total);
-            const uint64_t o = it.out_off + written;
-#pragma unroll
-            for (int j = 0; j < kSlotsPer; ++j) {
-                const ull key = rk[j];
-                if (key == kEmptyKey) continue;
-                const uint32_t i = s0 + j;
-                uint32_t a = i;
-                while (a > 0 && tk[a - 1] != kEmptyKey) --a;  // cluster start
-                uint32_t less = 0;
-                for (uint32_t q = a; q < (uint32_t)kSlots; ++q) {
-                    const ull x = tk[q];
-                    if (x == kEmptyKey) break;
-                    less += x < key;
-                }
-                const uint32_t rank = ord - (i - a) + less;  // count.rs:119 order
-                out_keys[o + rank] = key;
-                out_counts[o + rank] = (uint64_t)tc[i];
-                ++ord;
-            }
-            written += D;
-            ++sub;
-            __syncthreads();
-            if (sub >> lg) break;
-        }
-        if (t == 0) n_out[item] = written;
+    for (int w = 0; w < kCB / 64; ++w) {
+        const uint32_t s = wsum[w];
+        wbase += w < wid ? s : 0u;
+        tot += s;
     }
+    __syncthreads();
+    *total = tot;
+    return wbase + inc - v;
+}
+
+// Top kHomeBits of the r remaining bits (r > kHomeBits): monotone in the key.
+__device__ __forceinline__ uint32_t home_of(uint64_t key, uint32_t r) {
+    return (uint32_t)(key >> (r - kHomeBits)) & (kHomes - 1);
+}
+
+// Packed u16 pair helpers (home h lives in word h >> 1, half h & 1).
+__device__ __forceinline__ uint32_t half_shift(uint32_t h) { return (h & 1u) << 4; }
+__device__ __forceinline__ uint32_t half_of(uint32_t word, uint32_t h) { return (word >> half_shift(h)) & 0xFFFFu; }
+
+// Instances of an item (scalar loop over its segments: block-uniform).
+__device__ __forceinline__ uint64_t item_total(const DevItem &it, const DevSeg *__restrict__ segs) {
+    uint64_t total = 0;
+    for (uint32_t sg = 0; sg < it.seg_count; ++sg) total += segs[it.seg_begin + sg].len;
+    return total;
+}
+
+// Load a tag/full-mode item's instances into registers (flat index over its
+// segments; such items hold <= kCapI instances, so 32-bit indices).
+template <bool W>
+__device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__restrict__ segs, ull (&kk)[kPer],
+                                          ull (&ww)[kPer]) {
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        kk[u] = kEmptyKey;
+        ww[u] = 1;
+    }
+    uint32_t sbase = 0;
+    for (uint32_t sg = 0; sg < it.seg_count; ++sg) {
+        const DevSeg s = segs[it.seg_begin + sg];
+        const uint32_t len = (uint32_t)s.len;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            if ((uint32_t)u * kCB >= sbase + len) break;  // block-uniform: rows past the segment
+            const uint32_t f = (uint32_t)u * kCB + t - sbase;  // wraps for f < sbase
+            if (f < len) {
+                kk[u] = s.keys[f];
+                if (W && s.counts) ww[u] = s.counts[f];
+            }
+        }
+        sbase += len;
+    }
+}
+
+// Insertion sort of sk[a, a + n) (+ weights), n small.
+template <bool W>
+__device__ __forceinline__ void slice_sort(ull *sk, ull *sw, uint32_t a, uint32_t n) {
+    for (uint32_t i = a + 1; i < a + n; ++i) {
+        const ull x = sk[i];
+        const ull xw = W ? sw[i] : 0ull;
+        uint32_t j = i;
+        while (j > a && sk[j - 1] > x) {
+            sk[j] = sk[j - 1];
+            if (W) sw[j] = sw[j - 1];
+            --j;
+        }
+        sk[j] = x;
+        if (W) sw[j] = xw;
+    }
+}
+
+__device__ __forceinline__ uint32_t slice_distinct(const ull *sk, uint32_t a, uint32_t n) {
+    uint32_t d = 0;
+    ull prev = kEmptyKey;
+    for (uint32_t i = a; i < a + n; ++i) {
+        const ull x = sk[i];
+        d += x != prev;
+        prev = x;
+    }
+    return d;
+}
+
+// Tag-mode LDS state between items: all tags empty, all counters zero.
+template <bool W>
+__device__ __forceinline__ void tag_reset(ull *lds) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(lds);
+    __syncthreads();
+    for (int j = threadIdx.x; j < kHomes; j += kCB) lds[j] = kEmptyKey;
+    for (int j = kTagBytes / 4 + threadIdx.x; j < Lds<W>::kFixed / 4; j += kCB) p[j] = 0;
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// full mode (fallback): every instance counting-sorted by home
+// ---------------------------------------------------------------------------
+
+template <bool W>
+__device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
+                                           ull *lds, uint32_t *wsum, uint64_t *__restrict__ out_keys,
+                                           uint64_t *__restrict__ out_counts) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t r = it.rem_bits;
+    const uint64_t out_off = it.out_off;
+    ull kk[kPer];
+    ull ww[kPer];
+    load_item<W>(it, segs, kk, ww);
+    ull *sk = lds;
+    ull *sw = lds + kCapI;
+    uint32_t *hc = reinterpret_cast<uint32_t *>(lds + kCapI * (W ? 2 : 1));
+    __syncthreads();  // the previous item's LDS state is dead
+    hc[2 * t] = 0;
+    hc[2 * t + 1] = 0;
+    __syncthreads();
+    uint32_t hp[kPer];  // home << 16 | pos
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if ((uint32_t)u >= nrows) break;  // block-uniform
+        hp[u] = 0;
+        if (kk[u] != kEmptyKey) {
+            const uint32_t h = home_of(kk[u], r);
+            const uint32_t o = atomicAdd(&hc[h >> 1], 1u << half_shift(h));
+            hp[u] = (h << 16) | half_of(o, h);
+        }
+    }
+    __syncthreads();
+    const uint32_t w0 = hc[2 * t], w1 = hc[2 * t + 1];
+    const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
+    const uint32_t n = c0 + c1 + c2 + (w1 >> 16);
+    uint32_t ntot;
+    const uint32_t a = block_excl_scan32(n, wsum, &ntot);
+    hc[2 * t] = a | ((a + c0) << 16);
+    hc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if ((uint32_t)u >= nrows) break;  // block-uniform
+        if (kk[u] != kEmptyKey) {
+            const uint32_t h = hp[u] >> 16;
+            const uint32_t dst = half_of(hc[h >> 1], h) + (hp[u] & 0xFFFFu);
+            sk[dst] = kk[u];
+            if (W) sw[dst] = ww[u];
+        }
+    }
+    __syncthreads();
+    slice_sort<W>(sk, sw, a, n);
+    const uint32_t d = slice_distinct(sk, a, n);
+    uint32_t D;
+    const uint32_t od = block_excl_scan32(d, wsum, &D);
+    uint64_t o = out_off + od;  // DashMap value = instances (count.rs:33)
+    uint32_t i = a;
+    while (i < a + n) {
+        const ull key = sk[i];
+        ull c = 0;
+        do {
+            c += W ? sw[i] : 1ull;
+            ++i;
+        } while (i < a + n && sk[i] == key);
+        out_keys[o] = key;
+        out_counts[o] = c;
+        ++o;
+    }
+    return __builtin_amdgcn_readfirstlane(D);
+}
+
+// ---------------------------------------------------------------------------
+// tag mode
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t kDeferred = ~0u;
+
+template <bool W>
+__device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
+                                             const ull (&kk)[kPer], const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
+                                             uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts) {
+    const uint32_t r = it.rem_bits;
+    const uint64_t out_off = it.out_off;
+    typedef Lds<W> L;
+    typedef typename CountType<W>::T CT;
+    const uint32_t t = threadIdx.x;
+    char *base = reinterpret_cast<char *>(lds);
+    ull *tag = lds;
+    uint32_t *tc16 = reinterpret_cast<uint32_t *>(lds + kHomes);
+    ull *tc64 = lds + kHomes;
+    uint32_t *rc = reinterpret_cast<uint32_t *>(base + L::kRc);  // rest counts, then rest offsets
+    uint32_t *hd = reinterpret_cast<uint32_t *>(base + L::kHd);  // rest distinct, then output offsets
+    uint32_t *lt = reinterpret_cast<uint32_t *>(base + L::kLt);  // rest distinct keys below the tag
+    ull *rk = reinterpret_cast<ull *>(base + L::kFixed);
+    ull *rw = rk + L::kRest;
+    uint8_t *rf = reinterpret_cast<uint8_t *>(rk + (W ? 2 : 1) * L::kRest);
+
+    // 1. claim / count tags; rest instances take a slot in their home's run
+    uint32_t hp[kPer];  // rest: home << 16 | pos; otherwise ~0
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if ((uint32_t)u >= nrows) break;  // block-uniform
+        hp[u] = ~0u;
+        const ull x = kk[u];
+        if (x != kEmptyKey) {
+            const uint32_t h = home_of(x, r);
+            const ull old = atomicCAS(&tag[h], kEmptyKey, x);
+            if (old == kEmptyKey || old == x) {  // DashMap entry().or_insert().fetch_add() (count.rs:31-34)
+                if (W)
+                    atomicAdd(&tc64[h], ww[u]);
+                else
+                    atomicAdd(&tc16[h >> 1], 1u << half_shift(h));  // <= 4096 per item: no carry
+            } else {
+                const uint32_t o = atomicAdd(&rc[h >> 1], 1u << half_shift(h));
+                hp[u] = (h << 16) | half_of(o, h);
+            }
+        }
+    }
+    __syncthreads();
+    PMARK(2);
+    // 2. rest offsets: thread t owns homes [4t, 4t+4) = words 2t, 2t+1
+    {
+        const uint32_t w0 = rc[2 * t], w1 = rc[2 * t + 1];
+        const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
+        uint32_t rtot;
+        const uint32_t a = block_excl_scan32(c0 + c1 + c2 + (w1 >> 16), wsum, &rtot);
+        if (__builtin_amdgcn_readfirstlane(rtot) > (uint32_t)L::kRest) {  // block-uniform
+            tag_reset<W>(lds);
+            return kDeferred;  // too many rest instances: k_count_slow takes the item
+        }
+        rc[2 * t] = a | ((a + c0) << 16);
+        rc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
+        if (t == 0) wsum[kCB / 64] = rtot;  // rest total, read by every rest position below
+    }
+    __syncthreads();
+    PMARK(3);
+    // 3. scatter rest instances into home order
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if ((uint32_t)u >= nrows) break;
+        if (hp[u] != ~0u) {
+            const uint32_t h = hp[u] >> 16;
+            const uint32_t dst = half_of(rc[h >> 1], h) + (hp[u] & 0xFFFFu);
+            rk[dst] = kk[u];
+            if (W) rw[dst] = ww[u];
+        }
+    }
+    __syncthreads();
+    PMARK(4);
+    // 4. rest positions, one per lane: count, first occurrence in the home's
+    //    run, and what the home's distinct count / tag rank must include
+    const uint32_t rtot = __builtin_amdgcn_readfirstlane(wsum[kCB / 64]);
+    ull px[L::kRestIters];
+    CT pc[L::kRestIters];
+    uint32_t prange[L::kRestIters];  // hs << 16 | he; 0 = not a first occurrence
+#pragma unroll
+    for (int k = 0; k < L::kRestIters; ++k) {
+        prange[k] = 0;
+        if ((uint32_t)k * kCB >= rtot) break;  // block-uniform
+        const uint32_t p = (uint32_t)k * kCB + t;
+        if (p < rtot) {
+            const ull x = rk[p];
+            const uint32_t h = home_of(x, r);
+            const uint32_t hs = half_of(rc[h >> 1], h);
+            const uint32_t he = h + 1 < (uint32_t)kHomes ? half_of(rc[(h + 1) >> 1], h + 1) : rtot;
+            CT c = 0;
+            bool first = true;
+            for (uint32_t q = hs; q < he; ++q) {
+                const bool eq = rk[q] == x;
+                c += eq ? (W ? (CT)rw[q] : (CT)1) : (CT)0;
+                first = first && !(eq && q < p);
+            }
+            rf[p] = first ? 1 : 0;
+            px[k] = x;
+            pc[k] = c;
+            if (first) {
+                prange[k] = (hs << 16) | he;
+                atomicAdd(&hd[h >> 1], 1u << half_shift(h));
+                if (x < tag[h]) atomicAdd(&lt[h >> 1], 1u << half_shift(h));
+            }
+        }
+    }
+    __syncthreads();
+    PMARK(5);
+    // 5. output offsets per home: [tag] + rest distinct keys
+    ull tg[kHomesPer];
+    uint32_t ho[kHomesPer];
+    uint32_t D;
+    {
+        const uint32_t w0 = hd[2 * t], w1 = hd[2 * t + 1];
+        uint32_t dq[kHomesPer] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+        uint32_t d = 0;
+#pragma unroll
+        for (int q = 0; q < kHomesPer; ++q) {
+            tg[q] = tag[kHomesPer * t + q];
+            dq[q] += tg[q] != kEmptyKey;
+            ho[q] = d;
+            d += dq[q];
+        }
+        const uint32_t od = block_excl_scan32(d, wsum, &D);
+#pragma unroll
+        for (int q = 0; q < kHomesPer; ++q) ho[q] += od;
+        hd[2 * t] = ho[0] | (ho[1] << 16);
+        hd[2 * t + 1] = ho[2] | (ho[3] << 16);
+    }
+    __syncthreads();
+    PMARK(6);
+    // 6a. tags: rank = home offset + rest distinct keys below the tag
+    {
+        const uint32_t l0 = lt[2 * t], l1 = lt[2 * t + 1];
+        const uint32_t lq[kHomesPer] = {l0 & 0xFFFFu, l0 >> 16, l1 & 0xFFFFu, l1 >> 16};
+        uint32_t nq[kHomesPer];
+        if (!W) {
+            const uint32_t n0 = tc16[2 * t], n1 = tc16[2 * t + 1];
+            nq[0] = n0 & 0xFFFFu;
+            nq[1] = n0 >> 16;
+            nq[2] = n1 & 0xFFFFu;
+            nq[3] = n1 >> 16;
+        }
+#pragma unroll
+        for (int q = 0; q < kHomesPer; ++q) {
+            if (tg[q] != kEmptyKey) {
+                const uint64_t o = out_off + ho[q] + lq[q];
+                out_keys[o] = tg[q];
+                out_counts[o] = W ? (uint64_t)tc64[kHomesPer * t + q] : (uint64_t)nq[q];
+            }
+        }
+    }
+    // 6b. rest keys: rank = home offset + rest distinct keys below + [tag below]
+#pragma unroll
+    for (int k = 0; k < L::kRestIters; ++k) {
+        if ((uint32_t)k * kCB >= rtot) break;
+        if (prange[k]) {
+            const ull x = px[k];
+            const uint32_t hs = prange[k] >> 16, he = prange[k] & 0xFFFFu;
+            uint32_t less = 0;
+            for (uint32_t q = hs; q < he; ++q) less += (rf[q] && rk[q] < x) ? 1u : 0u;
+            const uint32_t h = home_of(x, r);
+            const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + (tag[h] < x ? 1u : 0u);
+            out_keys[o] = x;
+            out_counts[o] = (uint64_t)pc[k];
+        }
+    }
+    PMARK(7);
+    // reset this thread's homes for the next item once every reader is done
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kHomesPer; ++q) {
+        tag[kHomesPer * t + q] = kEmptyKey;
+        if (W) tc64[kHomesPer * t + q] = 0;
+    }
+    if (!W) {
+        tc16[2 * t] = 0;
+        tc16[2 * t + 1] = 0;
+    }
+    rc[2 * t] = rc[2 * t + 1] = 0;
+    hd[2 * t] = hd[2 * t + 1] = 0;
+    lt[2 * t] = lt[2 * t + 1] = 0;
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(D);
+}
+
+// ---------------------------------------------------------------------------
+// dense mode: direct-address counters (rem_bits <= kDenseBits)
+// ---------------------------------------------------------------------------
+
+template <bool W>
+__device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *__restrict__ segs,
+                                               uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts,
+                                               ull *lds, uint32_t *wsum) {
+    typedef typename CountType<W>::T CT;
+    const uint32_t t = threadIdx.x;
+    const uint32_t r = it.rem_bits;
+    const uint32_t nslots = 1u << r;
+    const ull mask = (ull)nslots - 1ull;
+    ull *slot_key = lds;                                      // [kHomes]
+    CT *cnt = reinterpret_cast<CT *>(lds + kHomes);           // [kHomes]
+    __syncthreads();  // the previous item's LDS state is dead
+    for (uint32_t j = t; j < nslots; j += kCB) cnt[j] = 0;
+    __syncthreads();
+    for (uint32_t sg = 0; sg < it.seg_count; ++sg) {
+        const DevSeg s = segs[it.seg_begin + sg];
+        for (uint64_t base = 0; base < s.len; base += (uint64_t)kCB * kLoadU) {
+            ull kk[kLoadU];
+            CT ww[kLoadU];
+#pragma unroll
+            for (int u = 0; u < kLoadU; ++u) {
+                const uint64_t idx = base + (uint64_t)u * kCB + t;
+                kk[u] = idx < s.len ? s.keys[idx] : kEmptyKey;
+                ww[u] = (W && s.counts && idx < s.len) ? (CT)s.counts[idx] : (CT)1;
+            }
+#pragma unroll
+            for (int u = 0; u < kLoadU; ++u) {
+                if (kk[u] != kEmptyKey) {
+                    const uint32_t h = (uint32_t)(kk[u] & mask);
+                    atomicAdd(&cnt[h], ww[u]);
+                    slot_key[h] = kk[u];  // all writers of a slot store the same key
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t d = 0;
+    for (uint32_t q = 0; q < kHomesPer; ++q) {
+        const uint32_t j = t * kHomesPer + q;
+        d += (j < nslots && cnt[j] != 0) ? 1u : 0u;
+    }
+    uint32_t D;
+    uint64_t o = it.out_off + block_excl_scan32(d, wsum, &D);
+    for (uint32_t q = 0; q < kHomesPer; ++q) {
+        const uint32_t j = t * kHomesPer + q;
+        if (j < nslots && cnt[j] != 0) {
+            out_keys[o] = slot_key[j];
+            out_counts[o] = (uint64_t)cnt[j];
+            ++o;
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(D);
+}
+
+// Tag-mode kernel.  Items it cannot take (dense-mode items, rest overflow)
+// go to the deferred list defer[ctl[1]++] for k_count_slow, which runs right
+// after it: separate kernels keep the rare paths' registers out of this one.
+template <bool W>
+__global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM_COUNT_WPE)))
+void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
+                   uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
+                   ull *__restrict__ ctl, uint32_t *__restrict__ defer) {
+    __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
+    __shared__ uint32_t wsum[kCB / 64 + 1];
+    const uint32_t t = threadIdx.x;
+    tag_reset<W>(lds);
+    if (OKM_COUNT_PROF && t == 0) g_prof_last = clock64();
+    // Block-uniform values that steer code containing barriers come from
+    // blockIdx / scalar loads (see DESIGN.md on the structuriser).
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        PMARK(0);
+        const DevItem it = items[item];
+        const uint64_t total = item_total(it, segs);
+        uint32_t written = kDeferred;
+        if (it.rem_bits > (uint32_t)kDenseBits && total <= (uint64_t)kCapI) {
+            ull kk[kPer];
+            ull ww[kPer];
+            load_item<W>(it, segs, kk, ww);
+            PMARK(1);
+            const uint32_t nrows = (uint32_t)((total + kCB - 1) / kCB);  // rows of kk in use (block-uniform)
+            written = tag_item<W>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);
+        }
+        if (t == 0) {
+            if (written == kDeferred)
+                defer[atomicAdd(reinterpret_cast<unsigned int *>(ctl + 1), 1u)] = item;
+            else
+                n_out[item] = written;
+        }
+        PMARK(9);
+    }
+}
+
+// Deferred items: dense mode, or full mode (every instance counting-sorted).
+template <bool W>
+__global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ items, const DevSeg *__restrict__ segs,
+                                                    uint64_t *__restrict__ out_keys,
+                                                    uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
+                                                    ull *__restrict__ ctl, const uint32_t *__restrict__ defer) {
+    constexpr int kBytes = Lds<W>::kFullBytes > kHomes * 12 ? Lds<W>::kFullBytes : kHomes * 12;
+    __shared__ __attribute__((aligned(16))) ull lds[kBytes / 8];
+    __shared__ uint32_t wsum[kCB / 64 + 1];
+    const uint32_t ndefer = *reinterpret_cast<volatile const unsigned int *>(ctl + 1);
+    for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
+        const uint32_t item = defer[j];
+        const DevItem it = items[item];
+        const uint64_t total = item_total(it, segs);
+        uint32_t written = 0;
+        if (it.rem_bits <= (uint32_t)kDenseBits) {
+            written = dense_item<W>(it, segs, out_keys, out_counts, lds, wsum);
+        } else if (total <= (uint64_t)kCapI) {
+            written = full_item<W>(it, segs, (uint32_t)((total + kCB - 1) / kCB), lds, wsum, out_keys, out_counts);
+        } else if (threadIdx.x == 0) {
+            atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
+        }
+        if (threadIdx.x == 0) n_out[item] = written;
+        __syncthreads();  // LDS reuse by the next item
+    }
+}
+
+// Phase cycle totals of an OKM_COUNT_PROF build (zeroes them).
+void count_prof_read(unsigned long long *out16) {
+    (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_count_prof), 16 * sizeof(unsigned long long));
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_count_prof), z, sizeof(z));
 }
 
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, bool weighted) {
+                        unsigned long long *ctl, uint32_t *defer, bool weighted) {
     if (!nitems) return;
-    const uint32_t grid = nitems < 2048u ? nitems : 2048u;
-    if (weighted)
-        hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, (hipStream_t)stream, items, nitems,
-                           segs, out_keys, out_counts, n_out, ctl);
-    else
-        hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, (hipStream_t)stream, items, nitems,
-                           segs, out_keys, out_counts, n_out, ctl);
+    const uint32_t grid = nitems < 4096u ? nitems : 4096u;
+    const uint32_t sgrid = nitems < 1024u ? nitems : 1024u;  // exits at once when nothing was deferred
+    hipStream_t s = (hipStream_t)stream;
+    if (weighted) {
+        hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
+                           out_counts, n_out, ctl, defer);
+        hipLaunchKernelGGL(k_count_slow<true>, dim3(sgrid), dim3(kCB), 0, s, items, segs, out_keys, out_counts,
+                           n_out, ctl, defer);
+    } else {
+        hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
+                           out_counts, n_out, ctl, defer);
+        hipLaunchKernelGGL(k_count_slow<false>, dim3(sgrid), dim3(kCB), 0, s, items, segs, out_keys, out_counts,
+                           n_out, ctl, defer);
+    }
 }
 
 }  // namespace okm

@@ -529,13 +529,16 @@ static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
     invalidate_result(c);
     const uint32_t twok = 2u * c->k;
-    const uint64_t cap = count_item_capacity();        // distinct keys per LDS pass
-    const uint32_t capbits = log2_floor(cap);          // 2^capbits <= cap: never needs a 2nd pass
+    // sort-mode items hold at most count_item_capacity() instances; items with
+    // at most count_dense_bits() remaining key bits are counted by direct
+    // address and may be any size (okm_count.hip)
+    const uint64_t item_max = count_item_capacity();   // split parts larger than this
+    const uint32_t capbits = count_dense_bits();
     // Items are sized in instances, assuming some duplication (reads cover
     // the genome several times); an item with more distinct keys than one
     // pass holds is still counted exactly, in several passes (okm_count.hip).
-    const uint64_t item_max = cap * 2;                 // split parts larger than this
-    const uint64_t target = item_max * 3 / 4;          // aim below it after a split
+    const uint64_t target = item_max * 3 / 4;          // aim below it after a split (canonical-key density
+                                                       // gradients and line padding must still fit)
     bool weighted = false;
     for (auto &r : c->runs) weighted |= (r.counts != nullptr);
     const uint32_t maxb = log2_floor(part_max_bins(weighted));  // bits one pass can split
@@ -683,6 +686,8 @@ static okm_status do_count(okm_ctx *c) {
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    uint32_t *defer;
+    OKM_TRY(pool_get(c->pool, nitems, &defer));
     c->hprof.mark("items.build");
     if (!device_items) {
         HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
@@ -692,7 +697,7 @@ static okm_status do_count(okm_ctx *c) {
     HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, weighted);
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted);
     c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
@@ -720,6 +725,7 @@ static okm_status do_count(okm_ctx *c) {
     c->pool.put(n_out);
     c->pool.put(dense_off);
     c->pool.put(scan_tmp);
+    c->pool.put(defer);
     c->n_res = nd;
     c->info.distinct = nd;
     c->counted = true;
@@ -836,6 +842,10 @@ void okm_destroy(okm_ctx *c) {
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
+
+// Tuning hook (not part of the C ABI header): phase cycle totals of an
+// OKM_COUNT_PROF=1 build of the counting kernel; zeroes them.
+extern "C" void okm_debug_count_prof(unsigned long long *out16) { okm::count_prof_read(out16); }
 
 okm_status okm_reset(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");

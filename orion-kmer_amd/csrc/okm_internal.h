@@ -83,13 +83,17 @@ void launch_exclusive_scan(void *stream, const unsigned long long *in, unsigned 
                            uint64_t n, unsigned long long *tmp);
 
 // LDS counting of partitions (okm_count.hip); writes sorted distinct
-// (key,count) at out_off and n_out[item].  ctl[0] = error word, ctl[1] = item
-// queue (both zeroed before the launch).  count_item_capacity() = distinct
-// keys one LDS pass holds (bigger items take several passes).
+// (key,count) at out_off and n_out[item].  ctl[0] = error word, ctl[1] =
+// deferred-item count (both zeroed before the launch).  An item holds at most count_item_capacity() instances unless
+// its rem_bits <= count_dense_bits() (direct-address counting, any size).
 uint32_t count_item_capacity();
+void count_prof_read(unsigned long long *out16);  // OKM_COUNT_PROF builds only
+uint32_t count_dense_bits();
+// ctl[1] counts deferred items (list `defer`, nitems entries) for the second
+// kernel of the launch.
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, bool weighted);
+                        unsigned long long *ctl, uint32_t *defer, bool weighted);
 
 // A part that took part in a device-side split round: its children are the
 // output bins [out_base, out_base + nlocal) of the round.

@@ -120,11 +120,12 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise OkmError(OKM_E_DEVICE, f"{LIB_PATH} is missing: build it with "
+    path = os.environ.get("OKM_LIB") or LIB_PATH  # OKM_LIB: an alternative build (A/B timing)
+    if not os.path.exists(path):
+        raise OkmError(OKM_E_DEVICE, f"{path} is missing: build it with "
                                      f"`python -c 'import __graft_entry__ as g; g.build()'` "
                                      f"or `make -C orion-kmer_amd` (there is no fallback)")
-    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in PROTOTYPES.items():
         fn = getattr(lib, name)
         fn.restype = res

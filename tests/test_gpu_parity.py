@@ -283,6 +283,35 @@ def test_hot_key_and_long_record():
     assert info["levels"] >= 2
 
 
+@pytest.mark.parametrize("k", [31, 17])
+def test_unique_keys_full_mode(k):
+    # one 2 Mbp random record: (almost) every k-mer is distinct, so the LDS
+    # items overflow the tag mode's rest buffer and take the full-mode kernel;
+    # the pairs merge of two halves exercises its weighted variant
+    g = okm.synth_reads(1, 2_000_000, genome_len=2_000_000, genome_seed=77 + k, seed=5, sub_rate=0.0)
+    rec = bytes(g[:2_000_000])
+    oc = OracleCounter(k)
+    oc.add_records([rec])
+    ek, ec = oc.result(1)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records([rec])
+        gk, gc = ctr.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    parts = []
+    for sl in (rec[:1_000_030], rec[1_000_000:]):
+        with okm.KmerCounter(k) as c:
+            c.add_records([sl])
+            parts.append(c.result(1))
+    with okm.KmerCounter(k) as m:
+        for pk, pc in parts:
+            m.add_pairs(pk, pc)
+        mk, mc = m.result(1)
+    oc2 = OracleCounter(k)
+    oc2.add_records([rec[:1_000_030], rec[1_000_000:]])
+    ek2, ec2 = oc2.result(1)
+    assert np.array_equal(mk, ek2) and np.array_equal(mc, ec2)
+
+
 def test_empty_inputs():
     with okm.KmerCounter(21) as ctr:
         ctr.add_records([])
