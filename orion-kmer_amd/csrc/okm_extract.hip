@@ -6,16 +6,23 @@
 //   kmer.rs:37-57   seq_to_u64           -> rolling forward word `fwd`
 //   kmer.rs:79-94   reverse_complement   -> rolling `rc`
 //   kmer.rs:99-106  canonical_u64        -> min(fwd, rc)
-//   count.rs:23-38  window loop          -> scan_segment + valid-run counter
+//   count.rs:23-38  window loop          -> scan_windows + valid-run counter
 //
 // Two kernels per batch.  extract_hist counts, per persistent block, the keys
 // of each bin (top l1 bits of the 2k-bit key); the host turns the totals into
-// bin offsets.  extract_scatter recomputes the k-mers (ALU is cheap next to
-// HBM) and places them exactly: each block owns one contiguous slice per bin
-// (claimed with one returning atomic per (block, bin)), and every 8192-window
-// tile is counting-sorted by bin in LDS first so that each bin's keys leave
-// the CU as one contiguous run (~256 B at 256 bins) instead of 8-byte
-// scattered stores (which cost 3.5x the bytes in HBM writes).
+// bin offsets.  extract_scatter places every key exactly: each block owns one
+// contiguous slice per bin (claimed with one returning atomic per (block,
+// bin)), and every 8192-window tile is counting-sorted by bin in LDS first so
+// that each bin's keys leave the CU as one contiguous run (~256 B at 256 bins)
+// instead of 8-byte scattered stores (which cost 3.5x the bytes in HBM
+// writes).
+//
+// Both kernels are instantiated for common k (template K) besides the generic
+// runtime-k one: with K known, the window index of every byte step is a
+// compile-time constant, so extract_scatter keeps a thread's 32 keys (and
+// their within-bin ranks, returned by the histogram atomic) in registers and
+// computes each k-mer ONCE; the generic kernel computes them twice.  Emits are
+// branch-free: an invalid window counts into a dummy bin.
 #include "okm_dev_common.h"
 
 namespace okm {
@@ -34,27 +41,31 @@ __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
     return shift >= 64 ? 0u : (uint32_t)(key >> shift);
 }
 
-constexpr int kSeg = 32;           // window starts per thread
-constexpr int kLoad = kSeg + 32;   // bytes per thread: covers kSeg + k - 1 for k <= 32
 constexpr int kExtractBlock = 256;
-constexpr int kTile = kExtractBlock * kSeg;
+constexpr int kSegS = 32;                      // scatter: window starts per thread
+constexpr int kTile = kExtractBlock * kSegS;   // scatter tile: 8192 windows
+constexpr int kSegH = 64;                      // hist: window starts per thread
+constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
 constexpr int kMaxL1Bins = 256;
 
-uint32_t extract_tile() { return (uint32_t)kTile; }
+uint32_t extract_tile() { return (uint32_t)kHTile; }  // chunks are multiples of both tiles
 uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
 
-// Walk the windows starting in [w0, w0 + kSeg) of a batch of n bytes.  Every
-// window whose k bytes are all valid is canonicalised and handed to emit().
+// Walk the windows starting in [w0, w0 + SEG) of a batch of n bytes and call
+// emit(j, key, valid) for each window start j = 0..SEG-1, in order (K > 0: j
+// is a compile-time constant after unrolling; K = 0: runtime k, runtime j).
 // Bytes at or beyond n read as 0 (invalid), so windows never run off the end;
 // record separators are invalid bytes, so windows never cross records.
-template <typename Emit>
-__device__ __forceinline__ void scan_segment(const uint8_t *__restrict__ seq, uint64_t n,
-                                             uint64_t w0, uint32_t k, Emit &&emit) {
-    uint32_t w[kLoad / 4];
-    if (w0 + kLoad <= n) {
+template <int SEG, int K, typename Emit>
+__device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
+                                             uint32_t k_rt, Emit &&emit) {
+    constexpr int LOAD = SEG + 32;  // bytes: covers SEG + k - 1 for k <= 32 (16-B multiple)
+    const uint32_t k = K ? (uint32_t)K : k_rt;
+    uint32_t w[LOAD / 4];
+    if (w0 + LOAD <= n) {
         const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
 #pragma unroll
-        for (int q = 0; q < kLoad / 16; ++q) {
+        for (int q = 0; q < LOAD / 16; ++q) {
             const uint4 v = p[q];
             w[4 * q + 0] = v.x;
             w[4 * q + 1] = v.y;
@@ -63,7 +74,7 @@ __device__ __forceinline__ void scan_segment(const uint8_t *__restrict__ seq, ui
         }
     } else {
 #pragma unroll
-        for (int q = 0; q < kLoad / 4; ++q) {
+        for (int q = 0; q < LOAD / 4; ++q) {
             uint32_t x = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -78,50 +89,69 @@ __device__ __forceinline__ void scan_segment(const uint8_t *__restrict__ seq, ui
     const uint32_t rcs = 2 * k - 2;
     uint64_t fwd = 0, rc = 0;
     uint32_t run = 0;
+    constexpr int STEPS = K ? SEG + K - 1 : LOAD - 1;
 #pragma unroll
-    for (int i = 0; i < kLoad - 1; ++i) {
+    for (int i = 0; i < STEPS; ++i) {
         const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
         const uint32_t code = base_code(c);
         fwd = ((fwd << 2) | code) & kmask;                    // kmer.rs:51, rolled
         rc = (rc >> 2) | ((uint64_t)(code ^ 3u) << rcs);     // kmer.rs:87-91, rolled
         run = base_valid(c) ? run + 1 : 0;
-        const int start = i - (int)k + 1;
-        if (run >= k && start >= 0 && start < kSeg) emit(fwd < rc ? fwd : rc);  // kmer.rs:101
+        if (K) {
+            if (i >= K - 1) emit(i - K + 1, fwd < rc ? fwd : rc, run >= (uint32_t)K);  // kmer.rs:101
+        } else {
+            const int j = i - (int)k + 1;  // block-uniform condition
+            if (j >= 0 && j < SEG) emit(j, fwd < rc ? fwd : rc, run >= k);
+        }
     }
 }
 
-__global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq,
-                                                                ExtractGeom g,
-                                                                uint32_t *__restrict__ HC,
-                                                                ull *__restrict__ Hg) {
-    __shared__ uint32_t lh[kMaxL1Bins];
-    for (uint32_t b = threadIdx.x; b < g.nbins; b += kExtractBlock) lh[b] = 0;
+template <int K>
+__global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq, ExtractGeom g,
+                                                                uint32_t *__restrict__ HC, ull *__restrict__ Hg) {
+    __shared__ uint32_t lh[kMaxL1Bins + 1];  // + dummy bin for invalid windows
+    for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
     __syncthreads();
     const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
-    const uint32_t shift = g.shift;
-    for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
-        const uint64_t w0 = t0 + (uint64_t)threadIdx.x * kSeg;
+    const uint32_t shift = g.shift, nb = g.nbins;
+    for (uint64_t t0 = beg; t0 < end; t0 += kHTile) {
+        const uint64_t w0 = t0 + (uint64_t)threadIdx.x * kSegH;
         if (w0 < end)
-            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) { atomicAdd(&lh[bin_of(key, shift)], 1u); });
+            scan_windows<kSegH, K>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
+                atomicAdd(&lh[valid ? bin_of(key, shift) : nb], 1u);
+            });
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < g.nbins; b += kExtractBlock) {
+    for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
         const uint32_t h = lh[b];
-        HC[(uint64_t)blockIdx.x * g.nbins + b] = h;
+        HC[(uint64_t)blockIdx.x * nb + b] = h;
         if (h) atomicAdd(&Hg[b], (ull)h);
     }
 }
 
-__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t *__restrict__ seq,
-                                                                   ExtractGeom g,
+// Shared tail of the scatter tile: bin offsets within the tile.
+__device__ __forceinline__ uint32_t tile_offsets(uint32_t t, uint32_t nb, uint32_t *hist, uint32_t *lofs,
+                                                 uint32_t *lcur, ull *wsum) {
+    ull tile_n;
+    const uint32_t my = t < nb ? hist[t] : 0u;
+    const uint32_t off = (uint32_t)block_excl_scan<kExtractBlock>(my, wsum, &tile_n);
+    if (t < nb) {
+        lofs[t] = off;
+        lcur[t] = off;
+    }
+    return (uint32_t)tile_n;
+}
+
+template <int K>
+__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
                                                                    const uint32_t *__restrict__ HC,
                                                                    ull *__restrict__ cursor,
                                                                    uint64_t *__restrict__ out) {
-    __shared__ ull stage[kTile];
-    __shared__ ull gcur[kMaxL1Bins];     // this block's next output index per bin
-    __shared__ uint32_t hist[kMaxL1Bins];
-    __shared__ uint32_t lofs[kMaxL1Bins];  // tile-local start of each bin in `stage`
+    __shared__ ull stage[kTile + 64];        // + one dummy slot per lane for invalid windows (K > 0)
+    __shared__ ull gcur[kMaxL1Bins];         // this block's next output index per bin
+    __shared__ uint32_t hist[kMaxL1Bins + 1];
+    __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
     __shared__ uint32_t lcur[kMaxL1Bins];
     __shared__ ull wsum[kExtractBlock / 64];
     const uint32_t t = threadIdx.x;
@@ -134,27 +164,48 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
-        if (t < nb) hist[t] = 0;
+        if (t <= nb) hist[t] = 0;
         __syncthreads();
-        const uint64_t w0 = t0 + (uint64_t)t * kSeg;
-        if (w0 < end)
-            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) { atomicAdd(&hist[bin_of(key, shift)], 1u); });
-        __syncthreads();
-        ull tile_n;
-        const uint32_t my = t < nb ? hist[t] : 0u;
-        const uint32_t off = (uint32_t)block_excl_scan<kExtractBlock>(my, wsum, &tile_n);
-        if (t < nb) {
-            lofs[t] = off;
-            lcur[t] = off;
+        const uint64_t w0 = t0 + (uint64_t)t * kSegS;
+        const bool live = w0 < end;
+        uint32_t tile_n;
+        if (K) {
+            // one sweep: keys and their within-bin ranks stay in registers
+            ull kk[kSegS];
+            uint32_t rk[kSegS];  // bin << 16 | rank; invalid: nb << 16
+#pragma unroll
+            for (int j = 0; j < kSegS; ++j) rk[j] = nb << 16;
+            if (live)
+                scan_windows<kSegS, K>(seq, g.n, w0, g.k, [&](int j, uint64_t key, bool valid) {
+                    const uint32_t b = valid ? bin_of(key, shift) : nb;
+                    kk[j] = key;
+                    rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
+                });
+            __syncthreads();
+            tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kSegS; ++j) {
+                const uint32_t b = rk[j] >> 16;
+                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTile + (t & 63u);
+                stage[dst] = kk[j];
+            }
+        } else {
+            if (live)
+                scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
+                    atomicAdd(&hist[valid ? bin_of(key, shift) : nb], 1u);
+                });
+            __syncthreads();
+            tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+            __syncthreads();
+            if (live)
+                scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
+                    if (valid) stage[atomicAdd(&lcur[bin_of(key, shift)], 1u)] = key;
+                });
         }
         __syncthreads();
-        if (w0 < end)
-            scan_segment(seq, g.n, w0, g.k, [&](uint64_t key) {
-                stage[atomicAdd(&lcur[bin_of(key, shift)], 1u)] = key;
-            });
-        __syncthreads();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
-        for (uint32_t j = t; j < (uint32_t)tile_n; j += kExtractBlock) {
+        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
             const ull key = stage[j];
             const uint32_t b = bin_of(key, shift);
             out[gcur[b] + (j - lofs[b])] = key;
@@ -164,16 +215,39 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     }
 }
 
+// k values with a specialised instantiation (others use the runtime-k kernel)
+#define OKM_EXTRACT_KS(X) X(17) X(21) X(25) X(27) X(31) X(32)
+
 void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g, uint32_t *HC,
                          unsigned long long *Hg) {
-    hipLaunchKernelGGL(k_extract_hist, dim3(g.nblocks), dim3(kExtractBlock), 0, (hipStream_t)stream, seq, g,
-                       HC, Hg);
+    hipStream_t s = (hipStream_t)stream;
+    switch (g.k) {
+#define OKM_CASE(KV)                                                                                  \
+    case KV:                                                                                          \
+        hipLaunchKernelGGL(k_extract_hist<KV>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, Hg); \
+        return;
+        OKM_EXTRACT_KS(OKM_CASE)
+#undef OKM_CASE
+    default:
+        hipLaunchKernelGGL(k_extract_hist<0>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, Hg);
+    }
 }
 
 void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
                             const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys) {
-    hipLaunchKernelGGL(k_extract_scatter, dim3(g.nblocks), dim3(kExtractBlock), 0, (hipStream_t)stream, seq,
-                       g, HC, cursor, out_keys);
+    hipStream_t s = (hipStream_t)stream;
+    switch (g.k) {
+#define OKM_CASE(KV)                                                                                      \
+    case KV:                                                                                              \
+        hipLaunchKernelGGL(k_extract_scatter<KV>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, \
+                           cursor, out_keys);                                                             \
+        return;
+        OKM_EXTRACT_KS(OKM_CASE)
+#undef OKM_CASE
+    default:
+        hipLaunchKernelGGL(k_extract_scatter<0>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
+                           out_keys);
+    }
 }
 
 }  // namespace okm

@@ -16,7 +16,10 @@
 
 namespace okm {
 
-constexpr int kPartBlock = 256;
+#ifndef OKM_PART_BLOCK
+#define OKM_PART_BLOCK 1024
+#endif
+constexpr int kPartBlock = OKM_PART_BLOCK;  // scatter threads per workgroup (LDS-limited to 1 block/CU)
 constexpr int kLine = 16;      // keys per 128-B line
 constexpr int kLoadU = 8;      // keys per thread in flight per batch
 

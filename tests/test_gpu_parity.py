@@ -196,6 +196,7 @@ def test_compare_k_mismatch_cli(tmp_path):
     (31, 40_000, 150, 2_000_000), (21, 40_000, 150, 500_000), (32, 20_000, 150, 1_000_000),
     (15, 30_000, 100, 300_000), (5, 5_000, 150, 100_000), (1, 2_000, 50, 10_000), (2, 2_000, 50, 10_000),
     (11, 20_000, 150, 50_000), (31, 2_000, 5_000, 1_000_000),
+    (17, 20_000, 150, 400_000), (25, 20_000, 150, 400_000), (27, 20_000, 120, 400_000),
 ])
 def test_random_vs_oracle(k, n_reads, read_len, genome):
     batch = okm.synth_reads(n_reads, read_len, genome_len=genome, genome_seed=k, seed=100 + k,
