@@ -1,0 +1,110 @@
+"""Multi-process (gloo, CPU) tests of the owner-partitioned table merge,
+okm/dist.py.
+
+Each rank counts its own contiguous shard of reads (count.rs:23-38 is per
+record, so shards need no halo), the ranks exchange (key, count) runs by
+value-range owner, every owner re-counts its range, and the concatenation of
+the owners' ranges in rank order must equal the single-process table of all
+reads, bit for bit.  Local counting here is the C restatement
+(oracle/okm_oracle.c, test infrastructure) so the test runs without a GPU;
+bench.py runs the same exchange over RCCL with the HIP engine.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import okm
+from okm import dist as okm_dist
+from oracle import OracleCounter
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _reads(n_reads: int, read_len: int, seed: int) -> np.ndarray:
+    return okm.synth_reads(n_reads, read_len, genome_len=200_000, genome_seed=seed, seed=seed + 1,
+                           sub_rate=0.01, n_rate=0.001)
+
+
+def _oracle_merge(k):
+    def merge(rk: torch.Tensor, rc: torch.Tensor):
+        oc = OracleCounter(k)
+        if rk.numel():
+            oc.add_pairs(rk.numpy().view(np.uint64), rc.numpy().view(np.uint64))
+        mk, mc = oc.result(1)
+        return torch.from_numpy(mk.view(np.int64).copy()), torch.from_numpy(mc.view(np.int64).copy())
+    return merge
+
+
+def _worker(rank, world, port, k, n_reads, read_len, seed, empty_rank, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        batch = _reads(n_reads, read_len, seed)
+        recs = batch.reshape(n_reads, read_len + 1)
+        shard = np.array_split(recs, world)[rank]
+        oc = OracleCounter(k)
+        if rank != empty_rank and len(shard):
+            oc.add_separated(np.ascontiguousarray(shard).reshape(-1))
+        lk, lc = oc.result(1)
+        keys = torch.from_numpy(lk.view(np.int64).copy())
+        counts = torch.from_numpy(lc.view(np.int64).copy())
+        mk, mc = okm_dist.distributed_merge(keys, counts, k, _oracle_merge(k))
+        # owned ranges are sorted and disjoint, in rank order
+        gk, gc = okm_dist.gather_global(mk, mc)
+        if rank == 0:
+            np.savez(out_path, keys=gk, counts=gc)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, k, n_reads=6_000, read_len=150, seed=11, empty_rank=-1, tmp_path=None):
+    out = os.path.join(str(tmp_path), f"merged_{world}_{k}.npz")
+    mp.spawn(_worker, args=(world, _free_port(), k, n_reads, read_len, seed, empty_rank, out),
+             nprocs=world, join=True)
+    got = np.load(out)
+    batch = _reads(n_reads, read_len, seed)
+    recs = batch.reshape(n_reads, read_len + 1)
+    oc = OracleCounter(k)
+    for r, part in enumerate(np.array_split(recs, world)):
+        if r != empty_rank and len(part):
+            oc.add_separated(np.ascontiguousarray(part).reshape(-1))
+    ek, ec = oc.result(1)
+    return got["keys"], got["counts"], ek, ec
+
+
+@pytest.mark.parametrize("world,k", [(2, 31), (2, 32), (3, 21)])
+def test_owner_partitioned_merge_equals_single_table(world, k, tmp_path):
+    gk, gc, ek, ec = _run(world, k, tmp_path=tmp_path)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_merge_with_an_empty_rank(tmp_path):
+    gk, gc, ek, ec = _run(2, 25, empty_rank=1, tmp_path=tmp_path)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_owner_ranges_balance_and_cover():
+    rng = np.random.default_rng(0)
+    hist = rng.integers(0, 1000, 1 << 12)
+    for world in (1, 2, 3, 8):
+        b = okm_dist.owner_ranges(hist, world)
+        assert b[0] == 0 and b[-1] == len(hist) and len(b) == world + 1
+        assert all(x <= y for x, y in zip(b, b[1:]))
+        per = [hist[b[r]:b[r + 1]].sum() for r in range(world)]
+        assert max(per) - min(per) <= 2 * hist.max()
+    # all mass in one bin: one owner takes it, the others get empty ranges
+    h = np.zeros(64, np.int64)
+    h[7] = 100
+    b = okm_dist.owner_ranges(h, 4)
+    assert b[0] == 0 and b[-1] == 64 and sorted(b) == b
