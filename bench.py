@@ -52,6 +52,17 @@ GENOME_SEED = 2
 READ_SEED = 2
 
 
+def pmc_traffic():
+    """Newest committed rocprofv3 PMC traffic summary (tools/profile_round.sh):
+    HBM bytes per launch per kernel, read = 2 x FETCH_SIZE (gfx950), + WRITE_SIZE."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -173,9 +184,16 @@ def main():
         dom = max(kernels, key=lambda n: stats[n]["total_ms"])
         dk = kernels[dom]
         ach = dk["achieved_GBs"]
+        traffic, tsrc = pmc_traffic()
+        tk = (traffic or {}).get(dom)
         roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
+                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                "traffic": round(tk["traffic_bytes"]) if tk else None,
+                "traffic_unit": "bytes per launch (HBM, rocprofv3 PMC)",
+                "traffic_source": tsrc if tk else None,
                 "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"]}
+        if tk:
+            roof["traffic_GBs"] = round(tk["traffic_bytes"] / (dk["avg_ms"] * 1e-3) / 1e9, 1)
         tot_ms = sum(s["total_ms"] for s in stats.values())
         tot_bytes = sum(s["alg_bytes"] for s in stats.values())
         roof["path_achieved_GBs"] = round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1) if tot_ms > 0 else None
