@@ -337,12 +337,20 @@ static okm_status sync(okm_ctx *c) {
 }
 
 // Host prefix sum of a device histogram -> offsets (host) and device cursor.
-static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &off) {
+// align > 1: every bin's slot is rounded up to `align` keys (starts on a
+// 128-B line for align 16); *exact (if given) receives the unpadded total.
+static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &off, uint64_t align = 1,
+                                  uint64_t *exact = nullptr) {
     std::vector<unsigned long long> h(nb);
     HIP_TRY(hipMemcpyAsync(h.data(), c->Hg, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     off.assign(nb + 1, 0);
-    for (size_t b = 0; b < nb; ++b) off[b + 1] = off[b] + h[b];
+    uint64_t tot = 0;
+    for (size_t b = 0; b < nb; ++b) {
+        off[b + 1] = off[b] + (h[b] + align - 1) / align * align;
+        tot += h[b];
+    }
+    if (exact) *exact = tot;
     HIP_TRY(hipMemcpyAsync(c->cursor, off.data(), nb * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
     return OKM_OK;
 }
@@ -368,14 +376,16 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     HIP_TRY(hipGetLastError());
 
     Run run;
-    OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
+    uint64_t total = 0;  // bins start on 128-B lines; slot tails hold kEmptyKey
+    OKM_TRY(hist_to_offsets(c, c->nbins, run.off, 16, &total));
     c->hprof.mark("l1.hist+sync");
-    const uint64_t total = run.off.back();
     if (total == 0) return OKM_OK;
-    OKM_TRY(pool_get(c->pool, total, &run.keys));
+    OKM_TRY(pool_get(c->pool, run.off.back(), &run.keys));
     c->timer.begin(c->stream);
     launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys);
     c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * (double)total);
+    HIP_TRY(hipGetLastError());
+    launch_fill_line_tails(c->stream, c->cursor, c->nbins, run.keys);
     HIP_TRY(hipGetLastError());
     c->runs.push_back(std::move(run));
     c->info.kmers += total;

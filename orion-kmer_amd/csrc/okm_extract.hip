@@ -215,6 +215,19 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     }
 }
 
+__global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__ end, uint32_t nbins,
+                                                         uint64_t *__restrict__ keys) {
+    const uint32_t b = blockIdx.x * 16 + (threadIdx.x >> 4), j = threadIdx.x & 15;
+    if (b >= nbins) return;
+    const ull e = end[b];
+    if (e + j < ((e + 15) & ~15ull)) keys[e + j] = kEmptyKey;
+}
+
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys) {
+    hipLaunchKernelGGL(k_fill_line_tails, dim3((nbins + 15) / 16), dim3(256), 0, (hipStream_t)stream, end, nbins,
+                       keys);
+}
+
 // k values with a specialised instantiation (others use the runtime-k kernel)
 #define OKM_EXTRACT_KS(X) X(17) X(21) X(25) X(27) X(31) X(32)
 

@@ -73,6 +73,9 @@ void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, 
 void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks,
                          uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
                          unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts);
+// Pads [end[b], roundup(end[b], 16)) of every bin with kEmptyKey (bins start
+// on 16-key lines; end = the cursor after the scatter).
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys);
 uint32_t extract_tile();
 uint32_t extract_max_bins();
 uint32_t part_max_bins(bool weighted);
