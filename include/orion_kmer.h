@@ -64,8 +64,22 @@ typedef enum okm_status {
 
 typedef enum okm_mode {
     OKM_MODE_COUNT = 0,    /* count.rs: DashMap<u64, AtomicUsize> */
-    OKM_MODE_SET = 1       /* build.rs:50-58: DashSet<u64> */
+    OKM_MODE_SET = 1,      /* build.rs:50-58: DashSet<u64> */
+    /* Flag, OR-ed into the mode: opt into k in 33..64 (two-u64 keys, SURVEY
+     * §8 a3-a5 extension, BASELINE configs[3]).  Without it k > 32 fails with
+     * OKM_E_INVALID_K exactly like the reference (count.rs:43-45). */
+    OKM_MODE_WIDE = 0x100
 } okm_mode;
+
+/* A k-mer for k in 33..64: the same MSB-first 2-bit encoding as kmer.rs:37-57
+ * over 2k bits, value = hi * 2^64 + lo.  In a context created with k > 32
+ * every `keys` array of the calls below holds one okm_key128, i.e. two u64, per
+ * entry instead of one u64: okm_add_pairs[_device], okm_fetch_counts,
+ * okm_finish_counts / okm_finish_set, okm_result_device; so does
+ * okm_write_counts_tsv for k > 32. */
+typedef struct okm_key128 {
+    uint64_t lo, hi;
+} okm_key128;
 
 /* ------------------------------------------------------------------------
  * Library / device
@@ -195,6 +209,11 @@ int okm_u64_to_seq(uint64_t v, uint8_t k, char *out);
 uint64_t okm_reverse_complement_u64(uint64_t v, uint8_t k);
 /* kmer.rs:99-106 */
 uint64_t okm_canonical_u64(uint64_t v, uint8_t k);
+/* The k in 33..64 extension of the four (no reference: restatement-defined). */
+int okm_seq_to_u128(const uint8_t *seq, size_t len, uint8_t k, okm_key128 *out);
+int okm_u128_to_seq(okm_key128 v, uint8_t k, char *out);
+okm_key128 okm_reverse_complement_u128(okm_key128 v, uint8_t k);
+okm_key128 okm_canonical_u128(okm_key128 v, uint8_t k);
 
 /* ------------------------------------------------------------------------
  * Host record source — replaces needletail parse_fastx_reader + record
@@ -221,7 +240,8 @@ okm_status okm_parse_buffer(const uint8_t *data, uint64_t n, uint8_t **seq, uint
  * Output codecs — utils.rs:167-198 get_output_writer (.gz/.xz/.zst by
  * extension, else plain) and the TSV of count.rs:127-135.
  * ---------------------------------------------------------------------- */
-/* Writes "KMER\tCOUNT\n" lines for sorted (keys, counts). */
+/* Writes "KMER\tCOUNT\n" lines for sorted (keys, counts); k in 1..64 (keys
+ * are okm_key128 pairs for k > 32). */
 okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *keys,
                                 const uint64_t *counts, uint64_t n);
 /* Writes `n` raw bytes through the extension-selected compressor. */

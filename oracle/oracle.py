@@ -55,6 +55,20 @@ def load() -> ctypes.CDLL:
     lib.oracle_counter_windows.argtypes = [c_void_p]
     lib.oracle_counter_result.restype = c_uint64
     lib.oracle_counter_result.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]
+    lib.oracle_seq_to_u128.restype = c_int
+    lib.oracle_seq_to_u128.argtypes = [c_char_p, c_size_t, c_uint8, c_void_p]
+    lib.oracle_counter_wide_new.restype = c_void_p
+    lib.oracle_counter_wide_new.argtypes = [c_uint8]
+    lib.oracle_counter_wide_free.argtypes = [c_void_p]
+    lib.oracle_counter_wide_add_record.argtypes = [c_void_p, c_char_p, c_size_t, c_int]
+    lib.oracle_counter_wide_add_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int]
+    lib.oracle_counter_wide_add_pairs.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64]
+    lib.oracle_counter_wide_distinct.restype = c_uint64
+    lib.oracle_counter_wide_distinct.argtypes = [c_void_p]
+    lib.oracle_counter_wide_windows.restype = c_uint64
+    lib.oracle_counter_wide_windows.argtypes = [c_void_p]
+    lib.oracle_counter_wide_result.restype = c_uint64
+    lib.oracle_counter_wide_result.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]
     _lib = lib
     return lib
 
@@ -116,4 +130,50 @@ class OracleCounter:
         keys = np.empty(max(n, 1), dtype=np.uint64)
         counts = np.empty(max(n, 1), dtype=np.uint64)
         m = load().oracle_counter_result(self.h, min_count, keys.ctypes.data, counts.ctypes.data, n)
+        return keys[:m].copy(), counts[:m].copy()
+
+
+class OracleCounterWide(OracleCounter):
+    """k in 33..64 (restatement-defined two-u64 extension): keys are (n, 2)
+    uint64 arrays of [lo, hi] words, value = hi * 2**64 + lo."""
+
+    def __init__(self, k: int):
+        self.k = k
+        self.h = load().oracle_counter_wide_new(k)
+        if not self.h:
+            raise ValueError(f"Invalid K-mer size: {k}. Must be between 1 and 64.")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            load().oracle_counter_wide_free(self.h)
+            self.h = None
+
+    def add_records(self, seqs: Sequence[bytes], normalized: bool = False) -> None:
+        for s in seqs:
+            load().oracle_counter_wide_add_record(self.h, s, len(s), 1 if normalized else 0)
+
+    def add_batch(self, data: np.ndarray, offsets: np.ndarray, normalized: bool = False) -> None:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        load().oracle_counter_wide_add_batch(self.h, data.ctypes.data, offsets.ctypes.data, len(offsets) - 1,
+                                             1 if normalized else 0)
+
+    def add_pairs(self, keys: np.ndarray, counts: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64).reshape(-1, 2)
+        counts = np.ascontiguousarray(counts, dtype=np.uint64)
+        load().oracle_counter_wide_add_pairs(self.h, keys.ctypes.data, counts.ctypes.data, len(counts))
+
+    @property
+    def distinct(self) -> int:
+        return int(load().oracle_counter_wide_distinct(self.h))
+
+    @property
+    def windows(self) -> int:
+        return int(load().oracle_counter_wide_windows(self.h))
+
+    def result(self, min_count: int = 1) -> Tuple[np.ndarray, np.ndarray]:
+        n = self.distinct
+        keys = np.empty((max(n, 1), 2), dtype=np.uint64)
+        counts = np.empty(max(n, 1), dtype=np.uint64)
+        m = load().oracle_counter_wide_result(self.h, min_count, keys.ctypes.data, counts.ctypes.data, n)
         return keys[:m].copy(), counts[:m].copy()

@@ -136,7 +136,10 @@ static int parse(int argc, char **argv, const std::vector<OptSpec> &spec, int st
             continue;
         }
         if (!o->takes_value) {
-            if (std::string(o->lng) == "verbose") g_verbose++;
+            if (std::string(o->lng) == "verbose")
+                g_verbose++;
+            else
+                a.opts.emplace_back(o->lng, "1");
             continue;
         }
         if (!has_eq) {
@@ -194,7 +197,7 @@ static const char *kVersion = "orion-kmer 0.1.0";
 
 static void print_help(const std::string &cmd) {
     if (cmd == "count")
-        printf("Count k-mers in FASTA/FASTQ files\n\nUsage: orion-kmer count [OPTIONS] --kmer-size <KMER_SIZE> --input-files <INPUT_FILES>... --output-file <OUTPUT_FILE>\n\nOptions:\n  -k, --kmer-size <KMER_SIZE>      The length of the k-mer\n  -i, --input-files <INPUT_FILES>...  One or more input FASTA/FASTQ files. Supports .gz, .xz, .zst compression.\n  -o, --output-file <OUTPUT_FILE>  Output file for k-mer counts (kmer<TAB>count)\n  -m, --min-count <MIN_COUNT>      Minimum count to report a k-mer [default: 1]\n  -t, --threads <THREADS>          Number of threads to use (0 for all logical cores) [default: 0]\n  -v, --verbose...                 Verbosity level (e.g., -v, -vv)\n      --device <DEVICE>            GPU ordinal (MI355X engine) [default: 0]\n  -h, --help                       Print help\n  -V, --version                    Print version\n");
+        printf("Count k-mers in FASTA/FASTQ files\n\nUsage: orion-kmer count [OPTIONS] --kmer-size <KMER_SIZE> --input-files <INPUT_FILES>... --output-file <OUTPUT_FILE>\n\nOptions:\n  -k, --kmer-size <KMER_SIZE>      The length of the k-mer\n  -i, --input-files <INPUT_FILES>...  One or more input FASTA/FASTQ files. Supports .gz, .xz, .zst compression.\n  -o, --output-file <OUTPUT_FILE>  Output file for k-mer counts (kmer<TAB>count)\n  -m, --min-count <MIN_COUNT>      Minimum count to report a k-mer [default: 1]\n      --wide                       Allow k up to 64 (two-u64 keys; extension, not in the reference)\n  -t, --threads <THREADS>          Number of threads to use (0 for all logical cores) [default: 0]\n  -v, --verbose...                 Verbosity level (e.g., -v, -vv)\n      --device <DEVICE>            GPU ordinal (MI355X engine) [default: 0]\n  -h, --help                       Print help\n  -V, --version                    Print version\n");
     else if (cmd == "build")
         printf("Build a unique k-mer database from genome assemblies\n\nUsage: orion-kmer build [OPTIONS] --kmer-size <KMER_SIZE> --genomes <GENOME_FILES>... --output-file <OUTPUT_FILE>\n");
     else if (cmd == "compare")
@@ -235,7 +238,7 @@ static int feed_file(okm_ctx *ctx, const std::string &path, bool decompress_by_e
 
 static int open_engine(okm_ctx **ctx, uint8_t k, okm_mode mode) {
     okm_status s = okm_create(ctx, k, mode, g_device, 0);
-    if (s == OKM_E_INVALID_K) return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and 32.");
+    if (s == OKM_E_INVALID_K) return die(err_detail());  // errors.rs:6 text (or its k<=64 form with --wide)
     if (s != OKM_OK) return die("MI355X engine unavailable: " + err_detail());
     return 0;
 }
@@ -252,9 +255,14 @@ static int run_count(const Args &a) {
     uint64_t min_count = 1;
     if (get_one(a, "min-count", ms) && !parse_u64(ms, min_count))
         return usage_error("invalid value '" + ms + "' for '--min-count <MIN_COUNT>'");
-    if (k == 0 || k > 32) return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and 32.");
+    // --wide: opt-in two-u64 keys for k in 33..64 (not in the reference, whose
+    // error for k > 32 is kept byte-identical without it)
+    std::string wflag;
+    const bool wide = get_one(a, "wide", wflag);
+    if (k == 0 || k > (wide ? 64 : 32))
+        return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and " + (wide ? "64." : "32."));
     okm_ctx *ctx = nullptr;
-    if ((rc = open_engine(&ctx, k, OKM_MODE_COUNT))) return rc;
+    if ((rc = open_engine(&ctx, k, (okm_mode)(OKM_MODE_COUNT | (wide ? OKM_MODE_WIDE : 0))))) return rc;
     for (auto &p : inputs) {
         info("orion_kmer::commands::count", "Processing file: " + p);
         if ((rc = feed_file(ctx, p, true, "Failed to get input reader for file: "))) {
@@ -505,6 +513,7 @@ int main(int argc, char **argv) {
         spec.push_back({"input-files", 'i', true, true});
         spec.push_back({"output-file", 'o', true, false});
         spec.push_back({"min-count", 'm', true, false});
+        spec.push_back({"wide", 0, false, false});
     } else if (cmd == "build") {
         spec.push_back({"kmer-size", 'k', true, false});
         spec.push_back({"genomes", 'g', true, true});

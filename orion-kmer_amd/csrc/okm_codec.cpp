@@ -63,4 +63,47 @@ uint64_t okm_canonical_u64(uint64_t v, uint8_t k) {
     return v < rc ? v : rc;
 }
 
+// ---- k in 33..64: the same MSB-first encoding over 2k bits (restatement-defined)
+
+typedef unsigned __int128 u128;
+static inline u128 to128(okm_key128 v) { return ((u128)v.hi << 64) | v.lo; }
+static inline okm_key128 from128(u128 x) { return okm_key128{(uint64_t)x, (uint64_t)(x >> 64)}; }
+
+int okm_seq_to_u128(const uint8_t *seq, size_t len, uint8_t k, okm_key128 *out) {
+    if (k == 0 || k > 64 || len != (size_t)k || !seq) return 0;
+    u128 v = 0;
+    for (size_t i = 0; i < len; ++i) {
+        const int c = base_code(seq[i]);
+        if (c < 0) return 0;
+        v = (v << 2) | (u128)c;
+    }
+    if (out) *out = from128(v);
+    return 1;
+}
+
+int okm_u128_to_seq(okm_key128 v, uint8_t k, char *out) {
+    if (k == 0 || k > 64 || !out) return 0;
+    u128 x = to128(v);
+    for (int i = k - 1; i >= 0; --i) {
+        out[i] = "ACGT"[(unsigned)(x & 3u)];
+        x >>= 2;
+    }
+    return 1;
+}
+
+okm_key128 okm_reverse_complement_u128(okm_key128 v, uint8_t k) {
+    if (k == 0 || k > 64) return okm_key128{0, 0};
+    u128 x = to128(v), r = 0;
+    for (int i = 0; i < k; ++i) {  // kmer.rs:83-92 over 2k bits
+        r = (r << 2) | ((x & 3u) ^ 3u);
+        x >>= 2;
+    }
+    return from128(r);
+}
+
+okm_key128 okm_canonical_u128(okm_key128 v, uint8_t k) {
+    const okm_key128 rc = okm_reverse_complement_u128(v, k);
+    return to128(v) < to128(rc) ? v : rc;
+}
+
 }  // extern "C"

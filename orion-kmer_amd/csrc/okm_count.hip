@@ -126,6 +126,9 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
 __device__ __forceinline__ uint32_t home_of(uint64_t key, uint32_t r) {
     return (uint32_t)(key >> (r - kHomeBits)) & (kHomes - 1);
 }
+__device__ __forceinline__ uint32_t home_of(const K128 &key, uint32_t r) {
+    return (uint32_t)KeyOps<K128>::shr(key, r - kHomeBits) & (kHomes - 1);
+}
 
 // Packed u16 pair helpers (home h lives in word h >> 1, half h & 1).
 __device__ __forceinline__ uint32_t half_shift(uint32_t h) { return (h & 1u) << 4; }
@@ -140,13 +143,13 @@ __device__ __forceinline__ uint64_t item_total(const DevItem &it, const DevSeg *
 
 // Load a tag/full-mode item's instances into registers (flat index over its
 // segments; such items hold <= kCapI instances, so 32-bit indices).
-template <bool W>
-__device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__restrict__ segs, ull (&kk)[kPer],
+template <bool W, typename KT = ull>
+__device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__restrict__ segs, KT (&kk)[kPer],
                                           ull (&ww)[kPer]) {
     const uint32_t t = threadIdx.x;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-        kk[u] = kEmptyKey;
+        kk[u] = KeyOps<KT>::empty();
         ww[u] = 1;
     }
     uint32_t sbase = 0;
@@ -158,7 +161,7 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
             if ((uint32_t)u * kCB >= sbase + len) break;  // block-uniform: rows past the segment
             const uint32_t f = (uint32_t)u * kCB + t - sbase;  // wraps for f < sbase
             if (f < len) {
-                kk[u] = s.keys[f];
+                kk[u] = reinterpret_cast<const KT *>(s.keys)[f];
                 if (W && s.counts) ww[u] = s.counts[f];
             }
         }
@@ -167,13 +170,13 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
 }
 
 // Insertion sort of sk[a, a + n) (+ weights), n small.
-template <bool W>
-__device__ __forceinline__ void slice_sort(ull *sk, ull *sw, uint32_t a, uint32_t n) {
+template <bool W, typename KT>
+__device__ __forceinline__ void slice_sort(KT *sk, ull *sw, uint32_t a, uint32_t n) {
     for (uint32_t i = a + 1; i < a + n; ++i) {
-        const ull x = sk[i];
+        const KT x = sk[i];
         const ull xw = W ? sw[i] : 0ull;
         uint32_t j = i;
-        while (j > a && sk[j - 1] > x) {
+        while (j > a && KeyOps<KT>::lt(x, sk[j - 1])) {
             sk[j] = sk[j - 1];
             if (W) sw[j] = sw[j - 1];
             --j;
@@ -183,12 +186,13 @@ __device__ __forceinline__ void slice_sort(ull *sk, ull *sw, uint32_t a, uint32_
     }
 }
 
-__device__ __forceinline__ uint32_t slice_distinct(const ull *sk, uint32_t a, uint32_t n) {
+template <typename KT>
+__device__ __forceinline__ uint32_t slice_distinct(const KT *sk, uint32_t a, uint32_t n) {
     uint32_t d = 0;
-    ull prev = kEmptyKey;
+    KT prev = KeyOps<KT>::empty();
     for (uint32_t i = a; i < a + n; ++i) {
-        const ull x = sk[i];
-        d += x != prev;
+        const KT x = sk[i];
+        d += KeyOps<KT>::eq(x, prev) ? 0u : 1u;
         prev = x;
     }
     return d;
@@ -208,19 +212,20 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 // full mode (fallback): every instance counting-sorted by home
 // ---------------------------------------------------------------------------
 
-template <bool W>
+template <bool W, typename KT>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
-                                           ull *lds, uint32_t *wsum, uint64_t *__restrict__ out_keys,
-                                           uint64_t *__restrict__ out_counts) {
+                                              ull *lds, uint32_t *wsum, uint64_t *__restrict__ out_keys_raw,
+                                              uint64_t *__restrict__ out_counts) {
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
-    ull kk[kPer];
+    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
+    KT kk[kPer];
     ull ww[kPer];
-    load_item<W>(it, segs, kk, ww);
-    ull *sk = lds;
-    ull *sw = lds + kCapI;
-    uint32_t *hc = reinterpret_cast<uint32_t *>(lds + kCapI * (W ? 2 : 1));
+    load_item<W, KT>(it, segs, kk, ww);
+    KT *sk = reinterpret_cast<KT *>(lds);
+    ull *sw = reinterpret_cast<ull *>(sk + kCapI);
+    uint32_t *hc = reinterpret_cast<uint32_t *>(sw + (W ? kCapI : 0));
     __syncthreads();  // the previous item's LDS state is dead
     hc[2 * t] = 0;
     hc[2 * t + 1] = 0;
@@ -230,7 +235,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
     for (int u = 0; u < kPer; ++u) {
         if ((uint32_t)u >= nrows) break;  // block-uniform
         hp[u] = 0;
-        if (kk[u] != kEmptyKey) {
+        if (!KeyOps<KT>::is_empty(kk[u])) {
             const uint32_t h = home_of(kk[u], r);
             const uint32_t o = atomicAdd(&hc[h >> 1], 1u << half_shift(h));
             hp[u] = (h << 16) | half_of(o, h);
@@ -247,8 +252,8 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-        if ((uint32_t)u >= nrows) break;  // block-uniform
-        if (kk[u] != kEmptyKey) {
+        if ((uint32_t)u >= nrows) break;
+        if (!KeyOps<KT>::is_empty(kk[u])) {
             const uint32_t h = hp[u] >> 16;
             const uint32_t dst = half_of(hc[h >> 1], h) + (hp[u] & 0xFFFFu);
             sk[dst] = kk[u];
@@ -263,12 +268,12 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
     uint64_t o = out_off + od;  // DashMap value = instances (count.rs:33)
     uint32_t i = a;
     while (i < a + n) {
-        const ull key = sk[i];
+        const KT key = sk[i];
         ull c = 0;
         do {
             c += W ? sw[i] : 1ull;
             ++i;
-        } while (i < a + n && sk[i] == key);
+        } while (i < a + n && KeyOps<KT>::eq(sk[i], key));
         out_keys[o] = key;
         out_counts[o] = c;
         ++o;
@@ -471,35 +476,37 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 // dense mode: direct-address counters (rem_bits <= kDenseBits)
 // ---------------------------------------------------------------------------
 
-template <bool W>
+template <bool W, typename KT>
 __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *__restrict__ segs,
-                                               uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts,
+                                               uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
                                                ull *lds, uint32_t *wsum) {
     typedef typename CountType<W>::T CT;
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint32_t nslots = 1u << r;
     const ull mask = (ull)nslots - 1ull;
-    ull *slot_key = lds;                                      // [kHomes]
-    CT *cnt = reinterpret_cast<CT *>(lds + kHomes);           // [kHomes]
+    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
+    KT *slot_key = reinterpret_cast<KT *>(lds);               // [kHomes]
+    CT *cnt = reinterpret_cast<CT *>(slot_key + kHomes);      // [kHomes]
     __syncthreads();  // the previous item's LDS state is dead
     for (uint32_t j = t; j < nslots; j += kCB) cnt[j] = 0;
     __syncthreads();
     for (uint32_t sg = 0; sg < it.seg_count; ++sg) {
         const DevSeg s = segs[it.seg_begin + sg];
+        const KT *keys = reinterpret_cast<const KT *>(s.keys);
         for (uint64_t base = 0; base < s.len; base += (uint64_t)kCB * kLoadU) {
-            ull kk[kLoadU];
+            KT kk[kLoadU];
             CT ww[kLoadU];
 #pragma unroll
             for (int u = 0; u < kLoadU; ++u) {
                 const uint64_t idx = base + (uint64_t)u * kCB + t;
-                kk[u] = idx < s.len ? s.keys[idx] : kEmptyKey;
+                kk[u] = idx < s.len ? keys[idx] : KeyOps<KT>::empty();
                 ww[u] = (W && s.counts && idx < s.len) ? (CT)s.counts[idx] : (CT)1;
             }
 #pragma unroll
             for (int u = 0; u < kLoadU; ++u) {
-                if (kk[u] != kEmptyKey) {
-                    const uint32_t h = (uint32_t)(kk[u] & mask);
+                if (!KeyOps<KT>::is_empty(kk[u])) {
+                    const uint32_t h = (uint32_t)(KeyOps<KT>::shr(kk[u], 0) & mask);  // the key's remaining bits
                     atomicAdd(&cnt[h], ww[u]);
                     slot_key[h] = kk[u];  // all writers of a slot store the same key
                 }
@@ -563,25 +570,31 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     }
 }
 
-// Deferred items: dense mode, or full mode (every instance counting-sorted).
-template <bool W>
-__global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ items, const DevSeg *__restrict__ segs,
+// Deferred items (defer != nullptr: the ctl[1] items listed there), or every
+// item (defer == nullptr: wide keys, which have no tag mode — LDS has no
+// 128-bit CAS): dense mode, or full mode (every instance counting-sorted).
+template <typename KT, bool W>
+__global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ items, uint32_t nitems,
+                                                    const DevSeg *__restrict__ segs,
                                                     uint64_t *__restrict__ out_keys,
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                                                     ull *__restrict__ ctl, const uint32_t *__restrict__ defer) {
-    constexpr int kBytes = Lds<W>::kFullBytes > kHomes * 12 ? Lds<W>::kFullBytes : kHomes * 12;
+    constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2;
+    constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
+    constexpr int kBytes = kFull > kDense ? kFull : kDense;
     __shared__ __attribute__((aligned(16))) ull lds[kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
-    const uint32_t ndefer = *reinterpret_cast<volatile const unsigned int *>(ctl + 1);
+    const uint32_t ndefer = defer ? *reinterpret_cast<volatile const unsigned int *>(ctl + 1) : nitems;
     for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
-        const uint32_t item = defer[j];
+        const uint32_t item = defer ? defer[j] : j;
         const DevItem it = items[item];
         const uint64_t total = item_total(it, segs);
         uint32_t written = 0;
         if (it.rem_bits <= (uint32_t)kDenseBits) {
-            written = dense_item<W>(it, segs, out_keys, out_counts, lds, wsum);
+            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum);
         } else if (total <= (uint64_t)kCapI) {
-            written = full_item<W>(it, segs, (uint32_t)((total + kCB - 1) / kCB), lds, wsum, out_keys, out_counts);
+            written = full_item<W, KT>(it, segs, (uint32_t)((total + kCB - 1) / kCB), lds, wsum, out_keys,
+                                       out_counts);
         } else if (threadIdx.x == 0) {
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
         }
@@ -599,21 +612,31 @@ void count_prof_read(unsigned long long *out16) {
 
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, uint32_t *defer, bool weighted) {
+                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide) {
     if (!nitems) return;
+    hipStream_t s = (hipStream_t)stream;
+    if (wide) {  // every item through the full / dense modes
+        const uint32_t grid = nitems < 4096u ? nitems : 4096u;
+        if (weighted)
+            hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr);
+        else
+            hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr);
+        return;
+    }
     const uint32_t grid = nitems < 4096u ? nitems : 4096u;
     const uint32_t sgrid = nitems < 1024u ? nitems : 1024u;  // exits at once when nothing was deferred
-    hipStream_t s = (hipStream_t)stream;
     if (weighted) {
         hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer);
-        hipLaunchKernelGGL(k_count_slow<true>, dim3(sgrid), dim3(kCB), 0, s, items, segs, out_keys, out_counts,
-                           n_out, ctl, defer);
+        hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
+                           out_counts, n_out, ctl, (const uint32_t *)defer);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer);
-        hipLaunchKernelGGL(k_count_slow<false>, dim3(sgrid), dim3(kCB), 0, s, items, segs, out_keys, out_counts,
-                           n_out, ctl, defer);
+        hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
+                           out_counts, n_out, ctl, (const uint32_t *)defer);
     }
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "okm_internal.h"
+#include "okm_key.h"
 
 namespace okm {
 

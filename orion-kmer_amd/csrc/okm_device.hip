@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
                                                     const uint64_t *__restrict__ lk,
                                                     const uint64_t *__restrict__ lc, DevItem *__restrict__ items,
                                                     DevSeg *__restrict__ segs, uint64_t item_max,
-                                                    uint32_t capbits, ull *__restrict__ flags) {
+                                                    uint32_t capbits, ull *__restrict__ flags, uint32_t kw) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nout) return;
     // parent = last part whose first output bin is <= i
@@ -87,12 +87,12 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     const uint32_t rem = parents[lo].rem;
     const ull o = offs[i], len = offs[i + 1] - o;
     DevSeg s;
-    s.keys = lk + o;
+    s.keys = lk + o * kw;
     s.counts = lc ? lc + o : nullptr;
     s.len = len;
     s.key_base = 0;
     s.out_base = 0;
-    s.shift = 64;
+    s.shift = kSingleBin;
     s.nlocal = 1;
     s.pad = 0;
     segs[i] = s;
@@ -109,22 +109,23 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
 
 void launch_make_items(void *stream, const ull *offs, uint32_t nout, const DevParent *parents, uint32_t nparents,
                        const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs, uint64_t item_max,
-                       uint32_t capbits, ull *flags) {
+                       uint32_t capbits, ull *flags, uint32_t kw) {
     if (!nout) return;
     hipLaunchKernelGGL(k_make_items, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, offs, nout,
-                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags);
+                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw);
 }
 
 // ---------------------------------------------------------------------------
 // Result assembly
 // ---------------------------------------------------------------------------
 
+template <typename KT>
 __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict__ items,
                                                        uint32_t nitems, const ull *__restrict__ n_out,
                                                        const ull *__restrict__ dense_off,
-                                                       const uint64_t *__restrict__ sk,
+                                                       const KT *__restrict__ sk,
                                                        const uint64_t *__restrict__ sc,
-                                                       uint64_t *__restrict__ dk,
+                                                       KT *__restrict__ dk,
                                                        uint64_t *__restrict__ dc) {
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
@@ -138,11 +139,17 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts, uint64_t *dst_keys,
-                          uint64_t *dst_counts) {
+                          uint64_t *dst_counts, bool wide) {
     if (!nitems) return;
     const uint32_t grid = nitems < 8192u ? nitems : 8192u;
-    hipLaunchKernelGGL(k_compact_items, dim3(grid), dim3(256), 0, (hipStream_t)stream, items,
-                       nitems, n_out, dense_off, src_keys, src_counts, dst_keys, dst_counts);
+    if (wide)
+        hipLaunchKernelGGL(k_compact_items<K128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
+                           dense_off, reinterpret_cast<const K128 *>(src_keys), src_counts,
+                           reinterpret_cast<K128 *>(dst_keys), dst_counts);
+    else
+        hipLaunchKernelGGL(k_compact_items<ull>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
+                           dense_off, reinterpret_cast<const ull *>(src_keys), src_counts,
+                           reinterpret_cast<ull *>(dst_keys), dst_counts);
 }
 
 constexpr int kFilterBlock = 256;
@@ -164,9 +171,10 @@ __global__ __launch_bounds__(kFilterBlock) void k_filter_count(const uint64_t *_
     if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
 }
 
+template <typename KT>
 __global__ __launch_bounds__(kFilterBlock) void k_filter_scatter(
-    const uint64_t *__restrict__ keys, const uint64_t *__restrict__ counts, uint64_t n,
-    uint64_t min_count, const ull *__restrict__ block_offsets, uint64_t *__restrict__ dk,
+    const KT *__restrict__ keys, const uint64_t *__restrict__ counts, uint64_t n,
+    uint64_t min_count, const ull *__restrict__ block_offsets, KT *__restrict__ dk,
     uint64_t *__restrict__ dc) {
     __shared__ ull wsum[kFilterBlock / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kFilterTile + (uint64_t)threadIdx.x * kFilterPer;
@@ -194,30 +202,37 @@ void launch_filter_count(void *stream, const uint64_t *counts, uint64_t n, uint6
 
 void launch_filter_scatter(void *stream, const uint64_t *keys, const uint64_t *counts, uint64_t n,
                            uint64_t min_count, const unsigned long long *block_offsets,
-                           uint64_t *dst_keys, uint64_t *dst_counts) {
+                           uint64_t *dst_keys, uint64_t *dst_counts, bool wide) {
     const uint32_t nb = filter_blocks(n);
     if (!nb) return;
-    hipLaunchKernelGGL(k_filter_scatter, dim3(nb), dim3(kFilterBlock), 0, (hipStream_t)stream, keys,
-                       counts, n, min_count, block_offsets, dst_keys, dst_counts);
+    if (wide)
+        hipLaunchKernelGGL(k_filter_scatter<K128>, dim3(nb), dim3(kFilterBlock), 0, (hipStream_t)stream,
+                           reinterpret_cast<const K128 *>(keys), counts, n, min_count, block_offsets,
+                           reinterpret_cast<K128 *>(dst_keys), dst_counts);
+    else
+        hipLaunchKernelGGL(k_filter_scatter<ull>, dim3(nb), dim3(kFilterBlock), 0, (hipStream_t)stream,
+                           reinterpret_cast<const ull *>(keys), counts, n, min_count, block_offsets,
+                           reinterpret_cast<ull *>(dst_keys), dst_counts);
 }
 
 // ---------------------------------------------------------------------------
 // |A ∩ B| for compare.rs:58
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_intersect_count(const uint64_t *__restrict__ a,
-                                                         uint64_t na, const uint64_t *__restrict__ b,
-                                                         uint64_t nb, ull *__restrict__ out) {
+template <typename KT>
+__global__ __launch_bounds__(256) void k_intersect_count(const KT *__restrict__ a, uint64_t na,
+                                                         const KT *__restrict__ b, uint64_t nb,
+                                                         ull *__restrict__ out) {
     __shared__ ull wsum[4];
     ull hits = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < na; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t x = a[i];
+        const KT x = a[i];
         uint64_t lo = 0, hi = nb;
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if (b[mid] < x) lo = mid + 1; else hi = mid;
+            if (KeyOps<KT>::lt(b[mid], x)) lo = mid + 1; else hi = mid;
         }
-        hits += (lo < nb && b[lo] == x);
+        hits += (lo < nb && KeyOps<KT>::eq(b[lo], x));
     }
     ull total;
     block_excl_scan<256>(hits, wsum, &total);
@@ -225,12 +240,16 @@ __global__ __launch_bounds__(256) void k_intersect_count(const uint64_t *__restr
 }
 
 void launch_intersect_count(void *stream, const uint64_t *a, uint64_t na, const uint64_t *b,
-                            uint64_t nb, unsigned long long *out) {
+                            uint64_t nb, unsigned long long *out, bool wide) {
     if (!na || !nb) return;
     uint64_t g = (na + 255) / 256;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(k_intersect_count, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream, a, na,
-                       b, nb, out);
+    if (wide)
+        hipLaunchKernelGGL(k_intersect_count<K128>, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const K128 *>(a), na, reinterpret_cast<const K128 *>(b), nb, out);
+    else
+        hipLaunchKernelGGL(k_intersect_count<ull>, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const ull *>(a), na, reinterpret_cast<const ull *>(b), nb, out);
 }
 
 }  // namespace okm

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "okm_internal.h"
+#include "okm_key.h"
 
 namespace okm {
 
@@ -253,6 +254,8 @@ struct okm_ctx {
     okm_mode mode = OKM_MODE_COUNT;
     hipStream_t stream = nullptr;
     uint32_t l1_bits = 0, nbins = 1, shift1 = 64;
+    bool wide = false;   // k > 32: K128 keys (two u64 per key)
+    uint32_t kw = 1;     // u64 words per key
 
     DevPool pool;
     std::vector<Run> runs;
@@ -376,16 +379,16 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     HIP_TRY(hipGetLastError());
 
     Run run;
-    uint64_t total = 0;  // bins start on 128-B lines; slot tails hold kEmptyKey
-    OKM_TRY(hist_to_offsets(c, c->nbins, run.off, 16, &total));
+    uint64_t total = 0;  // bins start on 128-B lines; slot tails hold the empty key
+    OKM_TRY(hist_to_offsets(c, c->nbins, run.off, 16 / c->kw, &total));
     c->hprof.mark("l1.hist+sync");
     if (total == 0) return OKM_OK;
-    OKM_TRY(pool_get(c->pool, run.off.back(), &run.keys));
+    OKM_TRY(pool_get(c->pool, run.off.back() * c->kw, &run.keys));
     c->timer.begin(c->stream);
     launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys);
-    c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * (double)total);
+    c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * c->kw * (double)total);
     HIP_TRY(hipGetLastError());
-    launch_fill_line_tails(c->stream, c->cursor, c->nbins, run.keys);
+    launch_fill_line_tails(c->stream, c->cursor, c->nbins, run.keys, c->wide);
     HIP_TRY(hipGetLastError());
     c->runs.push_back(std::move(run));
     c->info.kmers += total;
@@ -396,7 +399,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
 struct Part {
     uint32_t seg_begin, seg_count;  // into the host segment table
     uint64_t len;
-    uint64_t prefix;                // absolute key prefix at `consumed` bits
+    unsigned __int128 prefix;       // absolute key prefix at `consumed` bits (2k <= 128)
     uint32_t consumed;
 };
 
@@ -432,8 +435,8 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
         max_local = std::max(max_local, nl);
         for (uint32_t s = 0; s < p.seg_count; ++s) {
             DevSeg d = segtab[p.seg_begin + s];
-            d.shift = twok - p.consumed - b;
-            d.key_base = p.prefix << b;
+            d.shift = b ? twok - p.consumed - b : kSingleBin;
+            d.key_base = (uint64_t)(p.prefix << b);  // local_bin works modulo 2^64
             d.out_base = L.out_base[t];
             d.nlocal = nl;
             const uint32_t sid = (uint32_t)psegs.size();
@@ -462,8 +465,8 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
     const double kb = weighted ? 16.0 : 8.0;
     c->timer.begin(c->stream);
-    launch_part_hist(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->Hg);
-    c->timer.end(c->stream, "part_hist", 8.0 * (double)total);
+    launch_part_hist(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->Hg, c->wide);
+    c->timer.end(c->stream, "part_hist", 8.0 * c->kw * (double)total);
     HIP_TRY(hipGetLastError());
     // bin offsets on the device; only the total crosses to the host
     launch_exclusive_scan(c->stream, c->Hg, L.d_offs, (uint64_t)nout + 1, scan_tmp);
@@ -474,15 +477,16 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     OKM_TRY(sync(c));
     c->hprof.mark("split.hist_sync");
     L.padded = padded;  // bins start on 128-B lines (okm_partition.hip)
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1), &L.lk));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1) * c->kw, &L.lk));
     level_bufs.push_back(L.lk);
     if (weighted) {
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1), &L.lc));
         level_bufs.push_back(L.lc);
     }
     c->timer.begin(c->stream);
-    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->cursor, L.lk, L.lc);
-    c->timer.end(c->stream, "part_scatter", 2.0 * kb * (double)total);
+    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, c->HC, c->cursor, L.lk, L.lc,
+                        c->wide);
+    c->timer.end(c->stream, "part_scatter", 2.0 * (kb + 8.0 * (c->kw - 1)) * (double)total);
     HIP_TRY(hipGetLastError());
     c->info.levels += 1;
     return OKM_OK;
@@ -508,10 +512,10 @@ static okm_status split_children_host(okm_ctx *c, const Level &L, std::vector<De
                 const uint64_t len = off[ob + 1] - off[ob];
                 if (!len) continue;
                 DevSeg d{};
-                d.keys = L.lk + off[ob];
+                d.keys = L.lk + off[ob] * c->kw;
                 d.counts = L.lc ? L.lc + off[ob] : nullptr;
                 d.len = len;
-                d.shift = 64;
+                d.shift = kSingleBin;
                 d.nlocal = 1;
                 Part ch{(uint32_t)segtab.size(), 1, len, (p.prefix << b) | l, p.consumed + b};
                 segtab.push_back(d);
@@ -563,10 +567,10 @@ static okm_status do_count(okm_ctx *c) {
             const uint64_t len = r.off[b + 1] - r.off[b];
             if (!len) continue;
             DevSeg d{};
-            d.keys = r.keys + r.off[b];
+            d.keys = r.keys + r.off[b] * c->kw;
             d.counts = r.counts ? r.counts + r.off[b] : nullptr;
             d.len = len;
-            d.shift = 64;
+            d.shift = kSingleBin;
             d.nlocal = 1;
             segtab.push_back(d);
             p.seg_count++;
@@ -624,7 +628,7 @@ static okm_status do_count(okm_ctx *c) {
             HIP_TRY(hipMemcpyAsync(d_par, par.data(), par.size() * sizeof(DevParent), hipMemcpyHostToDevice, c->stream));
             HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
             launch_make_items(c->stream, L.d_offs, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc, d_items, d_segs,
-                              item_max, capbits, flags);
+                              item_max, capbits, flags, c->kw);
             HIP_TRY(hipGetLastError());
             unsigned long long hf[2];
             HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
@@ -691,7 +695,7 @@ static okm_status do_count(okm_ctx *c) {
         OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
         OKM_TRY(pool_get(c->pool, nitems, &d_items));
     }
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sk));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
@@ -707,7 +711,7 @@ static okm_status do_count(okm_ctx *c) {
     HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted);
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide);
     c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
@@ -720,10 +724,10 @@ static okm_status do_count(okm_ctx *c) {
     if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     const uint64_t nd = hv[0];
     if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
     c->timer.begin(c->stream);
-    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts);
+    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide);
     c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
     HIP_TRY(hipGetLastError());
     OKM_TRY(sync(c));
@@ -814,8 +818,13 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     (void)distinct_hint;
     if (!out) return fail(OKM_E_ARG, "okm_create: out is NULL");
     *out = nullptr;
-    if (k == 0 || k > 32)
-        return fail(OKM_E_INVALID_K, "Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and 32.");
+    const bool wide_ok = (mode & OKM_MODE_WIDE) != 0;  // opt-in two-u64 extension (k <= 64)
+    mode = (okm_mode)(mode & ~OKM_MODE_WIDE);
+    if (k == 0 || k > 32) {
+        if (!wide_ok || k == 0 || k > 64)
+            return fail(OKM_E_INVALID_K, "Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and " +
+                                             (wide_ok ? "64." : "32."));
+    }
     if (mode != OKM_MODE_COUNT && mode != OKM_MODE_SET) return fail(OKM_E_ARG, "okm_create: bad mode");
     std::string why;
     if (!device_ok(device, &why)) return fail(OKM_E_DEVICE, why);
@@ -824,6 +833,8 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->device = device;
     c->k = k;
     c->mode = mode;
+    c->wide = k > 32;
+    c->kw = c->wide ? 2 : 1;
     c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins()), 2u * k);
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
@@ -947,15 +958,16 @@ okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64
     OKM_TRY(ensure_hg(c, c->nbins));
     HIP_TRY(hipMemsetAsync(c->Hg, 0, c->nbins * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
-    launch_part_hist(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->Hg);
-    c->timer.end(c->stream, "part_hist", 8.0 * (double)n);
+    launch_part_hist(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->Hg, c->wide);
+    c->timer.end(c->stream, "part_hist", 8.0 * c->kw * (double)n);
     HIP_TRY(hipGetLastError());
     Run run;
     OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1) * c->kw, &run.keys));
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
     c->timer.begin(c->stream);
-    launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys, run.counts);
+    launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys,
+                        run.counts, c->wide);
     c->timer.end(c->stream, "part_scatter", 32.0 * (double)n);
     HIP_TRY(hipGetLastError());
     OKM_TRY(sync(c));
@@ -971,9 +983,9 @@ okm_status okm_add_pairs(okm_ctx *c, const uint64_t *keys, const uint64_t *count
     if (!keys) return fail(OKM_E_ARG, "okm_add_pairs: null keys");
     HIP_TRY(hipSetDevice(c->device));
     uint64_t *dk = nullptr, *dc = nullptr;
-    OKM_TRY(pool_get(c->pool, n, &dk));
+    OKM_TRY(pool_get(c->pool, n * c->kw, &dk));
     if (counts) OKM_TRY(pool_get(c->pool, n, &dc));
-    HIP_TRY(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dk, keys, n * 8 * c->kw, hipMemcpyHostToDevice, c->stream));
     if (counts) HIP_TRY(hipMemcpyAsync(dc, counts, n * 8, hipMemcpyHostToDevice, c->stream));
     okm_status s = okm_add_pairs_device(c, dk, dc, n);
     c->pool.put(dk);
@@ -1048,9 +1060,9 @@ okm_status okm_fetch_counts(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint
             return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
         }
         if (m) {
-            OKM_TRY(pool_get(c->pool, m, &tk));
+            OKM_TRY(pool_get(c->pool, m * c->kw, &tk));
             OKM_TRY(pool_get(c->pool, m, &tc));
-            launch_filter_scatter(c->stream, c->res_keys, c->res_counts, c->n_res, min_count, bo, tk, tc);
+            launch_filter_scatter(c->stream, c->res_keys, c->res_counts, c->n_res, min_count, bo, tk, tc, c->wide);
             HIP_TRY(hipGetLastError());
         }
         c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
@@ -1061,7 +1073,7 @@ okm_status okm_fetch_counts(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint
     }
     if (m) {
         const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-        if (keys) HIP_TRY(hipMemcpyAsync(keys, src_k, m * 8, kind, c->stream));
+        if (keys) HIP_TRY(hipMemcpyAsync(keys, src_k, m * 8 * c->kw, kind, c->stream));
         if (counts) HIP_TRY(hipMemcpyAsync(counts, src_c, m * 8, kind, c->stream));
     }
     OKM_TRY(sync(c));
@@ -1077,7 +1089,7 @@ okm_status okm_finish_counts(okm_ctx *c, uint64_t min_count, uint64_t **keys, ui
     if (counts) *counts = nullptr;
     uint64_t m = 0;
     OKM_TRY(okm_result_size(c, min_count, &m));
-    uint64_t *hk = (uint64_t *)std::malloc(std::max<uint64_t>(m, 1) * 8);
+    uint64_t *hk = (uint64_t *)std::malloc(std::max<uint64_t>(m, 1) * 8 * c->kw);
     uint64_t *hc = counts ? (uint64_t *)std::malloc(std::max<uint64_t>(m, 1) * 8) : nullptr;
     if (!hk || (counts && !hc)) {
         std::free(hk);
@@ -1131,7 +1143,7 @@ okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint6
             status = fail(OKM_E_DEVICE, "okm_set_intersection_size: copy");
             break;
         }
-        launch_intersect_count(st, da, sna, db, snb, dout);
+        launch_intersect_count(st, da, sna, db, snb, dout, false);
         unsigned long long h = 0;
         if (hipMemcpyAsync(&h, dout, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess) {

@@ -223,9 +223,142 @@ __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__
     if (e + j < ((e + 15) & ~15ull)) keys[e + j] = kEmptyKey;
 }
 
-void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys) {
-    hipLaunchKernelGGL(k_fill_line_tails, dim3((nbins + 15) / 16), dim3(256), 0, (hipStream_t)stream, end, nbins,
-                       keys);
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide);
+
+// ---------------------------------------------------------------------------
+// k in 33..64: two-u64 keys (K128, MSB-first over 2k bits), runtime k
+// ---------------------------------------------------------------------------
+
+constexpr int kSegW = 16;                       // scatter windows per thread
+constexpr int kTileW = kExtractBlock * kSegW;   // 4096 windows: 64 KiB stage
+
+template <int SEG, typename Emit>
+__device__ __forceinline__ void scan_windows_wide(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
+                                                  uint32_t k, Emit &&emit) {
+    constexpr int LOAD = SEG + 64;  // covers SEG + k - 1 for k <= 64
+    uint32_t w[LOAD / 4];
+    if (w0 + LOAD <= n) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
+#pragma unroll
+        for (int q = 0; q < LOAD / 16; ++q) {
+            const uint4 v = p[q];
+            w[4 * q + 0] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < LOAD / 4; ++q) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t idx = w0 + 4 * q + b;
+                x |= (idx < n ? (uint32_t)seq[idx] : 0u) << (8 * b);
+            }
+            w[q] = x;
+        }
+    }
+    const uint32_t hbits = 2 * k - 64;  // bits of the key in `hi` (k > 32)
+    const ull hmask = hbits >= 64 ? ~0ull : ((1ull << hbits) - 1ull);
+    const uint32_t rcs = 2 * k - 2 - 64;  // rc's new base lands in `hi`
+    K128 fwd{0, 0}, rc{0, 0};
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < LOAD - 1; ++i) {
+        const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+        const uint32_t code = base_code(c);
+        fwd.hi = ((fwd.hi << 2) | (fwd.lo >> 62)) & hmask;       // kmer.rs:51 over 2k bits
+        fwd.lo = (fwd.lo << 2) | code;
+        rc.lo = (rc.lo >> 2) | (rc.hi << 62);                     // kmer.rs:87-91 over 2k bits
+        rc.hi = (rc.hi >> 2) | ((ull)(code ^ 3u) << rcs);
+        run = base_valid(c) ? run + 1 : 0;
+        const int j = i - (int)k + 1;  // block-uniform condition
+        if (j >= 0 && j < SEG) emit(j, KeyOps<K128>::lt(fwd, rc) ? fwd : rc, run >= k);
+    }
+}
+
+__device__ __forceinline__ uint32_t bin_of_wide(const K128 &key, uint32_t shift) {
+    return shift >= 128 ? 0u : (uint32_t)KeyOps<K128>::shr(key, shift);
+}
+
+__global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8_t *__restrict__ seq, ExtractGeom g,
+                                                                     uint32_t *__restrict__ HC,
+                                                                     ull *__restrict__ Hg) {
+    __shared__ uint32_t lh[kMaxL1Bins + 1];
+    for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
+    const uint32_t shift = g.shift, nb = g.nbins;
+    for (uint64_t t0 = beg; t0 < end; t0 += kHTile) {
+        const uint64_t w0 = t0 + (uint64_t)threadIdx.x * kSegH;
+        if (w0 < end)
+            scan_windows_wide<kSegH>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
+                atomicAdd(&lh[valid ? bin_of_wide(key, shift) : nb], 1u);
+            });
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
+        const uint32_t h = lh[b];
+        HC[(uint64_t)blockIdx.x * nb + b] = h;
+        if (h) atomicAdd(&Hg[b], (ull)h);
+    }
+}
+
+__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const uint8_t *__restrict__ seq,
+                                                                        ExtractGeom g,
+                                                                        const uint32_t *__restrict__ HC,
+                                                                        ull *__restrict__ cursor,
+                                                                        K128 *__restrict__ out) {
+    __shared__ K128 stage[kTileW];
+    __shared__ ull gcur[kMaxL1Bins];
+    __shared__ uint32_t hist[kMaxL1Bins + 1];
+    __shared__ uint32_t lofs[kMaxL1Bins];
+    __shared__ uint32_t lcur[kMaxL1Bins];
+    __shared__ ull wsum[kExtractBlock / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t nb = g.nbins;
+    if (t < nb) {
+        const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
+        gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
+    const uint32_t shift = g.shift;
+    for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
+        if (t <= nb) hist[t] = 0;
+        __syncthreads();
+        const uint64_t w0 = t0 + (uint64_t)t * kSegW;
+        const bool live = w0 < end;
+        if (live)
+            scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
+                atomicAdd(&hist[valid ? bin_of_wide(key, shift) : nb], 1u);
+            });
+        __syncthreads();
+        const uint32_t tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+        __syncthreads();
+        if (live)
+            scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
+                if (valid) stage[atomicAdd(&lcur[bin_of_wide(key, shift)], 1u)] = key;
+            });
+        __syncthreads();
+        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
+            const K128 key = stage[j];
+            const uint32_t b = bin_of_wide(key, shift);
+            out[gcur[b] + (j - lofs[b])] = key;
+        }
+        __syncthreads();
+        if (t < nb) gcur[t] += hist[t];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill_line_tails_wide(const ull *__restrict__ end, uint32_t nbins,
+                                                              K128 *__restrict__ keys) {
+    const uint32_t b = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
+    if (b >= nbins) return;
+    const ull e = end[b];
+    if (e + j < ((e + 7) & ~7ull)) keys[e + j] = KeyOps<K128>::empty();
 }
 
 // k values with a specialised instantiation (others use the runtime-k kernel)
@@ -234,6 +367,10 @@ void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_
 void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g, uint32_t *HC,
                          unsigned long long *Hg) {
     hipStream_t s = (hipStream_t)stream;
+    if (g.k > 32) {
+        hipLaunchKernelGGL(k_extract_hist_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, Hg);
+        return;
+    }
     switch (g.k) {
 #define OKM_CASE(KV)                                                                                  \
     case KV:                                                                                          \
@@ -249,6 +386,11 @@ void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g,
 void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
                             const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys) {
     hipStream_t s = (hipStream_t)stream;
+    if (g.k > 32) {
+        hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
+                           reinterpret_cast<K128 *>(out_keys));
+        return;
+    }
     switch (g.k) {
 #define OKM_CASE(KV)                                                                                      \
     case KV:                                                                                              \
@@ -261,6 +403,15 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
         hipLaunchKernelGGL(k_extract_scatter<0>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
                            out_keys);
     }
+}
+
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide) {
+    if (wide)
+        hipLaunchKernelGGL(k_fill_line_tails_wide, dim3((nbins + 31) / 32), dim3(256), 0, (hipStream_t)stream, end,
+                           nbins, reinterpret_cast<K128 *>(keys));
+    else
+        hipLaunchKernelGGL(k_fill_line_tails, dim3((nbins + 15) / 16), dim3(256), 0, (hipStream_t)stream, end,
+                           nbins, keys);
 }
 
 }  // namespace okm

@@ -28,7 +28,7 @@ struct DevSeg {
     uint64_t len;
     uint64_t key_base;       // (key >> shift) - key_base = local bin in [0, nlocal)
     uint32_t out_base;       // first output bin of this segment (compact numbering)
-    uint32_t shift;          // 64 => a single bin
+    uint32_t shift;          // kSingleBin (255) => a single bin
     uint32_t nlocal;         // bins this segment splits into (<= pass maximum)
     uint32_t pad;
 };
@@ -68,14 +68,15 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
 
 // Generic key-range partition pass over a chunk list.  max_local bounds every
 // segment's nlocal; HC is nchunks x max_local.
+// wide: keys are K128 (two u64 each; pointers stay uint64_t*, lengths count keys).
 void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
-                      uint32_t max_local, uint32_t *HC, unsigned long long *Hg);
+                      uint32_t max_local, uint32_t *HC, unsigned long long *Hg, bool wide);
 void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks,
                          uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
-                         unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts);
-// Pads [end[b], roundup(end[b], 16)) of every bin with kEmptyKey (bins start
-// on 16-key lines; end = the cursor after the scatter).
-void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys);
+                         unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts, bool wide);
+// Pads [end[b], roundup(end[b], line)) of every bin with the empty key (bins
+// start on 128-B lines: 16 u64 / 8 K128 keys; end = the cursor after the scatter).
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide);
 uint32_t extract_tile();
 uint32_t extract_max_bins();
 uint32_t part_max_bins(bool weighted);
@@ -96,7 +97,7 @@ uint32_t count_dense_bits();
 // kernel of the launch.
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, uint32_t *defer, bool weighted);
+                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide);
 
 // A part that took part in a device-side split round: its children are the
 // output bins [out_base, out_base + nlocal) of the round.
@@ -110,24 +111,24 @@ struct DevParent {
 // too big for one item; flags[1] = max child length.
 void launch_make_items(void *stream, const unsigned long long *offs, uint32_t nout, const DevParent *parents,
                        uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
-                       uint64_t item_max, uint32_t capbits, unsigned long long *flags);
+                       uint64_t item_max, uint32_t capbits, unsigned long long *flags, uint32_t kw);
 
 // Gather the per-item results into dense arrays given exclusive offsets.
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts,
-                          uint64_t *dst_keys, uint64_t *dst_counts);
+                          uint64_t *dst_keys, uint64_t *dst_counts, bool wide);
 
 // Filter (count >= min) with order preserved; flags/scan in tmp.
 void launch_filter_count(void *stream, const uint64_t *counts, uint64_t n, uint64_t min_count,
                          unsigned long long *block_counts, uint32_t nblocks_hint);
 void launch_filter_scatter(void *stream, const uint64_t *keys, const uint64_t *counts, uint64_t n,
                            uint64_t min_count, const unsigned long long *block_offsets,
-                           uint64_t *dst_keys, uint64_t *dst_counts);
+                           uint64_t *dst_keys, uint64_t *dst_counts, bool wide);
 uint32_t filter_blocks(uint64_t n);
 
 // |A ∩ B| of sorted unique arrays (merge-path style binary search per element).
 void launch_intersect_count(void *stream, const uint64_t *a, uint64_t na, const uint64_t *b,
-                            uint64_t nb, unsigned long long *out);
+                            uint64_t nb, unsigned long long *out, bool wide);
 
 }  // namespace okm

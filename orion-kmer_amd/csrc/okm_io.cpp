@@ -467,11 +467,30 @@ size_t format_counts_tsv(uint8_t k, const uint64_t *keys, const uint64_t *counts
     const char *t = base4_table();
     out.clear();
     out.reserve(n * (k + 8));
-    char line[64];
+    char line[112];
     for (size_t i = 0; i < n; ++i) {
+        int pos = 0;
+        if (k > 32) {  // two-u64 keys {lo, hi}: base i from bits 2(k-1-i) of hi:lo
+            const uint64_t lo = keys[2 * i], hi = keys[2 * i + 1];
+            for (int j = 0; j < k; ++j) {
+                const unsigned b = 2 * (k - 1 - j);
+                line[pos++] = "ACGT"[(b >= 64 ? (hi >> (b - 64)) : (lo >> b)) & 3];
+            }
+            line[pos++] = '\t';
+            char num[24];
+            int nd = 0;
+            uint64_t c = counts[i];
+            do {
+                num[nd++] = (char)('0' + c % 10);
+                c /= 10;
+            } while (c);
+            while (nd) line[pos++] = num[--nd];
+            line[pos++] = '\n';
+            out.append(line, pos);
+            continue;
+        }
         const uint64_t v = keys[i];
         // u64_to_seq (kmer.rs:61-75): base i from bits 2(k-1-i)
-        int pos = 0;
         int rem = k;
         while (rem >= 4) {
             const unsigned shift = 2 * (rem - 4);
@@ -508,7 +527,7 @@ extern "C" {
 okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *keys, const uint64_t *counts,
                                 uint64_t n) {
     if (!path) return fail(OKM_E_ARG, "null path");
-    if (k == 0 || k > 32) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
+    if (k == 0 || k > 64) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
     OutWriter w;
     okm_status s = w.open(path);
     if (s != OKM_OK) return s;
@@ -516,7 +535,7 @@ okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *key
     const uint64_t step = 1 << 20;
     for (uint64_t o = 0; o < n; o += step) {
         const uint64_t m = std::min(step, n - o);
-        format_counts_tsv(k, keys + o, counts + o, m, buf);
+        format_counts_tsv(k, keys + o * (k > 32 ? 2 : 1), counts + o, m, buf);
         s = w.write(buf.data(), buf.size());
         if (s != OKM_OK) return s;
     }

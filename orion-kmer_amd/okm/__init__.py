@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (OKM_E_DEVICE, OKM_E_INVALID_K, OKM_E_IO, OKM_E_PARSE, OKM_E_RECORD,
-                   OKM_MODE_COUNT, OKM_MODE_SET, OKM_OK, RECORD_SEPARATOR, OkmError, check)
+                   OKM_MODE_COUNT, OKM_MODE_SET, OKM_MODE_WIDE, OKM_OK, RECORD_SEPARATOR, OkmError, check)
 
 __all__ = [
     "seq_to_u64", "u64_to_seq", "reverse_complement_u64", "canonical_u64",
@@ -66,6 +66,47 @@ def canonical_u64(v: int, k: int) -> int:
     if k <= 0 or k > 32:
         raise ValueError(f"Invalid k-mer length for reverse complement: {k}")
     return int(lib().okm_canonical_u64(v, k))
+
+
+def _k128(v: int) -> "_lib.Key128":
+    return _lib.Key128(v & 0xFFFFFFFFFFFFFFFF, v >> 64)
+
+
+def seq_to_u128(seq: bytes, k: int) -> Optional[int]:
+    """k in 1..64 extension of seq_to_u64 (restatement-defined for k > 32)."""
+    out = _lib.Key128(0, 0)
+    if k < 0 or k > 255:
+        return None
+    ok = lib().okm_seq_to_u128(bytes(seq), len(seq), k, byref(out))
+    return (out.hi << 64 | out.lo) if ok else None
+
+
+def u128_to_seq(v: int, k: int) -> bytes:
+    if k <= 0 or k > 64:
+        raise ValueError(f"Invalid k-mer length for decoding: {k}")
+    buf = ctypes.create_string_buffer(k)
+    lib().okm_u128_to_seq(_k128(v), k, buf)
+    return buf.raw
+
+
+def reverse_complement_u128(v: int, k: int) -> int:
+    if k <= 0 or k > 64:
+        raise ValueError(f"Invalid k-mer length for reverse complement: {k}")
+    r = lib().okm_reverse_complement_u128(_k128(v), k)
+    return r.hi << 64 | r.lo
+
+
+def canonical_u128(v: int, k: int) -> int:
+    if k <= 0 or k > 64:
+        raise ValueError(f"Invalid k-mer length for reverse complement: {k}")
+    r = lib().okm_canonical_u128(_k128(v), k)
+    return r.hi << 64 | r.lo
+
+
+def keys128_to_int(keys: np.ndarray) -> List[int]:
+    """(n, 2) [lo, hi] uint64 key arrays -> Python ints."""
+    keys = np.asarray(keys, dtype=np.uint64).reshape(-1, 2)
+    return [(int(h) << 64) | int(l) for l, h in keys]
 
 
 # ---------------------------------------------------------------------------
@@ -165,9 +206,10 @@ def read_fastx_file(path: str, decompress_by_extension: bool = True) -> List[byt
 
 
 def write_counts_tsv(path: str, k: int, keys: np.ndarray, counts: np.ndarray) -> None:
+    """keys: uint64 (k <= 32) or (n, 2) [lo, hi] (k in 33..64)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
     counts = np.ascontiguousarray(counts, dtype=np.uint64)
-    check(lib().okm_write_counts_tsv(path.encode(), k, keys.ctypes.data, counts.ctypes.data, len(keys)),
+    check(lib().okm_write_counts_tsv(path.encode(), k, keys.ctypes.data, counts.ctypes.data, len(counts)),
           "okm_write_counts_tsv")
 
 
@@ -188,12 +230,17 @@ def synth_reads(n_reads: int, read_len: int = 150, genome_len: int = 100_000_000
 class KmerCounter:
     """The GPU replacement of ``DashMap<u64, AtomicUsize>`` (count.rs:48) and
     of process_sequence_chunk (count.rs:23-38).  mode='set' mirrors build.rs's
-    DashSet."""
+    DashSet.  k in 33..64 needs wide=True (the opt-in two-u64 extension; the
+    reference rejects k > 32): keys are then (n, 2) uint64 arrays [lo, hi]."""
 
-    def __init__(self, k: int, mode: str = "count", device: int = 0, distinct_hint: int = 0):
+    def __init__(self, k: int, mode: str = "count", device: int = 0, distinct_hint: int = 0,
+                 wide: bool = False):
         self.k = k
+        self.wide = bool(wide) and k > 32
         self.ctx = c_void_p()
         m = OKM_MODE_SET if mode == "set" else OKM_MODE_COUNT
+        if wide:
+            m |= OKM_MODE_WIDE
         check(lib().okm_create(byref(self.ctx), k, m, device, distinct_hint), "okm_create")
 
     def close(self) -> None:
@@ -234,10 +281,11 @@ class KmerCounter:
 
     def add_pairs(self, keys: np.ndarray, counts: Optional[np.ndarray] = None) -> None:
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        n = keys.shape[0] if not self.wide else keys.size // 2
         if counts is not None:
             counts = np.ascontiguousarray(counts, dtype=np.uint64)
         check(lib().okm_add_pairs(self.ctx, keys.ctypes.data,
-                                  counts.ctypes.data if counts is not None else None, len(keys)),
+                                  counts.ctypes.data if counts is not None else None, n),
               "okm_add_pairs")
 
     def add_pairs_device(self, d_keys: int, d_counts: Optional[int], n: int) -> None:
@@ -253,7 +301,7 @@ class KmerCounter:
         """Sorted (keys, counts) with count >= min_count (count.rs:106-119)."""
         n = c_uint64()
         check(lib().okm_result_size(self.ctx, min_count, byref(n)), "okm_result_size")
-        keys = np.empty(n.value, dtype=np.uint64)
+        keys = np.empty((n.value, 2) if self.wide else n.value, dtype=np.uint64)
         counts = np.empty(n.value, dtype=np.uint64)
         got = c_uint64()
         check(lib().okm_fetch_counts(self.ctx, min_count, keys.ctypes.data, counts.ctypes.data, n.value,

@@ -34,6 +34,7 @@ OKM_E_FORMAT = 11
 
 OKM_MODE_COUNT = 0
 OKM_MODE_SET = 1
+OKM_MODE_WIDE = 0x100  # flag: k in 33..64 (two-u64 keys)
 RECORD_SEPARATOR = ord("\n")
 
 
@@ -52,6 +53,11 @@ class EngineInfo(Structure):
     _fields_ = [("kmers", c_uint64), ("distinct", c_uint64), ("l1_bits", c_uint32),
                 ("l2_bits", c_uint32), ("levels", c_uint32), ("work_items", c_uint32),
                 ("max_partition", c_uint64), ("device_bytes", c_uint64)]
+
+
+class Key128(Structure):
+    """okm_key128: value = hi * 2**64 + lo."""
+    _fields_ = [("lo", c_uint64), ("hi", c_uint64)]
 
 
 _P64 = POINTER(c_uint64)
@@ -91,6 +97,10 @@ PROTOTYPES = {
     "okm_u64_to_seq": (c_int, [c_uint64, c_uint8, POINTER(c_char)]),
     "okm_reverse_complement_u64": (c_uint64, [c_uint64, c_uint8]),
     "okm_canonical_u64": (c_uint64, [c_uint64, c_uint8]),
+    "okm_seq_to_u128": (c_int, [c_char_p, c_size_t, c_uint8, POINTER(Key128)]),
+    "okm_u128_to_seq": (c_int, [Key128, c_uint8, c_char_p]),
+    "okm_reverse_complement_u128": (Key128, [Key128, c_uint8]),
+    "okm_canonical_u128": (Key128, [Key128, c_uint8]),
     "okm_reader_open": (c_int, [POINTER(c_void_p), c_char_p, c_int]),
     "okm_reader_next": (c_int, [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_void_p), _P64]),
     "okm_reader_records": (c_uint64, [c_void_p]),
