@@ -163,8 +163,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
                         const uint32_t b = local_bin(kk[u], s);
                         const uint32_t pos = atomicAdd(&fill[b], 1u);
                         if (pos < (uint32_t)L) {
-                            buf[b * L + pos] = kk[u];
-                            if (W) cbuf[b * L + pos] = ww[u];
+                            // slot order inside a line is free: swizzle it by the bin so
+                            // that lanes filling the same position of different bins hit
+                            // different LDS banks (bins are 128 B apart)
+                            const uint32_t sl = b * L + (pos ^ (b & (L - 1)));
+                            buf[sl] = kk[u];
+                            if (W) cbuf[sl] = ww[u];
                             pend &= ~(1u << u);
                         }
                     }
@@ -186,8 +190,9 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
             const uint32_t f = fill[b];
             if (f) {
                 for (uint32_t q = f; q < (uint32_t)L; ++q) {
-                    buf[b * L + q] = KeyOps<KT>::empty();
-                    if (W) cbuf[b * L + q] = 0;
+                    const uint32_t sl = b * L + (q ^ (b & (L - 1)));
+                    buf[sl] = KeyOps<KT>::empty();
+                    if (W) cbuf[sl] = 0;
                 }
                 const ull g = gcur[b];
                 flush_line<KT, W>(buf + b * L, cbuf + b * L, out_keys + g, W ? out_counts + g : nullptr);

@@ -9,8 +9,8 @@ from okm import _lib
 reads = int(sys.argv[1]) if len(sys.argv) > 1 else 3355443
 lib = _lib.load()
 buf = okm.synth_reads(reads, 150, genome_len=100_000_000, genome_seed=1, seed=2, sub_rate=0.001, n_rate=0.0001)
-names = {0: "loop_top", 8: "unused", 1: "load", 2: "tag CAS+count(+load wait)", 3: "rest offsets", 4: "rest scatter",
-         5: "tags+slice sort(t0)", 6: "scan(wait slowest)", 7: "emit(t0)", 9: "n_out+fallback/dense"}
+names = {0: "loop_top", 8: "unused", 1: "load issue", 2: "P1 tag CAS+counts (+load wait)", 3: "P2 rest offsets", 4: "P3 rest scatter",
+         5: "P4 rest analysis", 6: "P5 home offsets", 7: "P6 emit", 9: "reset+n_out"}
 out = (ctypes.c_ulonglong * 16)()
 with okm.KmerCounter(31) as c:
     dev = okm.DeviceBuffer(len(buf))
