@@ -21,8 +21,15 @@ namespace okm {
 #define OKM_PART_BLOCK 1024
 #endif
 constexpr int kPartBlock = OKM_PART_BLOCK;  // threads per workgroup (scatter: LDS-limited to 1 block/CU)
-constexpr int kLoadU = 8;      // keys per thread in flight per scatter batch
+#ifndef OKM_PART_LOADU
+#define OKM_PART_LOADU 8
+#endif
+constexpr int kLoadU = OKM_PART_LOADU;  // keys per thread in flight per scatter batch
 constexpr int kHistU = 4;      // 16-B loads per thread in flight (histogram)
+
+#ifndef OKM_PART_TILE
+#define OKM_PART_TILE 1  // 1: LDS tile counting sort (exact runs, no padding); 0: per-bin line buffers
+#endif
 
 template <typename KT> struct Line {
     static constexpr int kKeys = 128 / (int)sizeof(KT);  // keys per 128-B line
@@ -40,6 +47,7 @@ __device__ __forceinline__ uint32_t local_bin(const KT &key, const DevSeg &s) {
 
 template <typename KT>
 __device__ __forceinline__ ull pad_line(ull n) {
+    if (OKM_PART_TILE) return n;  // tile scatter: exact placement, no line padding
     constexpr int L = Line<KT>::kKeys;
     return (n + L - 1) & ~(ull)(L - 1);
 }
@@ -202,6 +210,92 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
     }
 }
 
+// Tile variant: every 64-Ki-key chunk is processed in LDS tiles that are
+// counting-sorted by local bin, and each bin's run leaves as one contiguous
+// stretch of the chunk's exact slice (no padding, no append rounds).
+template <typename KT, bool W> struct Tile {
+    // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state
+    static constexpr int kKeys = (W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : 16384);
+    static constexpr int kPer = kKeys / kPartBlock;
+};
+
+template <typename KT, bool W>
+__global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
+    const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
+    uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
+    uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts) {
+    constexpr int T = Tile<KT, W>::kKeys, P = Tile<KT, W>::kPer;
+    extern __shared__ __attribute__((aligned(16))) ull lds[];
+    KT *stage = reinterpret_cast<KT *>(lds);                              // [T]
+    ull *cstage = reinterpret_cast<ull *>(stage + T);                     // [T] (W)
+    ull *gcur = W ? cstage + T : cstage;                                  // [max_local]
+    uint32_t *hist = reinterpret_cast<uint32_t *>(gcur + max_local);      // [max_local]
+    uint32_t *lofs = hist + max_local;                                    // [max_local]
+    __shared__ ull wsum[kPartBlock / 64];
+    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
+    const uint32_t t = threadIdx.x;
+
+    for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const DevChunk ch = chunks[c];
+        const DevSeg s = segs[ch.seg];
+        const uint32_t nl = s.nlocal;
+        for (uint32_t b = t; b < nl; b += kPartBlock) {
+            const uint32_t h = HC[(uint64_t)c * max_local + b];
+            gcur[b] = h ? atomicAdd(&cursor[s.out_base + b], (ull)h) : 0ull;
+        }
+        const KT *keys = reinterpret_cast<const KT *>(s.keys) + ch.begin;
+        const uint64_t *cnts = s.counts ? s.counts + ch.begin : nullptr;
+        for (uint64_t base = 0; base < ch.len; base += T) {
+            for (uint32_t b = t; b < nl; b += kPartBlock) hist[b] = 0;
+            __syncthreads();
+            KT kk[P];
+            ull ww[P];
+            uint32_t br[P];  // bin << 16 | rank; ~0 = empty
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const uint64_t idx = base + (uint64_t)u * kPartBlock + t;
+                kk[u] = idx < ch.len ? keys[idx] : KeyOps<KT>::empty();
+                ww[u] = (W && idx < ch.len) ? (cnts ? cnts[idx] : 1ull) : 1ull;
+            }
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                br[u] = ~0u;
+                if (!KeyOps<KT>::is_empty(kk[u])) {
+                    const uint32_t b = local_bin(kk[u], s);
+                    br[u] = (b << 16) | atomicAdd(&hist[b], 1u);
+                }
+            }
+            __syncthreads();
+            // tile-local bin offsets (nl <= kPartBlock: one bin per thread)
+            const uint32_t my = t < nl ? hist[t] : 0u;
+            ull tile_n;
+            const uint32_t off = (uint32_t)block_excl_scan<kPartBlock>(my, wsum, &tile_n);
+            if (t < nl) lofs[t] = off;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                if (br[u] != ~0u) {
+                    const uint32_t dst = lofs[br[u] >> 16] + (br[u] & 0xFFFFu);
+                    stage[dst] = kk[u];
+                    if (W) cstage[dst] = ww[u];
+                }
+            }
+            __syncthreads();
+            // each bin's run is contiguous in `stage` and in the output slice
+            for (uint32_t j = t; j < (uint32_t)tile_n; j += kPartBlock) {
+                const KT key = stage[j];
+                const uint32_t b = local_bin(key, s);
+                const ull o = gcur[b] + (j - lofs[b]);
+                out_keys[o] = key;
+                if (W) out_counts[o] = cstage[j];
+            }
+            __syncthreads();
+            if (t < nl) gcur[t] += hist[t];
+        }
+        __syncthreads();
+    }
+}
+
 static uint32_t part_grid(uint32_t nchunks) { return nchunks < 4096u ? nchunks : 4096u; }
 
 void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
@@ -229,6 +323,26 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
                                   hipFuncAttributeMaxDynamicSharedMemorySize, optin);
         (void)hipGetLastError();  // an unsupported attribute must not poison later checks
         attr_done = true;
+    }
+    if (OKM_PART_TILE) {
+        static bool attr_tile = false;
+        if (!attr_tile) {
+            int dev = 0, optin = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess ||
+                optin <= 0)
+                optin = 64 * 1024;
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, optin);
+            (void)hipGetLastError();
+            attr_tile = true;
+        }
+        constexpr int T = Tile<KT, W>::kKeys;
+        const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) +
+                           (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
+        hipLaunchKernelGGL((k_part_scatter_tile<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
+                           (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+        return;
     }
     constexpr int L = Line<KT>::kKeys;
     const size_t lds = (size_t)max_local * (128 + (W ? L * sizeof(ull) : 0) + sizeof(ull) + sizeof(uint32_t));
