@@ -86,7 +86,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    device = local
+    # one rank per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
+    device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
