@@ -89,8 +89,14 @@ def main():
     # one rank per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
+    # nccl (= RCCL over xGMI) is the product path; OKM_BENCH_BACKEND=gloo rehearses
+    # the same exchange through host memory (RCCL refuses two ranks on one GPU)
+    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     # ---- synthetic batch for this rank, made resident in HBM ---------------
     t0 = time.time()
@@ -108,20 +114,51 @@ def main():
     if world > 1:
         from okm import dist as okm_dist
 
+    class _DevView:  # zero-copy int64 view of an engine-owned device array
+        def __init__(self, ptr, n):
+            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False),
+                                             "version": 3, "strides": None}
+
+    zero_copy = [True]
+
+    def table_tensors(n):
+        """The counted table as int64 device tensors: views of the engine's
+        result arrays when torch takes __cuda_array_interface__, else a copy."""
+        if zero_copy[0] and n:
+            kp, cp, _ = ctr.result_device()
+            try:
+                return (torch.as_tensor(_DevView(kp, n), device="cuda"),
+                        torch.as_tensor(_DevView(cp, n), device="cuda"))
+            except Exception as e:  # pragma: no cover - torch build without the protocol
+                log(f"note: no zero-copy device views ({e}); copying the table")
+                zero_copy[0] = False
+        keys = torch.empty(n, dtype=torch.int64, device="cuda")
+        counts = torch.empty(n, dtype=torch.int64, device="cuda")
+        if n:
+            ctr.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
+        return keys, counts
+
     def step():
         ctr.reset()
         ctr.add_device_batch(dbuf.address, len(batch))
         n = ctr.count()
         if world == 1:
             return n
-        keys = torch.empty(n, dtype=torch.int64, device="cuda")
-        counts = torch.empty(n, dtype=torch.int64, device="cuda")
-        ctr.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
-        rk, rc, _ = okm_dist.exchange(keys, counts, K)
+        keys, counts = table_tensors(n)
+        if backend == "nccl":
+            rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
+        else:
+            rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
+            rk, rc = rk.cuda(), rc.cuda()
         torch.cuda.synchronize()
+        # each rank's slice is sorted: the owner counts them in place (no copy,
+        # no partition pass; okm_add_sorted_pairs_device)
         merger.reset()
-        if rk.numel():
-            merger.add_pairs_device(rk.data_ptr(), rc.data_ptr(), rk.numel())
+        off = 0
+        for sz in rs:
+            if sz:
+                merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
+            off += sz
         return merger.count()
 
     def barrier_sync():
@@ -142,7 +179,7 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t_start
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     stats = ctr.kernel_stats() if not args.no_timing else {}

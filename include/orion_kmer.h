@@ -130,6 +130,14 @@ okm_status okm_add_pairs_device(okm_ctx *ctx, const uint64_t *d_keys, const uint
                                 uint64_t n);
 /* Same, from HOST memory. */
 okm_status okm_add_pairs(okm_ctx *ctx, const uint64_t *keys, const uint64_t *counts, uint64_t n);
+/* (key, count) pairs in DEVICE memory whose keys are strictly ascending — e.g.
+ * a slice of another context's okm_result_device table, as received by the
+ * owner of a key range in the multi-GPU merge.  No copy: the buffers are
+ * borrowed and must stay alive and unchanged until okm_count returns.  When
+ * every input is sorted, counting splits them by binary search instead of
+ * partitioning them (counts add, as in okm_add_pairs_device). */
+okm_status okm_add_sorted_pairs_device(okm_ctx *ctx, const uint64_t *d_keys, const uint64_t *d_counts,
+                                       uint64_t n);
 
 /* Run the counting over everything added so far; *n_distinct receives the
  * number of distinct canonical k-mers (DashMap::len()).  Idempotent until the

@@ -116,6 +116,115 @@ void launch_make_items(void *stream, const ull *offs, uint32_t nout, const DevPa
 }
 
 // ---------------------------------------------------------------------------
+// Sorted runs (okm_add_sorted_pairs_device): key ranges by binary search
+// ---------------------------------------------------------------------------
+
+template <typename KT>
+__device__ __forceinline__ uint64_t lower_bound_bin(const KT *keys, uint64_t lo, uint64_t hi, uint32_t shift,
+                                                    uint64_t base, uint64_t target) {
+    // first j in [lo, hi) with (key_j >> shift) - base >= target (keys sorted; modulo 2^64 is exact
+    // because every key of the range lies in the part whose prefix `base` describes)
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint64_t x = (shift >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(keys[mid], shift)) - base;
+        if (x < target) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+template <typename KT>
+__global__ void k_bin_bounds(const KT *__restrict__ keys, uint64_t n, uint32_t shift, uint32_t nbins,
+                             ull *__restrict__ out) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nbins) return;
+    out[b] = b == nbins ? n : lower_bound_bin(keys, 0, n, shift, 0, b);
+}
+
+void launch_bin_bounds(void *stream, const uint64_t *keys, uint64_t n, uint32_t shift, uint32_t nbins,
+                       unsigned long long *out, bool wide) {
+    const dim3 g((nbins + 1 + 255) / 256), b(256);
+    if (wide)
+        hipLaunchKernelGGL(k_bin_bounds<K128>, g, b, 0, (hipStream_t)stream, reinterpret_cast<const K128 *>(keys), n,
+                           shift, nbins, out);
+    else
+        hipLaunchKernelGGL(k_bin_bounds<ull>, g, b, 0, (hipStream_t)stream, reinterpret_cast<const ull *>(keys), n,
+                           shift, nbins, out);
+}
+
+// One thread per item: item i is child c of part parts[p] (split by `bits`);
+// its segment in run r is the child's key range within rbins[p * nruns + r].
+template <typename KT>
+__global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t nparts, uint32_t nitems,
+                               const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1, uint32_t kw,
+                               DevItem *__restrict__ items, DevSeg *__restrict__ segs, ull *__restrict__ itemtot,
+                               uint64_t item_max, uint32_t capbits, ull *__restrict__ flags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems) return;
+    uint32_t lo = 0, hi = nparts;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (parts[mid].item_base <= i) lo = mid; else hi = mid;
+    }
+    const DevSortedPart P = parts[lo];
+    const uint32_t c = i - P.item_base;
+    const uint32_t shift = shift1 - P.bits;                 // child = next `bits` key bits
+    const uint64_t base = (uint64_t)P.bin << P.bits;       // (key >> shift) - base = child index
+    ull tot = 0;
+    for (uint32_t r = 0; r < nruns; ++r) {
+        const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
+        const KT *k = reinterpret_cast<const KT *>(rb.keys);
+        const uint64_t s0 = P.bits ? lower_bound_bin(k, 0, rb.len, shift, base, c) : 0;
+        const uint64_t s1 = P.bits && c + 1 < (1u << P.bits) ? lower_bound_bin(k, s0, rb.len, shift, base, c + 1) : rb.len;
+        DevSeg sg;
+        sg.keys = rb.keys + s0 * kw;
+        sg.counts = rb.counts ? rb.counts + s0 : nullptr;
+        sg.len = s1 - s0;
+        sg.key_base = 0;
+        sg.out_base = 0;
+        sg.shift = kSingleBin;
+        sg.nlocal = 1;
+        sg.pad = 0;
+        segs[(uint64_t)i * nruns + r] = sg;
+        tot += s1 - s0;
+    }
+    DevItem it;
+    it.seg_begin = i * nruns;
+    it.seg_count = nruns;
+    it.out_off = 0;  // set from the scan of itemtot (k_set_out_off)
+    it.rem_bits = shift;
+    it.pad = 0;
+    items[i] = it;
+    itemtot[i] = tot;
+    if (tot > item_max && shift > capbits) atomicAdd(&flags[0], 1ull);
+    atomicMax(&flags[1], tot);
+}
+
+__global__ void k_set_out_off(DevItem *__restrict__ items, uint32_t nitems, const ull *__restrict__ off) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nitems) items[i].out_off = off[i];
+}
+
+void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
+                         const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
+                         unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
+                         bool wide) {
+    if (!nitems) return;
+    const dim3 g((nitems + 255) / 256), b(256);
+    if (wide)
+        hipLaunchKernelGGL(k_sorted_items<K128>, g, b, 0, (hipStream_t)stream, parts, nparts, nitems, rbins, nruns,
+                           shift1, 2u, items, segs, itemtot, item_max, capbits, flags);
+    else
+        hipLaunchKernelGGL(k_sorted_items<ull>, g, b, 0, (hipStream_t)stream, parts, nparts, nitems, rbins, nruns,
+                           shift1, 1u, items, segs, itemtot, item_max, capbits, flags);
+}
+
+void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off) {
+    if (!nitems) return;
+    hipLaunchKernelGGL(k_set_out_off, dim3((nitems + 255) / 256), dim3(256), 0, (hipStream_t)stream, items, nitems,
+                       off);
+}
+
+// ---------------------------------------------------------------------------
 // Result assembly
 // ---------------------------------------------------------------------------
 

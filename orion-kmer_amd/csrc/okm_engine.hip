@@ -242,6 +242,9 @@ struct Run {
     uint64_t *keys = nullptr;
     uint64_t *counts = nullptr;  // null: every key weighs 1
     std::vector<uint64_t> off;   // nbins + 1 offsets
+    uint64_t n = 0;              // keys (sorted runs)
+    bool sorted = false;         // strictly ascending unique keys (okm_add_sorted_pairs_device)
+    bool borrowed = false;       // caller-owned memory: never returned to the pool
 };
 
 }  // namespace okm
@@ -539,9 +542,209 @@ static uint32_t log2_floor(uint64_t x) {
     return r;
 }
 
+// Count the items in LDS (okm_count.hip), then gather their sorted runs into
+// the dense result table.  Releases level_bufs, d_items and d_segs.
+static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems,
+                                    uint64_t out_total, uint64_t in_total, bool weighted,
+                                    std::vector<void *> &level_bufs) {
+    uint64_t *sk, *sc;
+    unsigned long long *n_out, *dense_off, *scan_tmp;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
+    OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
+    OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    uint32_t *defer;
+    OKM_TRY(pool_get(c->pool, nitems, &defer));
+    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    c->hprof.mark("items.h2d");
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide);
+    c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
+    HIP_TRY(hipGetLastError());
+    launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
+    HIP_TRY(hipGetLastError());
+    unsigned long long hv[2];
+    HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    c->hprof.mark("count+scan+sync");
+    if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    const uint64_t nd = hv[0];
+    if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    c->timer.begin(c->stream);
+    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide);
+    c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(sync(c));
+    for (void *p : level_bufs) c->pool.put(p);
+    c->pool.put(d_segs);
+    c->pool.put(d_items);
+    c->pool.put(sk);
+    c->pool.put(sc);
+    c->pool.put(n_out);
+    c->pool.put(dense_off);
+    c->pool.put(scan_tmp);
+    c->pool.put(defer);
+    c->n_res = nd;
+    c->info.distinct = nd;
+    c->counted = true;
+    c->hprof.mark("compact+sync");
+    c->hprof.dump("count");
+    return OKM_OK;
+}
+// L1-partition (key, count) pairs in device memory with the generic pass (one
+// segment, 2^l1 bins) into an owned run.
+static okm_status partition_pairs(okm_ctx *c, const uint64_t *d_keys, const uint64_t *d_counts, uint64_t n,
+                                  Run &run) {
+    DevSeg s{};
+    s.keys = d_keys;
+    s.counts = d_counts;
+    s.len = n;
+    s.key_base = 0;
+    s.out_base = 0;
+    s.shift = c->shift1;
+    s.nlocal = c->nbins;
+    std::vector<DevChunk> chunks;
+    for (uint64_t o = 0; o < n; o += kChunkKeys) chunks.push_back(DevChunk{0, 0, o, std::min(kChunkKeys, n - o)});
+    DevSeg *d_seg;
+    DevChunk *d_chunks;
+    OKM_TRY(pool_get(c->pool, 1, &d_seg));
+    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    HIP_TRY(hipMemcpyAsync(d_seg, &s, sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)c->nbins));
+    OKM_TRY(ensure_hg(c, c->nbins));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, c->nbins * sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_part_hist(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->Hg, c->wide);
+    c->timer.end(c->stream, "part_hist", 8.0 * c->kw * (double)n);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1) * c->kw, &run.keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
+    c->timer.begin(c->stream);
+    launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys,
+                        run.counts, c->wide);
+    c->timer.end(c->stream, "part_scatter", (16.0 + 16.0 * c->kw) * (double)n);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(sync(c));
+    c->pool.put(d_seg);
+    c->pool.put(d_chunks);
+    return OKM_OK;
+}
+
+
+// All runs sorted (okm_add_sorted_pairs_device, e.g. the per-rank slices an
+// owner receives in the multi-GPU merge): every L1 part is split into
+// key-range children by binary search in each run — no key moves — and each
+// child is one multi-segment item.  *fallback: a child is still too big for
+// one item (a hot key); the caller takes the partitioning path instead.
+static okm_status count_sorted(okm_ctx *c, bool *fallback) {
+    *fallback = false;
+    const uint32_t R = (uint32_t)c->runs.size();
+    const uint64_t item_max = count_item_capacity();
+    const uint32_t capbits = count_dense_bits();
+    const uint64_t target = item_max * 3 / 4;
+    bool weighted = false;
+    for (auto &r : c->runs) weighted |= r.counts != nullptr;
+    std::vector<DevSortedPart> parts;
+    std::vector<DevSeg> rbins;
+    uint32_t nitems = 0;
+    uint64_t in_total = 0;
+    for (uint32_t b = 0; b < c->nbins; ++b) {
+        uint64_t len = 0;
+        for (auto &r : c->runs) len += r.off[b + 1] - r.off[b];
+        if (!len) continue;
+        uint32_t bits = 0;
+        if (len > item_max && c->shift1 > capbits)
+            while (bits < 20 && bits < c->shift1 && (len >> bits) > target) ++bits;
+        parts.push_back(DevSortedPart{b, bits, nitems, (uint32_t)parts.size()});
+        nitems += 1u << bits;
+        in_total += len;
+        for (auto &r : c->runs) {
+            DevSeg d{};
+            d.keys = r.keys + r.off[b] * c->kw;
+            d.counts = r.counts ? r.counts + r.off[b] : nullptr;
+            d.len = r.off[b + 1] - r.off[b];
+            d.shift = kSingleBin;
+            d.nlocal = 1;
+            rbins.push_back(d);
+        }
+    }
+    c->info.l1_bits = c->l1_bits;
+    c->info.levels = 0;
+    c->info.work_items = nitems;
+    if (nitems == 0) {
+        c->counted = true;
+        c->n_res = 0;
+        c->info.distinct = 0;
+        return OKM_OK;
+    }
+    std::vector<void *> bufs;
+    DevSortedPart *d_parts;
+    DevSeg *d_rbins, *d_segs;
+    DevItem *d_items;
+    unsigned long long *itemtot, *offs, *tmp, *flags;
+    OKM_TRY(pool_get(c->pool, parts.size(), &d_parts));
+    OKM_TRY(pool_get(c->pool, rbins.size(), &d_rbins));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems * R, &d_segs));
+    OKM_TRY(pool_get(c->pool, nitems, &d_items));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &itemtot));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &offs));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &tmp));
+    OKM_TRY(pool_get(c->pool, 2, &flags));
+    for (void *p : {(void *)d_parts, (void *)d_rbins, (void *)itemtot, (void *)offs, (void *)tmp, (void *)flags})
+        bufs.push_back(p);
+    HIP_TRY(hipMemcpyAsync(d_parts, parts.data(), parts.size() * sizeof(DevSortedPart), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_rbins, rbins.data(), rbins.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(itemtot + nitems, 0, sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_sorted_items(c->stream, d_parts, (uint32_t)parts.size(), nitems, d_rbins, R, c->shift1, d_items, d_segs,
+                        itemtot, item_max, capbits, flags, c->wide);
+    launch_exclusive_scan(c->stream, itemtot, offs, (uint64_t)nitems + 1, tmp);
+    launch_set_out_off(c->stream, d_items, nitems, offs);
+    c->timer.end(c->stream, "sorted_items", 0.0);
+    HIP_TRY(hipGetLastError());
+    unsigned long long hf[2];
+    HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    if (hf[0]) {
+        for (void *p : bufs) c->pool.put(p);
+        c->pool.put(d_segs);
+        c->pool.put(d_items);
+        *fallback = true;
+        return OKM_OK;
+    }
+    c->info.max_partition = hf[1];
+    return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
+}
+
 static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
     invalidate_result(c);
+    bool any_sorted = false, all_sorted = !c->runs.empty();
+    for (auto &r : c->runs) {
+        any_sorted |= r.sorted;
+        all_sorted &= r.sorted;
+    }
+    if (all_sorted) {
+        bool fallback = false;
+        OKM_TRY(count_sorted(c, &fallback));
+        if (!fallback) return OKM_OK;
+    }
+    if (any_sorted) {  // mixed with unsorted input (or a hot key): partition the sorted runs
+        for (auto &r : c->runs) {
+            if (!r.sorted) continue;
+            Run owned;
+            OKM_TRY(partition_pairs(c, r.keys, r.counts, r.n, owned));
+            r = std::move(owned);
+        }
+    }
     const uint32_t twok = 2u * c->k;
     // sort-mode items hold at most count_item_capacity() instances; items with
     // at most count_dense_bits() remaining key bits are counted by direct
@@ -689,63 +892,14 @@ static okm_status do_count(okm_ctx *c) {
         c->info.distinct = 0;
         return OKM_OK;
     }
-    uint64_t *sk, *sc;
-    unsigned long long *n_out, *dense_off, *scan_tmp;
     if (!device_items) {
         OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
         OKM_TRY(pool_get(c->pool, nitems, &d_items));
-    }
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
-    OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
-    OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
-    uint32_t *defer;
-    OKM_TRY(pool_get(c->pool, nitems, &defer));
-    c->hprof.mark("items.build");
-    if (!device_items) {
         HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(d_items, items.data(), nitems * sizeof(DevItem), hipMemcpyHostToDevice, c->stream));
     }
-    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
-    c->timer.begin(c->stream);
-    c->hprof.mark("items.h2d");
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide);
-    c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
-    HIP_TRY(hipGetLastError());
-    launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
-    HIP_TRY(hipGetLastError());
-    unsigned long long hv[2];
-    HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    OKM_TRY(sync(c));
-    c->hprof.mark("count+scan+sync");
-    if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
-    const uint64_t nd = hv[0];
-    if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
-    c->timer.begin(c->stream);
-    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide);
-    c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
-    HIP_TRY(hipGetLastError());
-    OKM_TRY(sync(c));
-    for (void *p : level_bufs) c->pool.put(p);
-    c->pool.put(d_segs);
-    c->pool.put(d_items);
-    c->pool.put(sk);
-    c->pool.put(sc);
-    c->pool.put(n_out);
-    c->pool.put(dense_off);
-    c->pool.put(scan_tmp);
-    c->pool.put(defer);
-    c->n_res = nd;
-    c->info.distinct = nd;
-    c->counted = true;
-    c->hprof.mark("compact+sync");
-    c->hprof.dump("count");
-    return OKM_OK;
+    c->hprof.mark("items.build");
+    return count_and_compact(c, d_items, d_segs, nitems, out_total, in_total, weighted, level_bufs);
 }
 
 static bool device_ok(int device, std::string *why) {
@@ -874,6 +1028,7 @@ okm_status okm_reset(okm_ctx *c) {
     OKM_TRY(sync(c));
     invalidate_result(c);
     for (auto &r : c->runs) {
+        if (r.borrowed) continue;
         c->pool.put(r.keys);
         c->pool.put(r.counts);
     }
@@ -937,42 +1092,31 @@ okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64
     if (!d_keys) return fail(OKM_E_ARG, "okm_add_pairs_device: null keys");
     HIP_TRY(hipSetDevice(c->device));
     invalidate_result(c);
-    // L1-partition the pairs with the generic pass (one segment, 2^l1 bins)
-    DevSeg s{};
-    s.keys = d_keys;
-    s.counts = d_counts;
-    s.len = n;
-    s.key_base = 0;
-    s.out_base = 0;
-    s.shift = c->shift1;
-    s.nlocal = c->nbins;
-    std::vector<DevChunk> chunks;
-    for (uint64_t o = 0; o < n; o += kChunkKeys) chunks.push_back(DevChunk{0, 0, o, std::min(kChunkKeys, n - o)});
-    DevSeg *d_seg;
-    DevChunk *d_chunks;
-    OKM_TRY(pool_get(c->pool, 1, &d_seg));
-    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
-    HIP_TRY(hipMemcpyAsync(d_seg, &s, sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
-    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)c->nbins));
-    OKM_TRY(ensure_hg(c, c->nbins));
-    HIP_TRY(hipMemsetAsync(c->Hg, 0, c->nbins * sizeof(unsigned long long), c->stream));
-    c->timer.begin(c->stream);
-    launch_part_hist(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->Hg, c->wide);
-    c->timer.end(c->stream, "part_hist", 8.0 * c->kw * (double)n);
-    HIP_TRY(hipGetLastError());
     Run run;
-    OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1) * c->kw, &run.keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
-    c->timer.begin(c->stream);
-    launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys,
-                        run.counts, c->wide);
-    c->timer.end(c->stream, "part_scatter", 32.0 * (double)n);
+    OKM_TRY(partition_pairs(c, d_keys, d_counts, n, run));
+    c->runs.push_back(std::move(run));
+    return OKM_OK;
+}
+
+okm_status okm_add_sorted_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64_t *d_counts, uint64_t n) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    if (n == 0) return OKM_OK;
+    if (!d_keys) return fail(OKM_E_ARG, "okm_add_sorted_pairs_device: null keys");
+    HIP_TRY(hipSetDevice(c->device));
+    invalidate_result(c);
+    Run run;
+    run.keys = const_cast<uint64_t *>(d_keys);
+    run.counts = const_cast<uint64_t *>(d_counts);
+    run.n = n;
+    run.sorted = true;
+    run.borrowed = true;
+    // L1 bin boundaries by binary search: the run stays where it is
+    OKM_TRY(ensure_hg(c, c->nbins + 1));
+    launch_bin_bounds(c->stream, d_keys, n, c->shift1, c->nbins, c->Hg, c->wide);
     HIP_TRY(hipGetLastError());
+    run.off.assign(c->nbins + 1, 0);
+    HIP_TRY(hipMemcpyAsync(run.off.data(), c->Hg, (c->nbins + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
-    c->pool.put(d_seg);
-    c->pool.put(d_chunks);
     c->runs.push_back(std::move(run));
     return OKM_OK;
 }

@@ -113,6 +113,25 @@ void launch_make_items(void *stream, const unsigned long long *offs, uint32_t no
                        uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
                        uint64_t item_max, uint32_t capbits, unsigned long long *flags, uint32_t kw);
 
+// Sorted runs (okm_add_sorted_pairs_device).  out[b] = first index whose
+// (key >> shift) >= b, b = 0..nbins (out[nbins] = n).
+void launch_bin_bounds(void *stream, const uint64_t *keys, uint64_t n, uint32_t shift, uint32_t nbins,
+                       unsigned long long *out, bool wide);
+struct DevSortedPart {
+    uint32_t bin;        // L1 bin of the part
+    uint32_t bits;       // split into 2^bits children (0: one item)
+    uint32_t item_base;  // first item of its children
+    uint32_t slot;       // row of the part in the rbins table
+};
+// One multi-segment item per child: segs[i * nruns + r] = the child's key range
+// in run r (rbins[slot * nruns + r] = the part's range in run r); itemtot[i]
+// = its instances; flags[0] += children still too big, flags[1] = max.
+void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
+                         const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
+                         unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
+                         bool wide);
+void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off);
+
 // Gather the per-item results into dense arrays given exclusive offsets.
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,

@@ -215,7 +215,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
 // stretch of the chunk's exact slice (no padding, no append rounds).
 template <typename KT, bool W> struct Tile {
     // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state
-    static constexpr int kKeys = (W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : 16384);
+#ifndef OKM_PART_TILE_KEYS
+#define OKM_PART_TILE_KEYS 16384
+#endif
+    static constexpr int kKeys = (W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : OKM_PART_TILE_KEYS);
     static constexpr int kPer = kKeys / kPartBlock;
 };
 

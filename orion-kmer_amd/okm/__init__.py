@@ -292,6 +292,11 @@ class KmerCounter:
         check(lib().okm_add_pairs_device(self.ctx, c_void_p(d_keys), c_void_p(d_counts) if d_counts else None, n),
               "okm_add_pairs_device")
 
+    def add_sorted_pairs_device(self, d_keys: int, d_counts: Optional[int], n: int) -> None:
+        """Strictly ascending keys in device memory, borrowed until count()."""
+        check(lib().okm_add_sorted_pairs_device(self.ctx, c_void_p(d_keys), c_void_p(d_counts) if d_counts else None,
+                                                n), "okm_add_sorted_pairs_device")
+
     def count(self) -> int:
         n = c_uint64()
         check(lib().okm_count(self.ctx, byref(n)), "okm_count")

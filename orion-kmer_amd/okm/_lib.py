@@ -76,6 +76,7 @@ PROTOTYPES = {
     "okm_add_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int]),
     "okm_add_batch_device": (c_int, [c_void_p, c_void_p, c_uint64]),
     "okm_add_pairs_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
+    "okm_add_sorted_pairs_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
     "okm_add_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
     "okm_count": (c_int, [c_void_p, _P64]),
     "okm_fetch_counts": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, _P64, c_int]),

@@ -14,7 +14,9 @@ is the merge:
      sizes, then one moves keys and one moves counts;
   4. each owner adds the received (key, count) runs into a fresh counter
      (weights add, exactly the AtomicUsize fetch_add of count.rs:31-34) and
-     re-counts, giving its range sorted.
+     re-counts, giving its range sorted.  Every rank's slice arrives sorted, so
+     the engine takes them in place (okm_add_sorted_pairs_device: binary-search
+     splits, no partition pass).
 
 The global table is the concatenation of the owners' ranges in rank order,
 so no final merge is needed.  The same code runs over gloo with CPU tensors
@@ -78,6 +80,15 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, k: int,
              group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor, List[int]]:
     """Move every (key, count) of this rank's sorted table to the owner of its
     key range; returns the received concatenated runs and the bin bounds."""
+    rk, rc, bounds, _ = exchange_runs(keys, counts, k, group)
+    return rk, rc, bounds
+
+
+def exchange_runs(keys: torch.Tensor, counts: torch.Tensor, k: int,
+                  group: Optional[dist.ProcessGroup] = None):
+    """exchange(), also returning the number of pairs received from each rank:
+    rank r's run is rk[sum(sizes[:r]) : sum(sizes[:r+1])], sorted by key
+    (okm_add_sorted_pairs_device takes each run without copying)."""
     world = dist.get_world_size(group)
     dev = keys.device
     hist = local_histogram(keys, k)
@@ -106,7 +117,7 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, k: int,
     rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
     dist.all_to_all_single(rk, keys.contiguous(), rs, ss, group=group)
     dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
-    return rk, rc, bounds
+    return rk, rc, bounds, rs
 
 
 def distributed_merge(keys: torch.Tensor, counts: torch.Tensor, k: int, merge: MergeFn,

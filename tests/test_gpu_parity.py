@@ -364,3 +364,48 @@ def test_full_size_properties():
         gk, gc = ctr.result(1)
     ek, ec = oc.result(1)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def _upload(arr):
+    arr = np.ascontiguousarray(arr, dtype=np.uint64)
+    buf = okm.DeviceBuffer(max(arr.nbytes, 8))
+    if arr.nbytes:
+        buf.upload(arr)
+    return buf
+
+
+@pytest.mark.parametrize("k,wide", [(31, False), (32, False), (45, True)])
+def test_sorted_runs_merge_equals_whole(k, wide):
+    # the multi-GPU owner path: per-rank sorted slices added without copies and
+    # counted by binary-search splits (okm_add_sorted_pairs_device)
+    batch = okm.synth_reads(60_000, 150, genome_len=400_000, seed=21, sub_rate=0.01)
+    recs = [r for r in batch.tobytes().split(b"\n") if r]
+    shards = [recs[i::3] for i in range(3)]
+    tables = []
+    for sh in shards:
+        with okm.KmerCounter(k, wide=wide) as c:
+            c.add_records(sh, normalized=True)
+            tables.append(c.result(1))
+    with okm.KmerCounter(k, wide=wide) as whole:
+        whole.add_records(recs, normalized=True)
+        wk, wc = whole.result(1)
+    bufs = []
+    with okm.KmerCounter(k, wide=wide) as m:
+        for tk, tc in tables:
+            bk, bc = _upload(tk), _upload(tc)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(tc))
+        mk, mc = m.result(1)
+        info = m.engine_info()
+    assert np.array_equal(mk, wk) and np.array_equal(mc, wc)
+    assert info["levels"] == 0  # no partition pass: binary-search splits only
+    # mixed with unsorted input: the sorted runs are partitioned like pairs
+    with okm.KmerCounter(k, wide=wide) as m2:
+        bk, bc = _upload(tables[0][0]), _upload(tables[0][1])
+        m2.add_sorted_pairs_device(bk.address, bc.address, len(tables[0][1]))
+        m2.add_pairs(tables[1][0], tables[1][1])
+        m2.add_records(shards[2], normalized=True)
+        xk, xc = m2.result(1)
+    assert np.array_equal(xk, wk) and np.array_equal(xc, wc)
+    for b in bufs + [bk, bc]:
+        b.free()
