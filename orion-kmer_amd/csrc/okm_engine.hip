@@ -213,6 +213,10 @@ struct KernelTimer {
         (void)hipEventRecord(b, s);
         pending.push_back({id_of(name), cur_a, b, bytes});
     }
+    // algorithmic bytes of an already-timed launch known only after a sync
+    void add_bytes(const char *name, double bytes) {
+        if (on) stats[id_of(name)].alg_bytes += bytes;
+    }
     // call after the stream is synchronised
     void flush() {
         for (auto &p : pending) {
@@ -242,9 +246,11 @@ struct Run {
     uint64_t *keys = nullptr;
     uint64_t *counts = nullptr;  // null: every key weighs 1
     std::vector<uint64_t> off;   // nbins + 1 offsets
+    std::vector<uint64_t> end;   // per-bin ends (line padded) when bins do not abut (sampled L1)
     uint64_t n = 0;              // keys (sorted runs)
     bool sorted = false;         // strictly ascending unique keys (okm_add_sorted_pairs_device)
     bool borrowed = false;       // caller-owned memory: never returned to the pool
+    uint64_t len(uint32_t b) const { return (end.empty() ? off[b + 1] : end[b]) - off[b]; }
 };
 
 }  // namespace okm
@@ -271,6 +277,7 @@ struct okm_ctx {
     unsigned long long *Hg = nullptr, *cursor = nullptr;
     size_t Hg_cap = 0;
     unsigned long long *flag = nullptr;  // overflow word
+    unsigned long long *l1cap = nullptr; // sampled L1: cap_end | start | overflow
     uint8_t *staging = nullptr;          // device copy of a host batch
     size_t staging_cap = 0;
     uint8_t *pinned = nullptr;           // pinned host staging
@@ -361,6 +368,78 @@ static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &
     return OKM_OK;
 }
 
+// Tile sampling stride of the sampled L1 placement (0/1: always exact).
+static uint32_t l1_sample_stride() {
+    static const uint32_t s = [] {
+        const char *e = getenv("OKM_L1_SAMPLE");
+        return e ? (uint32_t)atoi(e) : 16u;
+    }();
+    return s;
+}
+
+// Sampled L1 placement: histogram every S-th tile, size each bin from that
+// sample (launch_l1_capacity), scatter with per-tile claims.  One host sync,
+// after the scatter, reads the bins' ends and the overflow flag; *placed is
+// false (nothing recorded) when some bin outgrew its capacity.
+static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const ExtractGeom &g, uint32_t S,
+                             bool *placed) {
+    *placed = false;
+    const uint64_t tile = extract_tile();
+    const uint64_t tiles = (n + tile - 1) / tile;
+    const uint32_t nb = c->nbins, align = 16 / c->kw;
+    ExtractGeom gs{n, c->k, c->shift1, nb, (uint32_t)((tiles + S - 1) / S), tile, S};
+    const uint64_t last = (uint64_t)(gs.nblocks - 1) * S * tile;  // the only sampled tile that can be short
+    const uint64_t sbytes = (uint64_t)(gs.nblocks - 1) * tile + std::min(tile, n - last);
+    const double scale = (double)n / (double)sbytes;
+    const char *dbg = getenv("OKM_L1_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
+    const double mul = dbg ? atof(dbg) : 1.0;
+    // sum_b est_b <= n (windows <= bytes); sum_b sqrt(s_b) <= sqrt(nb * sbytes)
+    const uint64_t limit = (uint64_t)(1.01 * (double)n + 6.0 * scale * std::sqrt((double)nb * (double)sbytes) +
+                                      (double)nb * (256.0 + align)) + 64;
+    OKM_TRY(ensure_hg(c, nb));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, nb * sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_extract_hist(c->stream, d_seq, gs, nullptr, c->Hg);
+    c->timer.end(c->stream, "extract_sample", (double)sbytes);
+    launch_l1_capacity(c->stream, c->Hg, nb, scale, mul, align, limit, c->cursor, c->l1cap);
+    HIP_TRY(hipGetLastError());
+    Run run;
+    OKM_TRY(pool_get(c->pool, limit * c->kw, &run.keys));
+    c->timer.begin(c->stream);
+    launch_extract_scatter(c->stream, d_seq, g, nullptr, c->cursor, run.keys, c->l1cap, c->l1cap + 2 * nb + 1);
+    c->timer.end(c->stream, "extract_scatter", (double)n);
+    HIP_TRY(hipGetLastError());
+    std::vector<unsigned long long> ends(nb), cap(2 * nb + 2);
+    HIP_TRY(hipMemcpyAsync(ends.data(), c->cursor, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(cap.data(), c->l1cap, cap.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
+    OKM_TRY(sync(c));
+    if (cap[2 * nb + 1]) {  // some bin outgrew its sampled capacity: redo exactly
+        c->pool.put(run.keys);
+        c->hprof.mark("l1.sampled_overflow");
+        return OKM_OK;
+    }
+    uint64_t total = 0;
+    run.off.assign(cap.begin() + nb, cap.begin() + 2 * nb + 1);
+    run.end.resize(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        total += ends[b] - run.off[b];
+        run.end[b] = (ends[b] + align - 1) / align * align;
+    }
+    c->timer.add_bytes("extract_scatter", 8.0 * c->kw * (double)total);
+    *placed = true;
+    if (total == 0) {
+        c->pool.put(run.keys);
+        return OKM_OK;
+    }
+    launch_fill_line_tails(c->stream, c->cursor, nb, run.keys, c->wide);
+    HIP_TRY(hipGetLastError());
+    c->runs.push_back(std::move(run));
+    c->info.kmers += total;
+    c->hprof.mark("l1.sampled");
+    return OKM_OK;
+}
+
 // L1 pass over a device-resident batch (whitespace-free records joined by
 // OKM_RECORD_SEPARATOR, 16-byte aligned).
 static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
@@ -371,7 +450,13 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, 2048);
     uint64_t chunk = ((tiles + nblocks - 1) / nblocks) * tile;
     nblocks = (uint32_t)((n + chunk - 1) / chunk);
-    ExtractGeom g{n, c->k, c->shift1, c->nbins, nblocks, chunk};
+    ExtractGeom g{n, c->k, c->shift1, c->nbins, nblocks, chunk, 1};
+    const uint32_t S = l1_sample_stride();
+    if (S > 1 && tiles >= 64ull * S && c->nbins > 1) {
+        bool placed = false;
+        OKM_TRY(l1_sampled(c, d_seq, n, g, S, &placed));
+        if (placed) return OKM_OK;
+    }
 
     OKM_TRY(ensure_hc(c, (size_t)nblocks * c->nbins));
     OKM_TRY(ensure_hg(c, c->nbins));
@@ -388,7 +473,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     if (total == 0) return OKM_OK;
     OKM_TRY(pool_get(c->pool, run.off.back() * c->kw, &run.keys));
     c->timer.begin(c->stream);
-    launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys);
+    launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys, nullptr, nullptr);
     c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * c->kw * (double)total);
     HIP_TRY(hipGetLastError());
     launch_fill_line_tails(c->stream, c->cursor, c->nbins, run.keys, c->wide);
@@ -657,7 +742,7 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
     uint64_t in_total = 0;
     for (uint32_t b = 0; b < c->nbins; ++b) {
         uint64_t len = 0;
-        for (auto &r : c->runs) len += r.off[b + 1] - r.off[b];
+        for (auto &r : c->runs) len += r.len(b);
         if (!len) continue;
         uint32_t bits = 0;
         if (len > item_max && c->shift1 > capbits)
@@ -669,7 +754,7 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
             DevSeg d{};
             d.keys = r.keys + r.off[b] * c->kw;
             d.counts = r.counts ? r.counts + r.off[b] : nullptr;
-            d.len = r.off[b + 1] - r.off[b];
+            d.len = r.len(b);
             d.shift = kSingleBin;
             d.nlocal = 1;
             rbins.push_back(d);
@@ -767,7 +852,7 @@ static okm_status do_count(okm_ctx *c) {
     for (uint32_t b = 0; b < c->nbins; ++b) {
         Part p{(uint32_t)segtab.size(), 0, 0, b, c->l1_bits};
         for (auto &r : c->runs) {
-            const uint64_t len = r.off[b + 1] - r.off[b];
+            const uint64_t len = r.len(b);
             if (!len) continue;
             DevSeg d{};
             d.keys = r.keys + r.off[b] * c->kw;
@@ -993,7 +1078,8 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess) {
         (void)hipGetLastError();
         delete c;
         return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
@@ -1012,6 +1098,7 @@ void okm_destroy(okm_ctx *c) {
     if (c->Hg) (void)hipFree(c->Hg);
     if (c->cursor) (void)hipFree(c->cursor);
     if (c->flag) (void)hipFree(c->flag);
+    if (c->l1cap) (void)hipFree(c->l1cap);
     if (c->staging) (void)hipFree(c->staging);
     if (c->pinned) (void)hipHostFree(c->pinned);
     (void)hipStreamDestroy(c->stream);

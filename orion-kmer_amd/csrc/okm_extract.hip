@@ -41,7 +41,10 @@ __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
     return shift >= 64 ? 0u : (uint32_t)(key >> shift);
 }
 
-constexpr int kExtractBlock = 256;
+#ifndef OKM_EXTRACT_BLOCK
+#define OKM_EXTRACT_BLOCK 256
+#endif
+constexpr int kExtractBlock = OKM_EXTRACT_BLOCK;
 constexpr int kSegS = 32;                      // scatter: window starts per thread
 constexpr int kTile = kExtractBlock * kSegS;   // scatter tile: 8192 windows
 constexpr int kSegH = 64;                      // hist: window starts per thread
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
     __shared__ uint32_t lh[kMaxL1Bins + 1];  // + dummy bin for invalid windows
     for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
     __syncthreads();
-    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t beg = (uint64_t)blockIdx.x * g.stride * g.chunk;  // stride > 1: a sample of the chunks
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift, nb = g.nbins;
     for (uint64_t t0 = beg; t0 < end; t0 += kHTile) {
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
         const uint32_t h = lh[b];
-        HC[(uint64_t)blockIdx.x * nb + b] = h;
+        if (HC) HC[(uint64_t)blockIdx.x * nb + b] = h;
         if (h) atomicAdd(&Hg[b], (ull)h);
     }
 }
@@ -143,11 +146,30 @@ __device__ __forceinline__ uint32_t tile_offsets(uint32_t t, uint32_t nb, uint32
     return (uint32_t)tile_n;
 }
 
+// Sampled-capacity placement: this tile's run of bin t claims its slot.
+__device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32_t *hist, ull *cursor,
+                                           const ull *cap_end, ull *ovf, ull *gcur) {
+    if (t < nb) {
+        const uint32_t h = hist[t];
+        ull g = ~0ull;
+        if (h) {
+            const ull p = atomicAdd(&cursor[t], (ull)h);
+            if (p + h <= cap_end[t])
+                g = p;
+            else
+                atomicOr(ovf, 1ull);
+        }
+        gcur[t] = g;
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
                                                                    const uint32_t *__restrict__ HC,
                                                                    ull *__restrict__ cursor,
-                                                                   uint64_t *__restrict__ out) {
+                                                                   uint64_t *__restrict__ out,
+                                                                   const ull *__restrict__ cap_end,
+                                                                   ull *__restrict__ ovf) {
     __shared__ ull stage[kTile + 64];        // + one dummy slot per lane for invalid windows (K > 0)
     __shared__ ull gcur[kMaxL1Bins];         // this block's next output index per bin
     __shared__ uint32_t hist[kMaxL1Bins + 1];
@@ -156,7 +178,10 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     __shared__ ull wsum[kExtractBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
-    if (t < nb) {
+    // HC: exact per-block counts (one claim per bin for the whole chunk);
+    // HC == nullptr: sampled capacities, one claim per (tile, bin), checked
+    // against cap_end (a run that would cross it is dropped and *ovf set)
+    if (t < nb && HC) {
         const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
         gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
     }
@@ -183,6 +208,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
                 });
             __syncthreads();
             tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+            if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) {
@@ -197,6 +223,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
                 });
             __syncthreads();
             tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+            if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
             __syncthreads();
             if (live)
                 scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
@@ -208,10 +235,11 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
         for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
             const ull key = stage[j];
             const uint32_t b = bin_of(key, shift);
-            out[gcur[b] + (j - lofs[b])] = key;
+            const ull gb = gcur[b];
+            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
         __syncthreads();
-        if (t < nb) gcur[t] += hist[t];
+        if (HC && t < nb) gcur[t] += hist[t];
     }
 }
 
@@ -288,7 +316,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8
     __shared__ uint32_t lh[kMaxL1Bins + 1];
     for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
     __syncthreads();
-    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t beg = (uint64_t)blockIdx.x * g.stride * g.chunk;  // stride > 1: a sample of the chunks
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift, nb = g.nbins;
     for (uint64_t t0 = beg; t0 < end; t0 += kHTile) {
@@ -301,7 +329,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
         const uint32_t h = lh[b];
-        HC[(uint64_t)blockIdx.x * nb + b] = h;
+        if (HC) HC[(uint64_t)blockIdx.x * nb + b] = h;
         if (h) atomicAdd(&Hg[b], (ull)h);
     }
 }
@@ -310,7 +338,9 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
                                                                         ExtractGeom g,
                                                                         const uint32_t *__restrict__ HC,
                                                                         ull *__restrict__ cursor,
-                                                                        K128 *__restrict__ out) {
+                                                                        K128 *__restrict__ out,
+                                                                        const ull *__restrict__ cap_end,
+                                                                        ull *__restrict__ ovf) {
     __shared__ K128 stage[kTileW];
     __shared__ ull gcur[kMaxL1Bins];
     __shared__ uint32_t hist[kMaxL1Bins + 1];
@@ -319,7 +349,10 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
     __shared__ ull wsum[kExtractBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
-    if (t < nb) {
+    // HC: exact per-block counts (one claim per bin for the whole chunk);
+    // HC == nullptr: sampled capacities, one claim per (tile, bin), checked
+    // against cap_end (a run that would cross it is dropped and *ovf set)
+    if (t < nb && HC) {
         const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
         gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
     }
@@ -337,6 +370,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
             });
         __syncthreads();
         const uint32_t tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+        if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
         __syncthreads();
         if (live)
             scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
@@ -346,10 +380,11 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
         for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
             const K128 key = stage[j];
             const uint32_t b = bin_of_wide(key, shift);
-            out[gcur[b] + (j - lofs[b])] = key;
+            const ull gb = gcur[b];
+            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
         __syncthreads();
-        if (t < nb) gcur[t] += hist[t];
+        if (HC && t < nb) gcur[t] += hist[t];
     }
 }
 
@@ -384,24 +419,25 @@ void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g,
 }
 
 void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
-                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys) {
+                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys,
+                            const unsigned long long *cap_end, unsigned long long *ovf) {
     hipStream_t s = (hipStream_t)stream;
     if (g.k > 32) {
         hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
-                           reinterpret_cast<K128 *>(out_keys));
+                           reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
         return;
     }
     switch (g.k) {
 #define OKM_CASE(KV)                                                                                      \
     case KV:                                                                                              \
         hipLaunchKernelGGL(k_extract_scatter<KV>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, \
-                           cursor, out_keys);                                                             \
+                           cursor, out_keys, cap_end, ovf);                                               \
         return;
         OKM_EXTRACT_KS(OKM_CASE)
 #undef OKM_CASE
     default:
         hipLaunchKernelGGL(k_extract_scatter<0>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
-                           out_keys);
+                           out_keys, cap_end, ovf);
     }
 }
 
@@ -412,6 +448,45 @@ void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_
     else
         hipLaunchKernelGGL(k_fill_line_tails, dim3((nbins + 15) / 16), dim3(256), 0, (hipStream_t)stream, end,
                            nbins, keys);
+}
+
+// Sampled L1 capacities (one block, nb <= kMaxL1Bins): Hs holds the window
+// counts of a sample of the tiles; est_b = Hs[b] * scale, and bin b gets
+// est + 6 sigma (sigma = scale * sqrt(Hs[b]), the sampling error) + 1% + 256
+// keys, rounded up to `align` keys.  Starts are exclusive sums (line
+// aligned); l1cap = [cap_end(nb) | start(nb + 1) | overflow flag].
+__global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs, uint32_t nb, double scale,
+                                                     double mul, uint32_t align, ull limit, ull *__restrict__ cursor,
+                                                     ull *__restrict__ l1cap) {
+    __shared__ ull cap[kMaxL1Bins];
+    const uint32_t t = threadIdx.x;
+    if (t < nb) {
+        const double s = (double)Hs[t];
+        const double est = s * scale;
+        const double c = (est * 1.01 + 6.0 * scale * sqrt(s) + 256.0) * mul;
+        cap[t] = ((ull)c + align - 1) / align * align;
+    }
+    __syncthreads();
+    if (t == 0) {
+        ull o = 0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const ull st = o < limit ? o : limit;
+            o += cap[b];
+            const ull en = o < limit ? o : limit;
+            cursor[b] = st;
+            l1cap[b] = en;
+            l1cap[nb + b] = st;
+        }
+        l1cap[2 * nb] = o < limit ? o : limit;
+        l1cap[2 * nb + 1] = 0;
+    }
+}
+
+void launch_l1_capacity(void *stream, const unsigned long long *Hs, uint32_t nb, double scale, double mul,
+                        uint32_t align, unsigned long long limit, unsigned long long *cursor,
+                        unsigned long long *l1cap) {
+    hipLaunchKernelGGL(k_l1_capacity, dim3(1), dim3(256), 0, (hipStream_t)stream, Hs, nb, scale, mul, align, limit,
+                       cursor, l1cap);
 }
 
 }  // namespace okm

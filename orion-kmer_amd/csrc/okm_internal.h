@@ -57,14 +57,22 @@ struct ExtractGeom {
     uint32_t nbins;    // 1 << l1 bits
     uint32_t nblocks;  // persistent blocks (chunks)
     uint64_t chunk;    // window starts per block (multiple of the tile)
+    uint32_t stride;   // block b covers chunk b * stride (> 1: a sample of the batch)
 };
 
 // L1: k-mer extraction from a batch, histogram by top key bits.
 void launch_extract_hist(void *stream, const uint8_t *seq, const ExtractGeom &g, uint32_t *HC,
                          unsigned long long *Hg);
-// L1: k-mer extraction + scatter into key-range partitions (exact placement).
+// L1: k-mer extraction + scatter into key-range partitions.  HC != null:
+// exact placement from launch_extract_hist's per-block counts.  HC == null:
+// sampled capacities (launch_l1_capacity), one claim per (tile, bin); a run
+// crossing cap_end[bin] is dropped and *ovf set (the caller redoes the batch).
 void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom &g,
-                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys);
+                            const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys,
+                            const unsigned long long *cap_end, unsigned long long *ovf);
+void launch_l1_capacity(void *stream, const unsigned long long *Hs, uint32_t nb, double scale, double mul,
+                        uint32_t align, unsigned long long limit, unsigned long long *cursor,
+                        unsigned long long *l1cap);
 
 // Generic key-range partition pass over a chunk list.  max_local bounds every
 // segment's nlocal; HC is nchunks x max_local.

@@ -409,3 +409,52 @@ def test_sorted_runs_merge_equals_whole(k, wide):
     assert np.array_equal(xk, wk) and np.array_equal(xc, wc)
     for b in bufs + [bk, bc]:
         b.free()
+
+
+def _count_device(batch, k, wide=False):
+    buf = okm.DeviceBuffer(len(batch))
+    buf.upload(batch)
+    with okm.KmerCounter(k, wide=wide) as ctr:
+        ctr.set_timing(True)
+        ctr.add_device_batch(buf.address, len(batch))
+        keys, counts = ctr.result(1)
+        stats = ctr.kernel_stats()
+        info = ctr.engine_info()
+    buf.free()
+    return keys, counts, stats, info
+
+
+@pytest.mark.parametrize("genome,cap_mul", [(5_000_000, None), (5_000_000, "0.5"), (2_000, None),
+                                            (5_000_000, "0.999")])
+def test_sampled_l1_placement(genome, cap_mul, monkeypatch):
+    # batches of >= 64 sampled tiles take the sampled L1 placement (bins sized
+    # from every 16th tile's histogram); OKM_L1_CAP_DEBUG shrinks the
+    # capacities so that some bins overflow and the batch is redone exactly
+    k = 31
+    if cap_mul:
+        monkeypatch.setenv("OKM_L1_CAP_DEBUG", cap_mul)
+    batch = okm.synth_reads(130_000, 150, genome_len=genome, genome_seed=5, seed=31, sub_rate=0.01, n_rate=0.001)
+    gk, gc, stats, info = _count_device(batch, k)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["kmers"] == oc.windows
+    assert stats["extract_sample"]["launches"] == 1
+    redone = "extract_hist" in stats
+    if cap_mul == "0.5":
+        assert redone
+    elif cap_mul is None:
+        assert not redone
+
+
+def test_sampled_l1_placement_wide():
+    from oracle import OracleCounterWide
+    k = 45
+    batch = okm.synth_reads(130_000, 150, genome_len=3_000_000, genome_seed=6, seed=45, sub_rate=0.01)
+    gk, gc, stats, _ = _count_device(batch, k, wide=True)
+    oc = OracleCounterWide(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk.reshape(-1, 2), ek) and np.array_equal(gc, ec)
+    assert stats["extract_sample"]["launches"] == 1 and "extract_hist" not in stats
