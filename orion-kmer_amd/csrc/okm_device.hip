@@ -70,7 +70,8 @@ void launch_exclusive_scan(void *stream, const ull *in, ull *out, uint64_t n, ul
 // Work list of the LDS counting pass, built on the device
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs, uint32_t nout,
+__global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs, const ull *__restrict__ ends,
+                                                    uint32_t nout,
                                                     const DevParent *__restrict__ parents, uint32_t nparents,
                                                     const uint64_t *__restrict__ lk,
                                                     const uint64_t *__restrict__ lc, DevItem *__restrict__ items,
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
         if (parents[mid].out_base <= i) lo = mid; else hi = mid;
     }
     const uint32_t rem = parents[lo].rem;
-    const ull o = offs[i], len = offs[i + 1] - o;
+    const ull o = offs[i], len = (ends ? ends[i] : offs[i + 1]) - o;
     DevSeg s;
     s.keys = lk + o * kw;
     s.counts = lc ? lc + o : nullptr;
@@ -107,12 +108,37 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     atomicMax(&flags[1], len);
 }
 
-void launch_make_items(void *stream, const ull *offs, uint32_t nout, const DevParent *parents, uint32_t nparents,
-                       const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs, uint64_t item_max,
-                       uint32_t capbits, ull *flags, uint32_t kw) {
+void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t nout, const DevParent *parents,
+                       uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
+                       uint64_t item_max, uint32_t capbits, ull *flags, uint32_t kw) {
     if (!nout) return;
-    hipLaunchKernelGGL(k_make_items, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, offs, nout,
+    hipLaunchKernelGGL(k_make_items, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, offs, ends, nout,
                        parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw);
+}
+
+// Sampled partition capacities: est = H[b] * scale of b's parent; the slot
+// gets est + 1% + 6 sigma (sigma = scale * sqrt(H[b]), the sampling error)
+// + 64 keys, rounded up to 16 keys.
+__global__ __launch_bounds__(256) void k_part_capacity(ull *__restrict__ H, uint32_t nout,
+                                                       const DevCapParent *__restrict__ parents, uint32_t nparents,
+                                                       double mul) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nout) return;
+    uint32_t lo = 0, hi = nparents;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (parents[mid].out_base <= i) lo = mid; else hi = mid;
+    }
+    const double scale = parents[lo].scale, s = (double)H[i];
+    const double c = (s * scale * 1.01 + 6.0 * scale * sqrt(s) + 64.0) * mul;
+    H[i] = ((ull)c + 15) & ~15ull;
+}
+
+void launch_part_capacity(void *stream, ull *H, uint32_t nout, const DevCapParent *parents, uint32_t nparents,
+                          double mul) {
+    if (!nout) return;
+    hipLaunchKernelGGL(k_part_capacity, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, H, nout,
+                       parents, nparents, mul);
 }
 
 // ---------------------------------------------------------------------------

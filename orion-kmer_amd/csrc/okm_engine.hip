@@ -497,17 +497,37 @@ static const uint64_t kChunkKeys = 1u << 16;
 // key order, of the parts that took part (offsets stay on the device).
 struct Level {
     unsigned long long *d_offs = nullptr;  // nout + 1 exclusive offsets (line padded)
+    unsigned long long *d_ends = nullptr;  // sampled placement: per-bin ends (else bins abut)
+    unsigned long long *d_ovf = nullptr;   // sampled placement: overflow word
     uint64_t *lk = nullptr, *lc = nullptr;
     uint32_t nout = 0;
-    uint64_t padded = 0;
+    uint64_t padded = 0;                   // keys of address space (offsets' total)
+    uint64_t total = 0;                    // input keys of the pass
     std::vector<uint32_t> out_base;        // first output bin of each participating part
 };
 
 // One partition pass: split every part in `todo` by its own number of bits
 // (0 bits = gather the part as one bin).
+static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &psegs,
+                                       const std::vector<DevChunk> &chunks, const std::vector<uint32_t> &todo,
+                                       const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
+                                       std::vector<void *> &level_bufs, Level &L);
+
+// Tile sampling stride of the sampled partition placement (0/1: exact).
+static uint32_t part_sample_stride() {
+    static const uint32_t s = [] {
+        const char *e = getenv("OKM_PART_SAMPLE");
+        return e ? (uint32_t)atoi(e) : 16u;
+    }();
+    return s;
+}
+
+// sampled: size the children from a histogram of 1/S of every chunk
+// (launch_part_capacity) instead of an exact pass, so no host sync sits
+// between the passes; L.d_ovf reports a child that outgrew its slot.
 static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, const std::vector<Part> &parts,
                                const std::vector<uint32_t> &todo, const std::vector<uint32_t> &bits, bool weighted,
-                               std::vector<void *> &level_bufs, Level &L) {
+                               std::vector<void *> &level_bufs, Level &L, bool sampled = false) {
     const uint32_t twok = 2u * c->k;
     std::vector<DevSeg> psegs;      // pass segments (one per input segment)
     std::vector<DevChunk> chunks;
@@ -535,8 +555,11 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
         total += p.len;
     }
     L.nout = nout;
-    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)max_local));
+    L.total = total;
     OKM_TRY(ensure_hg(c, nout + 1));
+    if (sampled)
+        return split_launch_sampled(c, psegs, chunks, todo, bits, weighted, max_local, level_bufs, L);
+    OKM_TRY(ensure_hc(c, chunks.size() * (size_t)max_local));
     DevSeg *d_segs;
     DevChunk *d_chunks;
     unsigned long long *scan_tmp;
@@ -580,13 +603,97 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     return OKM_OK;
 }
 
+static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &psegs,
+                                       const std::vector<DevChunk> &chunks, const std::vector<uint32_t> &todo,
+                                       const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
+                                       std::vector<void *> &level_bufs, Level &L) {
+    const uint32_t S = part_sample_stride(), nout = L.nout;
+    const uint64_t piece = kChunkKeys / S;
+    // sample = the first 1/S of every chunk; per parent: keys / sampled keys
+    std::vector<DevChunk> sample;
+    sample.reserve(chunks.size());
+    std::vector<uint64_t> seg_sampled(psegs.size(), 0);
+    for (const DevChunk &ch : chunks) {
+        const uint64_t l = std::min(piece, ch.len);
+        sample.push_back(DevChunk{ch.seg, 0, ch.begin, l});
+        seg_sampled[ch.seg] += l;
+    }
+    std::vector<DevCapParent> cp(todo.size());
+    double limit = 64.0 + 2.0 * nout;
+    for (size_t t = 0, sg = 0; t < todo.size(); ++t) {
+        uint64_t len = 0, sl = 0;
+        for (; sg < psegs.size() && psegs[sg].out_base == L.out_base[t]; ++sg) {
+            len += psegs[sg].len;
+            sl += seg_sampled[sg];
+        }
+        const double scale = sl ? (double)len / (double)sl : 1.0;
+        cp[t] = DevCapParent{L.out_base[t], 0, scale};
+        // sum_b est_b <= len; sum_b sqrt(s_b) <= sqrt(2^bits * sl); + 80 per bin (64 + rounding)
+        const double nl = (double)(1u << bits[t]);
+        limit += 1.01 * (double)len + 6.0 * scale * std::sqrt(nl * (double)sl) + 80.0 * nl;
+    }
+    const char *dbg = getenv("OKM_PART_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
+    const double mul = dbg ? atof(dbg) : 1.0;
+    DevSeg *d_segs;
+    DevChunk *d_chunks, *d_sample;
+    DevCapParent *d_cp;
+    unsigned long long *scan_tmp;
+    OKM_TRY(pool_get(c->pool, psegs.size(), &d_segs));
+    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    OKM_TRY(pool_get(c->pool, sample.size(), &d_sample));
+    OKM_TRY(pool_get(c->pool, cp.size(), &d_cp));
+    OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
+    OKM_TRY(pool_get(c->pool, (size_t)nout, &L.d_ends));
+    OKM_TRY(pool_get(c->pool, 1, &L.d_ovf));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
+    for (void *p : {(void *)d_segs, (void *)d_chunks, (void *)d_sample, (void *)d_cp, (void *)L.d_offs,
+                    (void *)L.d_ends, (void *)L.d_ovf, (void *)scan_tmp})
+        level_bufs.push_back(p);
+    L.padded = (uint64_t)limit;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &L.lk));
+    level_bufs.push_back(L.lk);
+    if (weighted) {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &L.lc));
+        level_bufs.push_back(L.lc);
+    }
+    HIP_TRY(hipMemcpyAsync(d_segs, psegs.data(), psegs.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_sample, sample.data(), sample.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_cp, cp.data(), cp.size() * sizeof(DevCapParent), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(L.d_ovf, 0, sizeof(unsigned long long), c->stream));
+    uint64_t sampled_keys = 0;
+    for (const DevChunk &ch : sample) sampled_keys += ch.len;
+    c->timer.begin(c->stream);
+    launch_part_hist(c->stream, d_segs, d_sample, (uint32_t)sample.size(), max_local, nullptr, c->Hg, c->wide);
+    c->timer.end(c->stream, "part_sample", 8.0 * c->kw * (double)sampled_keys);
+    launch_part_capacity(c->stream, c->Hg, nout, d_cp, (uint32_t)cp.size(), mul);
+    launch_exclusive_scan(c->stream, c->Hg, L.d_offs, (uint64_t)nout + 1, scan_tmp);
+    HIP_TRY(hipMemcpyAsync(L.d_ends, L.d_offs, (size_t)nout * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                           c->stream));
+    HIP_TRY(hipGetLastError());
+    const double kb = weighted ? 16.0 : 8.0;
+    c->timer.begin(c->stream);
+    launch_part_scatter(c->stream, d_segs, d_chunks, (uint32_t)chunks.size(), max_local, nullptr, L.d_ends, L.lk,
+                        L.lc, c->wide, L.d_offs + 1, L.d_ovf);
+    c->timer.end(c->stream, "part_scatter", 2.0 * (kb + 8.0 * (c->kw - 1)) * (double)L.total);
+    HIP_TRY(hipGetLastError());
+    c->hprof.mark("split.sampled_launch");
+    c->info.levels += 1;
+    return OKM_OK;
+}
+
 // Host view of a level: replace each participating part by its non-empty
 // children (rare path: a child is still too big for one LDS item).
 static okm_status split_children_host(okm_ctx *c, const Level &L, std::vector<DevSeg> &segtab,
                                       std::vector<Part> &parts, const std::vector<uint32_t> &todo,
                                       const std::vector<uint32_t> &bits) {
-    std::vector<uint64_t> off((size_t)L.nout + 1);
+    std::vector<uint64_t> off((size_t)L.nout + 1), end;
     HIP_TRY(hipMemcpyAsync(off.data(), L.d_offs, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    if (L.d_ends) {
+        end.resize(L.nout);
+        HIP_TRY(hipMemcpyAsync(end.data(), L.d_ends, end.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    }
     OKM_TRY(sync(c));
     std::vector<Part> next;
     next.reserve(parts.size() + L.nout);
@@ -597,7 +704,7 @@ static okm_status split_children_host(okm_ctx *c, const Level &L, std::vector<De
             const uint32_t b = bits[t];
             for (uint32_t l = 0; l < (1u << b); ++l) {
                 const uint32_t ob = L.out_base[t] + l;
-                const uint64_t len = off[ob + 1] - off[ob];
+                const uint64_t len = (end.empty() ? off[ob + 1] : end[ob]) - off[ob];
                 if (!len) continue;
                 DevSeg d{};
                 d.keys = L.lk + off[ob] * c->kw;
@@ -901,39 +1008,59 @@ static okm_status do_count(okm_ctx *c) {
         if (any) {
             c->info.l2_bits = *std::max_element(bits.begin(), bits.end());
             c->hprof.mark("split.plan");
-            Level L;
-            OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L));
-            std::vector<DevParent> par(parts.size());
-            for (uint32_t i = 0; i < parts.size(); ++i) par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
-            DevParent *d_par;
-            unsigned long long *flags;
-            OKM_TRY(pool_get(c->pool, par.size(), &d_par));
-            OKM_TRY(pool_get(c->pool, 2, &flags));
-            OKM_TRY(pool_get(c->pool, L.nout, &d_items));
-            OKM_TRY(pool_get(c->pool, L.nout, &d_segs));
-            level_bufs.push_back(d_par);
-            level_bufs.push_back(flags);
-            HIP_TRY(hipMemcpyAsync(d_par, par.data(), par.size() * sizeof(DevParent), hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
-            launch_make_items(c->stream, L.d_offs, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc, d_items, d_segs,
-                              item_max, capbits, flags, c->kw);
-            HIP_TRY(hipGetLastError());
-            unsigned long long hf[2];
-            HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
-            OKM_TRY(sync(c));
-            c->hprof.mark("split.round");
-            if (hf[0] == 0) {
-                device_items = true;
-                nitems = L.nout;
-                out_total = in_total = L.padded;
-                c->info.max_partition = hf[1];
-                if (hf[1] >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
-            } else {
-                c->pool.put(d_items);
-                c->pool.put(d_segs);
-                d_items = nullptr;
-                d_segs = nullptr;
-                OKM_TRY(split_children_host(c, L, segtab, parts, all, bits));
+            uint64_t keys_in = 0;
+            for (const Part &p : parts) keys_in += p.len;
+            const bool try_sampled = part_tile_mode() && part_sample_stride() > 1 && keys_in >= (1ull << 22);
+            for (int attempt = 0;; ++attempt) {
+                Level L;
+                OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L, try_sampled && !attempt));
+                std::vector<DevParent> par(parts.size());
+                for (uint32_t i = 0; i < parts.size(); ++i)
+                    par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
+                DevParent *d_par;
+                unsigned long long *flags;
+                OKM_TRY(pool_get(c->pool, par.size(), &d_par));
+                OKM_TRY(pool_get(c->pool, 2, &flags));
+                OKM_TRY(pool_get(c->pool, L.nout, &d_items));
+                OKM_TRY(pool_get(c->pool, L.nout, &d_segs));
+                level_bufs.push_back(d_par);
+                level_bufs.push_back(flags);
+                HIP_TRY(hipMemcpyAsync(d_par, par.data(), par.size() * sizeof(DevParent), hipMemcpyHostToDevice,
+                                       c->stream));
+                HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
+                launch_make_items(c->stream, L.d_offs, L.d_ends, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc,
+                                  d_items, d_segs, item_max, capbits, flags, c->kw);
+                HIP_TRY(hipGetLastError());
+                unsigned long long hf[3] = {0, 0, 0};
+                HIP_TRY(hipMemcpyAsync(hf, flags, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+                if (L.d_ovf)
+                    HIP_TRY(hipMemcpyAsync(&hf[2], L.d_ovf, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                           c->stream));
+                OKM_TRY(sync(c));
+                c->hprof.mark("split.round");
+                if (hf[2]) {  // a child outgrew its sampled slot: redo the pass exactly
+                    c->pool.put(d_items);
+                    c->pool.put(d_segs);
+                    d_items = nullptr;
+                    d_segs = nullptr;
+                    c->info.levels -= 1;
+                    continue;
+                }
+                if (hf[0] == 0) {
+                    device_items = true;
+                    nitems = L.nout;
+                    out_total = L.padded;  // items' output slots mirror their input slots
+                    in_total = L.total;
+                    c->info.max_partition = hf[1];
+                    if (hf[1] >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
+                } else {
+                    c->pool.put(d_items);
+                    c->pool.put(d_segs);
+                    d_items = nullptr;
+                    d_segs = nullptr;
+                    OKM_TRY(split_children_host(c, L, segtab, parts, all, bits));
+                }
+                break;
             }
         }
     }

@@ -75,13 +75,26 @@ void launch_l1_capacity(void *stream, const unsigned long long *Hs, uint32_t nb,
                         unsigned long long *l1cap);
 
 // Generic key-range partition pass over a chunk list.  max_local bounds every
-// segment's nlocal; HC is nchunks x max_local.
+// segment's nlocal; HC is nchunks x max_local (null: only Hg, e.g. a sample).
 // wide: keys are K128 (two u64 each; pointers stay uint64_t*, lengths count keys).
 void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                       uint32_t max_local, uint32_t *HC, unsigned long long *Hg, bool wide);
+// HC null (tile mode only): sampled capacities, bin b's slot ends at
+// cap_end[b]; one claim per (tile, bin), a crossing run is dropped and *ovf set.
 void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks,
                          uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
-                         unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts, bool wide);
+                         unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts, bool wide,
+                         const unsigned long long *cap_end = nullptr, unsigned long long *ovf = nullptr);
+bool part_tile_mode();
+// Sampled partition capacities: H[b] (sampled count of output bin b) becomes
+// the bin's capacity (in place); parents sorted by out_base.
+struct DevCapParent {
+    uint32_t out_base;
+    uint32_t pad;
+    double scale;            // parent keys / sampled parent keys
+};
+void launch_part_capacity(void *stream, unsigned long long *H, uint32_t nout, const DevCapParent *parents,
+                          uint32_t nparents, double mul);
 // Pads [end[b], roundup(end[b], line)) of every bin with the empty key (bins
 // start on 128-B lines: 16 u64 / 8 K128 keys; end = the cursor after the scatter).
 void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide);
@@ -115,11 +128,13 @@ struct DevParent {
 };
 
 // One item (and one segment) per output bin of a split round, straight from
-// the device offsets (nout + 1 entries).  flags[0] += children that are still
-// too big for one item; flags[1] = max child length.
-void launch_make_items(void *stream, const unsigned long long *offs, uint32_t nout, const DevParent *parents,
-                       uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
-                       uint64_t item_max, uint32_t capbits, unsigned long long *flags, uint32_t kw);
+// the device offsets (nout + 1 entries; bin b ends at ends[b], or at
+// offs[b + 1] when ends is null).  flags[0] += children that are still too
+// big for one item; flags[1] = max child length.
+void launch_make_items(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
+                       const DevParent *parents, uint32_t nparents, const uint64_t *lk, const uint64_t *lc,
+                       DevItem *items, DevSeg *segs, uint64_t item_max, uint32_t capbits,
+                       unsigned long long *flags, uint32_t kw);
 
 // Sorted runs (okm_add_sorted_pairs_device).  out[b] = first index whose
 // (key >> shift) >= b, b = 0..nbins (out[nbins] = n).

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
         __syncthreads();
         for (uint32_t b = threadIdx.x; b < s.nlocal; b += kPartBlock) {
             const uint32_t h = lh[b];
-            HC[(uint64_t)c * max_local + b] = h;
+            if (HC) HC[(uint64_t)c * max_local + b] = h;
             if (h) atomicAdd(&Hg[s.out_base + b], pad_line<KT>(h));
         }
         __syncthreads();
@@ -226,7 +226,8 @@ template <typename KT, bool W>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
     const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
     uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
-    uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts) {
+    uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts, const ull *__restrict__ cap_end,
+    ull *__restrict__ ovf) {
     constexpr int T = Tile<KT, W>::kKeys, P = Tile<KT, W>::kPer;
     extern __shared__ __attribute__((aligned(16))) ull lds[];
     KT *stage = reinterpret_cast<KT *>(lds);                              // [T]
@@ -242,10 +243,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
         const DevChunk ch = chunks[c];
         const DevSeg s = segs[ch.seg];
         const uint32_t nl = s.nlocal;
-        for (uint32_t b = t; b < nl; b += kPartBlock) {
-            const uint32_t h = HC[(uint64_t)c * max_local + b];
-            gcur[b] = h ? atomicAdd(&cursor[s.out_base + b], (ull)h) : 0ull;
-        }
+        if (HC)  // exact: one claim per bin for the whole chunk
+            for (uint32_t b = t; b < nl; b += kPartBlock) {
+                const uint32_t h = HC[(uint64_t)c * max_local + b];
+                gcur[b] = h ? atomicAdd(&cursor[s.out_base + b], (ull)h) : 0ull;
+            }
         const KT *keys = reinterpret_cast<const KT *>(s.keys) + ch.begin;
         const uint64_t *cnts = s.counts ? s.counts + ch.begin : nullptr;
         for (uint64_t base = 0; base < ch.len; base += T) {
@@ -274,6 +276,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
             ull tile_n;
             const uint32_t off = (uint32_t)block_excl_scan<kPartBlock>(my, wsum, &tile_n);
             if (t < nl) lofs[t] = off;
+            if (!HC && t < nl) {  // sampled capacities: claim this tile's run
+                const uint32_t h = hist[t];
+                ull g = ~0ull;
+                if (h) {
+                    const ull p = atomicAdd(&cursor[s.out_base + t], (ull)h);
+                    if (p + h <= cap_end[s.out_base + t])
+                        g = p;
+                    else
+                        atomicOr(ovf, 1ull);
+                }
+                gcur[t] = g;
+            }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < P; ++u) {
@@ -288,12 +302,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
             for (uint32_t j = t; j < (uint32_t)tile_n; j += kPartBlock) {
                 const KT key = stage[j];
                 const uint32_t b = local_bin(key, s);
-                const ull o = gcur[b] + (j - lofs[b]);
+                const ull g = gcur[b];
+                if (g == ~0ull) continue;  // sampled mode: the bin overflowed
+                const ull o = g + (j - lofs[b]);
                 out_keys[o] = key;
                 if (W) out_counts[o] = cstage[j];
             }
             __syncthreads();
-            if (t < nl) gcur[t] += hist[t];
+            if (HC && t < nl) gcur[t] += hist[t];
         }
         __syncthreads();
     }
@@ -312,10 +328,12 @@ void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, 
         hipLaunchKernelGGL(k_part_hist<ull>, g, b, lds, (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, Hg);
 }
 
+bool part_tile_mode() { return OKM_PART_TILE != 0; }
+
 template <typename KT, bool W>
 static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                            uint32_t max_local, const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys,
-                           uint64_t *out_counts) {
+                           uint64_t *out_counts, const ull *cap_end, ull *ovf) {
     static bool attr_done = false;  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per workgroup)
     if (!attr_done) {
         int dev = 0, optin = 0;
@@ -344,7 +362,8 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
         const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) +
                            (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
         hipLaunchKernelGGL((k_part_scatter_tile<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
-                           (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+                           (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                           cap_end, ovf);
         return;
     }
     constexpr int L = Line<KT>::kKeys;
@@ -355,18 +374,22 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
 
 void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                          uint32_t max_local, const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys,
-                         uint64_t *out_counts, bool wide) {
+                         uint64_t *out_counts, bool wide, const ull *cap_end, ull *ovf) {
     if (!nchunks) return;
     if (wide) {
         if (out_counts)
-            scatter_launch<K128, true>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+            scatter_launch<K128, true>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                                      cap_end, ovf);
         else
-            scatter_launch<K128, false>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+            scatter_launch<K128, false>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                                       cap_end, ovf);
     } else {
         if (out_counts)
-            scatter_launch<ull, true>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+            scatter_launch<ull, true>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                                    cap_end, ovf);
         else
-            scatter_launch<ull, false>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+            scatter_launch<ull, false>(stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                                     cap_end, ovf);
     }
 }
 

@@ -424,15 +424,20 @@ def _count_device(batch, k, wide=False):
     return keys, counts, stats, info
 
 
-@pytest.mark.parametrize("genome,cap_mul", [(5_000_000, None), (5_000_000, "0.5"), (2_000, None),
-                                            (5_000_000, "0.999")])
-def test_sampled_l1_placement(genome, cap_mul, monkeypatch):
+@pytest.mark.parametrize("genome,cap_mul,part_mul", [
+    (5_000_000, None, None), (5_000_000, "0.5", None), (2_000, None, None), (5_000_000, "0.999", None),
+    (5_000_000, None, "0.5"), (5_000_000, None, "0.97"), (2_000, "0.5", "0.5")])
+def test_sampled_placement(genome, cap_mul, part_mul, monkeypatch):
     # batches of >= 64 sampled tiles take the sampled L1 placement (bins sized
-    # from every 16th tile's histogram); OKM_L1_CAP_DEBUG shrinks the
-    # capacities so that some bins overflow and the batch is redone exactly
+    # from every 16th tile's histogram), and >= 4 Mi keys the sampled
+    # partition placement (children sized from 1/16 of every chunk);
+    # OKM_L1_CAP_DEBUG / OKM_PART_CAP_DEBUG shrink the capacities so that
+    # some bins overflow and the pass is redone exactly
     k = 31
     if cap_mul:
         monkeypatch.setenv("OKM_L1_CAP_DEBUG", cap_mul)
+    if part_mul:
+        monkeypatch.setenv("OKM_PART_CAP_DEBUG", part_mul)
     batch = okm.synth_reads(130_000, 150, genome_len=genome, genome_seed=5, seed=31, sub_rate=0.01, n_rate=0.001)
     gk, gc, stats, info = _count_device(batch, k)
     oc = OracleCounter(k)
@@ -441,11 +446,15 @@ def test_sampled_l1_placement(genome, cap_mul, monkeypatch):
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert info["kmers"] == oc.windows
     assert stats["extract_sample"]["launches"] == 1
-    redone = "extract_hist" in stats
+    l1_redone = "extract_hist" in stats
     if cap_mul == "0.5":
-        assert redone
+        assert l1_redone
     elif cap_mul is None:
-        assert not redone
+        assert not l1_redone
+    if genome > 100_000:  # a low-complexity batch has few distinct keys: no split
+        assert stats["part_sample"]["launches"] == 1
+        part_redone = "part_hist" in stats
+        assert part_redone == (part_mul == "0.5") or part_mul == "0.97"
 
 
 def test_sampled_l1_placement_wide():
