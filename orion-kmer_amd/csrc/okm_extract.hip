@@ -42,11 +42,23 @@ __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
 }
 
 #ifndef OKM_EXTRACT_BLOCK
-#define OKM_EXTRACT_BLOCK 256
+#define OKM_EXTRACT_BLOCK 512
 #endif
-constexpr int kExtractBlock = OKM_EXTRACT_BLOCK;
-constexpr int kSegS = 32;                      // scatter: window starts per thread
-constexpr int kTile = kExtractBlock * kSegS;   // scatter tile: 8192 windows
+#ifndef OKM_EXTRACT_SEG
+#define OKM_EXTRACT_SEG 16
+#endif
+#ifndef OKM_EXTRACT_WPE  // scatter: waves per SIMD the register budget must allow
+#define OKM_EXTRACT_WPE 4
+#endif
+#ifndef OKM_EXTRACT_PREFETCH  // scatter: load the next tile's bytes during this tile
+#define OKM_EXTRACT_PREFETCH 1
+#endif
+constexpr int kExtractBlock = 256;
+constexpr int kScatBlock = OKM_EXTRACT_BLOCK;  // k <= 32 scatter
+constexpr int kSegS = OKM_EXTRACT_SEG;         // scatter: window starts per thread
+constexpr int kTile = kScatBlock * kSegS;      // scatter tile: 8192 windows
+static_assert(kScatBlock >= 256 && (16384 % kTile) == 0, "scatter tile must divide the hist tile");
+static_assert(kSegS % 16 == 0, "scan_windows loads whole 16-B words");
 constexpr int kSegH = 64;                      // hist: window starts per thread
 constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
 constexpr int kMaxL1Bins = 256;
@@ -59,12 +71,17 @@ uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
 // is a compile-time constant after unrolling; K = 0: runtime k, runtime j).
 // Bytes at or beyond n read as 0 (invalid), so windows never run off the end;
 // record separators are invalid bytes, so windows never cross records.
-template <int SEG, int K, typename Emit>
-__device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
-                                             uint32_t k_rt, Emit &&emit) {
-    constexpr int LOAD = SEG + 32;  // bytes: covers SEG + k - 1 for k <= 32 (16-B multiple)
-    const uint32_t k = K ? (uint32_t)K : k_rt;
-    uint32_t w[LOAD / 4];
+template <int SEG> struct WinWords {
+    static constexpr int kLoad = SEG + 32;  // bytes: covers SEG + k - 1 for k <= 32 (16-B multiple)
+    uint32_t w[kLoad / 4];
+};
+
+// The bytes of windows [w0, w0 + SEG) (bytes at or beyond n read as 0).
+template <int SEG>
+__device__ __forceinline__ void load_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
+                                             WinWords<SEG> &ww) {
+    constexpr int LOAD = WinWords<SEG>::kLoad;
+    uint32_t *w = ww.w;
     if (w0 + LOAD <= n) {
         const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
 #pragma unroll
@@ -88,6 +105,13 @@ __device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, ui
             w[q] = x;
         }
     }
+}
+
+template <int SEG, int K, typename Emit>
+__device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_rt, Emit &&emit) {
+    constexpr int LOAD = WinWords<SEG>::kLoad;
+    const uint32_t k = K ? (uint32_t)K : k_rt;
+    const uint32_t *w = ww.w;
     const uint64_t kmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1ull);
     const uint32_t rcs = 2 * k - 2;
     uint64_t fwd = 0, rc = 0;
@@ -107,6 +131,14 @@ __device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, ui
             if (j >= 0 && j < SEG) emit(j, fwd < rc ? fwd : rc, run >= k);
         }
     }
+}
+
+template <int SEG, int K, typename Emit>
+__device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
+                                             uint32_t k_rt, Emit &&emit) {
+    WinWords<SEG> ww;
+    load_windows<SEG>(seq, n, w0, ww);
+    scan_words<SEG, K>(ww, k_rt, emit);
 }
 
 template <int K>
@@ -134,11 +166,12 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
 }
 
 // Shared tail of the scatter tile: bin offsets within the tile.
+template <int BLOCK>
 __device__ __forceinline__ uint32_t tile_offsets(uint32_t t, uint32_t nb, uint32_t *hist, uint32_t *lofs,
                                                  uint32_t *lcur, ull *wsum) {
     ull tile_n;
     const uint32_t my = t < nb ? hist[t] : 0u;
-    const uint32_t off = (uint32_t)block_excl_scan<kExtractBlock>(my, wsum, &tile_n);
+    const uint32_t off = (uint32_t)block_excl_scan<BLOCK>(my, wsum, &tile_n);
     if (t < nb) {
         lofs[t] = off;
         lcur[t] = off;
@@ -164,7 +197,7 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
 }
 
 template <int K>
-__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
+__global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_EXTRACT_WPE))) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
                                                                    const uint32_t *__restrict__ HC,
                                                                    ull *__restrict__ cursor,
                                                                    uint64_t *__restrict__ out,
@@ -175,7 +208,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     __shared__ uint32_t hist[kMaxL1Bins + 1];
     __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
     __shared__ uint32_t lcur[kMaxL1Bins];
-    __shared__ ull wsum[kExtractBlock / 64];
+    __shared__ ull wsum[kScatBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     // HC: exact per-block counts (one claim per bin for the whole chunk);
@@ -188,6 +221,10 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
     const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
+    WinWords<kSegS> ww;  // K > 0: this tile's bytes, loaded one tile ahead
+    if (K && OKM_EXTRACT_PREFETCH && beg + (uint64_t)t * kSegS < end)
+        load_windows<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
+    const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
         if (t <= nb) hist[t] = 0;
         __syncthreads();
@@ -200,15 +237,24 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
             uint32_t rk[kSegS];  // bin << 16 | rank; invalid: nb << 16
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) rk[j] = nb << 16;
+            if (!OKM_EXTRACT_PREFETCH && live) load_windows<kSegS>(seq, g.n, w0, ww);
             if (live)
-                scan_windows<kSegS, K>(seq, g.n, w0, g.k, [&](int j, uint64_t key, bool valid) {
+                scan_words<kSegS, K>(ww, g.k, [&](int j, uint64_t key, bool valid) {
                     const uint32_t b = valid ? bin_of(key, shift) : nb;
                     kk[j] = key;
                     rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
                 });
+            if (OKM_EXTRACT_PREFETCH && w0 + kTile < end)  // next tile, in flight meanwhile
+                load_windows<kSegS>(seq, g.n, w0 + kTile, ww);
             __syncthreads();
-            tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
-            if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
+            tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
+            // sampled capacities: issue this tile's claim now, consume it after the staging
+            uint32_t ch = 0;
+            ull cp = 0;
+            if (!HC && t < nb) {
+                ch = hist[t];
+                if (ch) cp = atomicAdd(&cursor[t], (ull)ch);
+            }
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) {
@@ -216,13 +262,18 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
                 const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTile + (t & 63u);
                 stage[dst] = kk[j];
             }
+            if (!HC && t < nb) {
+                const bool fits = ch && cp + ch <= capb;
+                if (ch && !fits) atomicOr(ovf, 1ull);
+                gcur[t] = fits ? cp : ~0ull;
+            }
         } else {
             if (live)
                 scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
                     atomicAdd(&hist[valid ? bin_of(key, shift) : nb], 1u);
                 });
             __syncthreads();
-            tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+            tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
             if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
             __syncthreads();
             if (live)
@@ -232,7 +283,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter(const uint8_t
         }
         __syncthreads();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
-        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
+        for (uint32_t j = t; j < tile_n; j += kScatBlock) {
             const ull key = stage[j];
             const uint32_t b = bin_of(key, shift);
             const ull gb = gcur[b];
@@ -369,7 +420,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
                 atomicAdd(&hist[valid ? bin_of_wide(key, shift) : nb], 1u);
             });
         __syncthreads();
-        const uint32_t tile_n = tile_offsets(t, nb, hist, lofs, lcur, wsum);
+        const uint32_t tile_n = tile_offsets<kExtractBlock>(t, nb, hist, lofs, lcur, wsum);
         if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
         __syncthreads();
         if (live)
@@ -430,13 +481,13 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
     switch (g.k) {
 #define OKM_CASE(KV)                                                                                      \
     case KV:                                                                                              \
-        hipLaunchKernelGGL(k_extract_scatter<KV>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, \
+        hipLaunchKernelGGL(k_extract_scatter<KV>, dim3(g.nblocks), dim3(kScatBlock), 0, s, seq, g, HC, \
                            cursor, out_keys, cap_end, ovf);                                               \
         return;
         OKM_EXTRACT_KS(OKM_CASE)
 #undef OKM_CASE
     default:
-        hipLaunchKernelGGL(k_extract_scatter<0>, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
+        hipLaunchKernelGGL(k_extract_scatter<0>, dim3(g.nblocks), dim3(kScatBlock), 0, s, seq, g, HC, cursor,
                            out_keys, cap_end, ovf);
     }
 }
