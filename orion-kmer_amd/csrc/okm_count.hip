@@ -539,7 +539,8 @@ template <bool W>
 __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM_COUNT_WPE)))
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
-                   ull *__restrict__ ctl, uint32_t *__restrict__ defer) {
+                   ull *__restrict__ ctl, uint32_t *__restrict__ defer, const ull *__restrict__ guard) {
+    if (guard && (guard[0] | guard[1])) return;  // speculative launch whose items were not valid
     __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     const uint32_t t = threadIdx.x;
@@ -578,7 +579,9 @@ __global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ 
                                                     const DevSeg *__restrict__ segs,
                                                     uint64_t *__restrict__ out_keys,
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
-                                                    ull *__restrict__ ctl, const uint32_t *__restrict__ defer) {
+                                                    ull *__restrict__ ctl, const uint32_t *__restrict__ defer,
+                                                    const ull *__restrict__ guard) {
+    if (guard && (guard[0] | guard[1])) return;
     constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2;
     constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
     constexpr int kBytes = kFull > kDense ? kFull : kDense;
@@ -612,31 +615,32 @@ void count_prof_read(unsigned long long *out16) {
 
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide) {
+                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
+                        const unsigned long long *guard) {
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
     if (wide) {  // every item through the full / dense modes
         const uint32_t grid = nitems < 4096u ? nitems : 4096u;
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                               out_counts, n_out, ctl, (const uint32_t *)nullptr);
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
         else
             hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr);
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
         return;
     }
     const uint32_t grid = nitems < 4096u ? nitems : 4096u;
     const uint32_t sgrid = nitems < 1024u ? nitems : 1024u;  // exits at once when nothing was deferred
     if (weighted) {
         hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer);
+                           out_counts, n_out, ctl, defer, guard);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer);
+                           out_counts, n_out, ctl, defer, guard);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard);
     }
 }
 

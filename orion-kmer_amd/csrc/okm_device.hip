@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     it.pad = 0;
     items[i] = it;
     if (len > item_max && rem > capbits) atomicAdd(&flags[0], 1ull);
-    atomicMax(&flags[1], len);
+    if (len >= (1ull << 32)) atomicOr(&flags[1], 2ull);  // u32 LDS counts could overflow: count weighted
+    atomicMax(&flags[2], len);
 }
 
 void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t nout, const DevParent *parents,
@@ -261,7 +262,10 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
                                                        const KT *__restrict__ sk,
                                                        const uint64_t *__restrict__ sc,
                                                        KT *__restrict__ dk,
-                                                       uint64_t *__restrict__ dc) {
+                                                       uint64_t *__restrict__ dc,
+                                                       const ull *__restrict__ guard,
+                                                       const ull *__restrict__ err) {
+    if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
         for (uint64_t j = threadIdx.x; j < n; j += 256) {
@@ -274,17 +278,18 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts, uint64_t *dst_keys,
-                          uint64_t *dst_counts, bool wide) {
+                          uint64_t *dst_counts, bool wide, const unsigned long long *guard,
+                          const unsigned long long *err) {
     if (!nitems) return;
     const uint32_t grid = nitems < 8192u ? nitems : 8192u;
     if (wide)
         hipLaunchKernelGGL(k_compact_items<K128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
                            dense_off, reinterpret_cast<const K128 *>(src_keys), src_counts,
-                           reinterpret_cast<K128 *>(dst_keys), dst_counts);
+                           reinterpret_cast<K128 *>(dst_keys), dst_counts, guard, err);
     else
         hipLaunchKernelGGL(k_compact_items<ull>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
                            dense_off, reinterpret_cast<const ull *>(src_keys), src_counts,
-                           reinterpret_cast<ull *>(dst_keys), dst_counts);
+                           reinterpret_cast<ull *>(dst_keys), dst_counts, guard, err);
 }
 
 constexpr int kFilterBlock = 256;

@@ -257,6 +257,9 @@ struct Run {
 
 using namespace okm;
 
+static const size_t kHpinBytes = size_t(4) << 20;
+static const size_t kHresWords = 2048;  // [0, 1024): L1 readback; [1024, 1040): count readback
+
 struct okm_ctx {
     int device = 0;
     uint8_t k = 0;
@@ -282,6 +285,9 @@ struct okm_ctx {
     size_t staging_cap = 0;
     uint8_t *pinned = nullptr;           // pinned host staging
     size_t pinned_cap = 0;
+    uint8_t *hpin = nullptr;             // pinned staging of small host->device tables (recycled at sync)
+    size_t hpin_used = 0;
+    unsigned long long *hres = nullptr;  // pinned landing area of small device->host reads
 
     // result
     bool counted = false;
@@ -346,6 +352,22 @@ static okm_status sync(okm_ctx *c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipGetLastError());
     c->timer.flush();
+    c->hpin_used = 0;  // every copy out of the pinned staging has completed
+    return OKM_OK;
+}
+
+// Host-to-device copy of a small table, staged in pinned memory so that the
+// DMA reads it directly (a pageable source takes a bounce copy and a blit).
+static okm_status h2d(okm_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return OKM_OK;
+    const size_t at = (c->hpin_used + 255) & ~size_t(255);
+    if (at + bytes <= kHpinBytes) {
+        memcpy(c->hpin + at, src, bytes);
+        c->hpin_used = at + bytes;
+        HIP_TRY(hipMemcpyAsync(dst, c->hpin + at, bytes, hipMemcpyHostToDevice, c->stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    }
     return OKM_OK;
 }
 
@@ -409,9 +431,9 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     launch_extract_scatter(c->stream, d_seq, g, nullptr, c->cursor, run.keys, c->l1cap, c->l1cap + 2 * nb + 1);
     c->timer.end(c->stream, "extract_scatter", (double)n);
     HIP_TRY(hipGetLastError());
-    std::vector<unsigned long long> ends(nb), cap(2 * nb + 2);
-    HIP_TRY(hipMemcpyAsync(ends.data(), c->cursor, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(cap.data(), c->l1cap, cap.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    unsigned long long *ends = c->hres, *cap = c->hres + nb;  // nb + 2 nb + 2 <= 1024 words
+    HIP_TRY(hipMemcpyAsync(ends, c->cursor, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(cap, c->l1cap, (2 * nb + 2) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
     OKM_TRY(sync(c));
     if (cap[2 * nb + 1]) {  // some bin outgrew its sampled capacity: redo exactly
@@ -420,7 +442,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
         return OKM_OK;
     }
     uint64_t total = 0;
-    run.off.assign(cap.begin() + nb, cap.begin() + 2 * nb + 1);
+    run.off.assign(cap + nb, cap + 2 * nb + 1);
     run.end.resize(nb);
     for (uint32_t b = 0; b < nb; ++b) {
         total += ends[b] - run.off[b];
@@ -511,7 +533,7 @@ struct Level {
 static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &psegs,
                                        const std::vector<DevChunk> &chunks, const std::vector<uint32_t> &todo,
                                        const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
-                                       std::vector<void *> &level_bufs, Level &L);
+                                       std::vector<void *> &level_bufs, Level &L, unsigned long long *ovf);
 
 // Tile sampling stride of the sampled partition placement (0/1: exact).
 static uint32_t part_sample_stride() {
@@ -522,12 +544,13 @@ static uint32_t part_sample_stride() {
     return s;
 }
 
-// sampled: size the children from a histogram of 1/S of every chunk
-// (launch_part_capacity) instead of an exact pass, so no host sync sits
-// between the passes; L.d_ovf reports a child that outgrew its slot.
+// ovf (sampled mode): size the children from a histogram of 1/S of every
+// chunk (launch_part_capacity) instead of an exact pass, so no host sync
+// sits between the passes; *ovf becomes nonzero when a child outgrew its
+// slot (the level is then invalid and must be redone exactly).
 static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, const std::vector<Part> &parts,
                                const std::vector<uint32_t> &todo, const std::vector<uint32_t> &bits, bool weighted,
-                               std::vector<void *> &level_bufs, Level &L, bool sampled = false) {
+                               std::vector<void *> &level_bufs, Level &L, unsigned long long *ovf = nullptr) {
     const uint32_t twok = 2u * c->k;
     std::vector<DevSeg> psegs;      // pass segments (one per input segment)
     std::vector<DevChunk> chunks;
@@ -557,8 +580,7 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     L.nout = nout;
     L.total = total;
     OKM_TRY(ensure_hg(c, nout + 1));
-    if (sampled)
-        return split_launch_sampled(c, psegs, chunks, todo, bits, weighted, max_local, level_bufs, L);
+    if (ovf) return split_launch_sampled(c, psegs, chunks, todo, bits, weighted, max_local, level_bufs, L, ovf);
     OKM_TRY(ensure_hc(c, chunks.size() * (size_t)max_local));
     DevSeg *d_segs;
     DevChunk *d_chunks;
@@ -571,8 +593,8 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     level_bufs.push_back(d_chunks);
     level_bufs.push_back(L.d_offs);
     level_bufs.push_back(scan_tmp);
-    HIP_TRY(hipMemcpyAsync(d_segs, psegs.data(), psegs.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
+    OKM_TRY(h2d(c, d_segs, psegs.data(), psegs.size() * sizeof(DevSeg)));
+    OKM_TRY(h2d(c, d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk)));
     HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
     const double kb = weighted ? 16.0 : 8.0;
     c->timer.begin(c->stream);
@@ -606,8 +628,9 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
 static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &psegs,
                                        const std::vector<DevChunk> &chunks, const std::vector<uint32_t> &todo,
                                        const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
-                                       std::vector<void *> &level_bufs, Level &L) {
+                                       std::vector<void *> &level_bufs, Level &L, unsigned long long *ovf) {
     const uint32_t S = part_sample_stride(), nout = L.nout;
+    L.d_ovf = ovf;
     const uint64_t piece = kChunkKeys / S;
     // sample = the first 1/S of every chunk; per parent: keys / sampled keys
     std::vector<DevChunk> sample;
@@ -644,10 +667,9 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
     OKM_TRY(pool_get(c->pool, cp.size(), &d_cp));
     OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
     OKM_TRY(pool_get(c->pool, (size_t)nout, &L.d_ends));
-    OKM_TRY(pool_get(c->pool, 1, &L.d_ovf));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
     for (void *p : {(void *)d_segs, (void *)d_chunks, (void *)d_sample, (void *)d_cp, (void *)L.d_offs,
-                    (void *)L.d_ends, (void *)L.d_ovf, (void *)scan_tmp})
+                    (void *)L.d_ends, (void *)scan_tmp})
         level_bufs.push_back(p);
     L.padded = (uint64_t)limit;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &L.lk));
@@ -656,12 +678,11 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &L.lc));
         level_bufs.push_back(L.lc);
     }
-    HIP_TRY(hipMemcpyAsync(d_segs, psegs.data(), psegs.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_sample, sample.data(), sample.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_cp, cp.data(), cp.size() * sizeof(DevCapParent), hipMemcpyHostToDevice, c->stream));
+    OKM_TRY(h2d(c, d_segs, psegs.data(), psegs.size() * sizeof(DevSeg)));
+    OKM_TRY(h2d(c, d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk)));
+    OKM_TRY(h2d(c, d_sample, sample.data(), sample.size() * sizeof(DevChunk)));
+    OKM_TRY(h2d(c, d_cp, cp.data(), cp.size() * sizeof(DevCapParent)));
     HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(L.d_ovf, 0, sizeof(unsigned long long), c->stream));
     uint64_t sampled_keys = 0;
     for (const DevChunk &ch : sample) sampled_keys += ch.len;
     c->timer.begin(c->stream);
@@ -735,10 +756,18 @@ static uint32_t log2_floor(uint64_t x) {
 }
 
 // Count the items in LDS (okm_count.hip), then gather their sorted runs into
-// the dense result table.  Releases level_bufs, d_items and d_segs.
+// the dense result table.  The table is first sized by the instance bound
+// (in_total), so the distinct total is read back once, at the end; when that
+// much memory is not to be had, the count is read first and the table sized
+// exactly.  Releases level_bufs, d_items and d_segs.
+// guard (a speculative launch over round-0 items, make_items' flags): the
+// kernels return at once when guard[0] or guard[1] is set; then *aborted is
+// set, hguard[0..2] receives the flags, and the caller keeps level_bufs,
+// d_items and d_segs.
 static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems,
                                     uint64_t out_total, uint64_t in_total, bool weighted,
-                                    std::vector<void *> &level_bufs) {
+                                    std::vector<void *> &level_bufs, const unsigned long long *guard = nullptr,
+                                    unsigned long long *hguard = nullptr, bool *aborted = nullptr) {
     uint64_t *sk, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
@@ -748,39 +777,76 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
     uint32_t *defer;
     OKM_TRY(pool_get(c->pool, nitems, &defer));
+    auto release_own = [&]() {
+        for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer})
+            c->pool.put(p);
+    };
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide);
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard);
     c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
     HIP_TRY(hipGetLastError());
-    unsigned long long hv[2];
+    // one-pass: the result table sized by the instance bound
+    const uint64_t bound = std::max<uint64_t>(in_total, 1);
+    uint64_t *rk = nullptr, *rc = nullptr;
+    bool one_pass = c->pool.get(bound * 8 * c->kw, (void **)&rk) == OKM_OK;
+    if (one_pass && c->pool.get(bound * 8, (void **)&rc) != OKM_OK) {
+        c->pool.put(rk);
+        one_pass = false;
+    }
+    if (!one_pass) (void)hipGetLastError();  // the exact-size path below
+    if (one_pass) {
+        c->timer.begin(c->stream);
+        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, guard, c->flag);
+        c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
+        HIP_TRY(hipGetLastError());
+    }
+    unsigned long long *hv = c->hres + 1024;  // [0] distinct, [1] error word, [2..4] guard words
     HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    if (guard)
+        HIP_TRY(hipMemcpyAsync(&hv[2], guard, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     c->hprof.mark("count+scan+sync");
+    if (guard) {
+        for (int i = 0; i < 3; ++i) hguard[i] = hv[2 + i];
+        *aborted = (hv[2] | hv[3]) != 0;
+        if (*aborted) {
+            release_own();
+            if (one_pass) {
+                c->pool.put(rk);
+                c->pool.put(rc);
+            }
+            return OKM_OK;
+        }
+    }
     if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     const uint64_t nd = hv[0];
-    if (!c->timer.stats.empty()) c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
-    c->timer.begin(c->stream);
-    launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide);
-    c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
-    HIP_TRY(hipGetLastError());
-    OKM_TRY(sync(c));
+    if (!c->timer.stats.empty()) {
+        c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
+        if (one_pass) c->timer.add_bytes("compact_items", 32.0 * (double)nd);
+    }
+    if (one_pass) {
+        c->res_keys = rk;
+        c->res_counts = rc;
+    } else {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        c->timer.begin(c->stream);
+        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts,
+                             c->wide);
+        c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
+        HIP_TRY(hipGetLastError());
+        OKM_TRY(sync(c));
+    }
     for (void *p : level_bufs) c->pool.put(p);
     c->pool.put(d_segs);
     c->pool.put(d_items);
-    c->pool.put(sk);
-    c->pool.put(sc);
-    c->pool.put(n_out);
-    c->pool.put(dense_off);
-    c->pool.put(scan_tmp);
-    c->pool.put(defer);
+    release_own();
     c->n_res = nd;
     c->info.distinct = nd;
     c->counted = true;
@@ -891,8 +957,8 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
     OKM_TRY(pool_get(c->pool, 2, &flags));
     for (void *p : {(void *)d_parts, (void *)d_rbins, (void *)itemtot, (void *)offs, (void *)tmp, (void *)flags})
         bufs.push_back(p);
-    HIP_TRY(hipMemcpyAsync(d_parts, parts.data(), parts.size() * sizeof(DevSortedPart), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_rbins, rbins.data(), rbins.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
+    OKM_TRY(h2d(c, d_parts, parts.data(), parts.size() * sizeof(DevSortedPart)));
+    OKM_TRY(h2d(c, d_rbins, rbins.data(), rbins.size() * sizeof(DevSeg)));
     HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(itemtot + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
@@ -992,7 +1058,6 @@ static okm_status do_count(okm_ctx *c) {
     DevSeg *d_segs = nullptr;
     uint32_t nitems = 0;
     uint64_t out_total = 0, in_total = 0;
-    bool device_items = false;
 
     // Round 0 on the device: every part takes part (0 bits = gathered as one
     // bin), so the level's bins are the count work list in key order and are
@@ -1011,63 +1076,60 @@ static okm_status do_count(okm_ctx *c) {
             uint64_t keys_in = 0;
             for (const Part &p : parts) keys_in += p.len;
             const bool try_sampled = part_tile_mode() && part_sample_stride() > 1 && keys_in >= (1ull << 22);
+            // The level's bins become the items and are counted at once
+            // (speculatively: the count kernels check make_items' flags), so
+            // the first host sync of the round comes after the compaction.
             for (int attempt = 0;; ++attempt) {
+                unsigned long long *flags;  // [0] children too big, [1] 1: slot overflow | 2: 64-bit counts, [2] max
+                OKM_TRY(pool_get(c->pool, 3, &flags));
+                level_bufs.push_back(flags);
+                HIP_TRY(hipMemsetAsync(flags, 0, 3 * sizeof(unsigned long long), c->stream));
                 Level L;
-                OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L, try_sampled && !attempt));
+                OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L,
+                                     try_sampled && !attempt ? flags + 1 : nullptr));
                 std::vector<DevParent> par(parts.size());
                 for (uint32_t i = 0; i < parts.size(); ++i)
                     par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
                 DevParent *d_par;
-                unsigned long long *flags;
                 OKM_TRY(pool_get(c->pool, par.size(), &d_par));
-                OKM_TRY(pool_get(c->pool, 2, &flags));
                 OKM_TRY(pool_get(c->pool, L.nout, &d_items));
                 OKM_TRY(pool_get(c->pool, L.nout, &d_segs));
                 level_bufs.push_back(d_par);
-                level_bufs.push_back(flags);
-                HIP_TRY(hipMemcpyAsync(d_par, par.data(), par.size() * sizeof(DevParent), hipMemcpyHostToDevice,
-                                       c->stream));
-                HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
+                OKM_TRY(h2d(c, d_par, par.data(), par.size() * sizeof(DevParent)));
                 launch_make_items(c->stream, L.d_offs, L.d_ends, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc,
                                   d_items, d_segs, item_max, capbits, flags, c->kw);
                 HIP_TRY(hipGetLastError());
+                c->hprof.mark("split.round_launch");
+                c->info.work_items = L.nout;
                 unsigned long long hf[3] = {0, 0, 0};
-                HIP_TRY(hipMemcpyAsync(hf, flags, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-                if (L.d_ovf)
-                    HIP_TRY(hipMemcpyAsync(&hf[2], L.d_ovf, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                           c->stream));
-                OKM_TRY(sync(c));
-                c->hprof.mark("split.round");
-                if (hf[2]) {  // a child outgrew its sampled slot: redo the pass exactly
-                    c->pool.put(d_items);
-                    c->pool.put(d_segs);
-                    d_items = nullptr;
-                    d_segs = nullptr;
+                bool aborted = false;
+                OKM_TRY(count_and_compact(c, d_items, d_segs, L.nout, L.padded, L.total, weighted, level_bufs, flags,
+                                          hf, &aborted));
+                if (!aborted) {
+                    c->info.max_partition = hf[2];
+                    return OKM_OK;
+                }
+                c->pool.put(d_items);
+                c->pool.put(d_segs);
+                d_items = nullptr;
+                d_segs = nullptr;
+                if (hf[1] & 1) {  // a child outgrew its sampled slot: redo the pass exactly
                     c->info.levels -= 1;
                     continue;
                 }
-                if (hf[0] == 0) {
-                    device_items = true;
-                    nitems = L.nout;
-                    out_total = L.padded;  // items' output slots mirror their input slots
-                    in_total = L.total;
-                    c->info.max_partition = hf[1];
-                    if (hf[1] >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
-                } else {
-                    c->pool.put(d_items);
-                    c->pool.put(d_segs);
-                    d_items = nullptr;
-                    d_segs = nullptr;
+                if (hf[0]) {  // children still too big for one item: host rounds below
                     OKM_TRY(split_children_host(c, L, segtab, parts, all, bits));
+                    break;
                 }
-                break;
+                weighted = true;  // a child of >= 2^32 instances: 64-bit counting
+                c->info.levels -= 1;
             }
         }
     }
 
     // Further rounds on the host view (only when a child is still too big:
     // skewed or adversarial key distributions).
-    for (int round = 1; !device_items && round < 64; ++round) {
+    for (int round = 1; round < 64; ++round) {
         std::vector<uint32_t> todo, bits;
         for (uint32_t i = 0; i < parts.size(); ++i) {
             const uint32_t b = plan(i);
@@ -1081,20 +1143,19 @@ static okm_status do_count(okm_ctx *c) {
         OKM_TRY(split_children_host(c, L, segtab, parts, todo, bits));
     }
 
+    // items on the host view: the parts themselves
     std::vector<DevItem> items;
-    if (!device_items) {
-        nitems = (uint32_t)parts.size();
-        items.resize(nitems);
-        for (uint32_t i = 0; i < nitems; ++i) {
-            // distinct <= instances, and <= 2^remaining-bits
-            const uint32_t rem = twok - parts[i].consumed;
-            const uint64_t bound = rem >= 63 ? parts[i].len : std::min<uint64_t>(parts[i].len, 1ull << rem);
-            items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total, rem, 0};
-            out_total += bound;
-            in_total += parts[i].len;
-            c->info.max_partition = std::max(c->info.max_partition, parts[i].len);
-            if (parts[i].len >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
-        }
+    nitems = (uint32_t)parts.size();
+    items.resize(nitems);
+    for (uint32_t i = 0; i < nitems; ++i) {
+        // distinct <= instances, and <= 2^remaining-bits
+        const uint32_t rem = twok - parts[i].consumed;
+        const uint64_t bound = rem >= 63 ? parts[i].len : std::min<uint64_t>(parts[i].len, 1ull << rem);
+        items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total, rem, 0};
+        out_total += bound;
+        in_total += parts[i].len;
+        c->info.max_partition = std::max(c->info.max_partition, parts[i].len);
+        if (parts[i].len >= (1ull << 32)) weighted = true;  // u32 LDS counts could overflow
     }
     c->info.work_items = nitems;
     if (nitems == 0) {
@@ -1104,12 +1165,10 @@ static okm_status do_count(okm_ctx *c) {
         c->info.distinct = 0;
         return OKM_OK;
     }
-    if (!device_items) {
-        OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
-        OKM_TRY(pool_get(c->pool, nitems, &d_items));
-        HIP_TRY(hipMemcpyAsync(d_segs, segtab.data(), segtab.size() * sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(d_items, items.data(), nitems * sizeof(DevItem), hipMemcpyHostToDevice, c->stream));
-    }
+    OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
+    OKM_TRY(pool_get(c->pool, nitems, &d_items));
+    OKM_TRY(h2d(c, d_segs, segtab.data(), segtab.size() * sizeof(DevSeg)));
+    OKM_TRY(h2d(c, d_items, items.data(), nitems * sizeof(DevItem)));
     c->hprof.mark("items.build");
     return count_and_compact(c, d_items, d_segs, nitems, out_total, in_total, weighted, level_bufs);
 }
@@ -1206,7 +1265,9 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->shift1 = 2u * k - c->l1_bits;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->hpin, kHpinBytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->hres, kHresWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         delete c;
         return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
@@ -1226,6 +1287,8 @@ void okm_destroy(okm_ctx *c) {
     if (c->cursor) (void)hipFree(c->cursor);
     if (c->flag) (void)hipFree(c->flag);
     if (c->l1cap) (void)hipFree(c->l1cap);
+    if (c->hpin) (void)hipHostFree(c->hpin);
+    if (c->hres) (void)hipHostFree(c->hres);
     if (c->staging) (void)hipFree(c->staging);
     if (c->pinned) (void)hipHostFree(c->pinned);
     (void)hipStreamDestroy(c->stream);

@@ -118,7 +118,8 @@ uint32_t count_dense_bits();
 // kernel of the launch.
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
-                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide);
+                        unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
+                        const unsigned long long *guard = nullptr);
 
 // A part that took part in a device-side split round: its children are the
 // output bins [out_base, out_base + nlocal) of the round.
@@ -130,7 +131,9 @@ struct DevParent {
 // One item (and one segment) per output bin of a split round, straight from
 // the device offsets (nout + 1 entries; bin b ends at ends[b], or at
 // offs[b + 1] when ends is null).  flags[0] += children that are still too
-// big for one item; flags[1] = max child length.
+// big for one item; flags[1] |= 2 when a child needs 64-bit counting;
+// flags[2] = max child length.  Count and compact kernels given `guard`
+// (= flags) return at once when guard[0] or guard[1] is set.
 void launch_make_items(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
                        const DevParent *parents, uint32_t nparents, const uint64_t *lk, const uint64_t *lc,
                        DevItem *items, DevSeg *segs, uint64_t item_max, uint32_t capbits,
@@ -155,11 +158,13 @@ void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t npar
                          bool wide);
 void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off);
 
-// Gather the per-item results into dense arrays given exclusive offsets.
+// Gather the per-item results into dense arrays given exclusive offsets
+// (nothing when a guard word or *err is set).
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts,
-                          uint64_t *dst_keys, uint64_t *dst_counts, bool wide);
+                          uint64_t *dst_keys, uint64_t *dst_counts, bool wide,
+                          const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr);
 
 // Filter (count >= min) with order preserved; flags/scan in tmp.
 void launch_filter_count(void *stream, const uint64_t *counts, uint64_t n, uint64_t min_count,
