@@ -122,6 +122,16 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
     return wbase + inc - v;
 }
 
+// Per-item output counts: u64 for weighted launches, u32 otherwise (every
+// count of an unweighted launch is < 2^32; the compaction widens them).
+template <bool W>
+__device__ __forceinline__ void store_count(uint64_t *out_counts, uint64_t o, uint64_t c) {
+    if (W)
+        out_counts[o] = c;
+    else
+        reinterpret_cast<uint32_t *>(out_counts)[o] = (uint32_t)c;
+}
+
 // Top kHomeBits of the r remaining bits (r > kHomeBits): monotone in the key.
 __device__ __forceinline__ uint32_t home_of(uint64_t key, uint32_t r) {
     return (uint32_t)(key >> (r - kHomeBits)) & (kHomes - 1);
@@ -275,7 +285,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
             ++i;
         } while (i < a + n && KeyOps<KT>::eq(sk[i], key));
         out_keys[o] = key;
-        out_counts[o] = c;
+        store_count<W>(out_counts, o, c);
         ++o;
     }
     return __builtin_amdgcn_readfirstlane(D);
@@ -434,7 +444,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             if (tg[q] != kEmptyKey) {
                 const uint64_t o = out_off + ho[q] + lq[q];
                 out_keys[o] = tg[q];
-                out_counts[o] = W ? (uint64_t)tc64[kHomesPer * t + q] : (uint64_t)nq[q];
+                store_count<W>(out_counts, o, W ? (uint64_t)tc64[kHomesPer * t + q] : (uint64_t)nq[q]);
             }
         }
     }
@@ -450,7 +460,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             const uint32_t h = home_of(x, r);
             const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + (tag[h] < x ? 1u : 0u);
             out_keys[o] = x;
-            out_counts[o] = (uint64_t)pc[k];
+            store_count<W>(out_counts, o, (uint64_t)pc[k]);
         }
     }
     PMARK(7);
@@ -525,7 +535,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
         const uint32_t j = t * kHomesPer + q;
         if (j < nslots && cnt[j] != 0) {
             out_keys[o] = slot_key[j];
-            out_counts[o] = (uint64_t)cnt[j];
+            store_count<W>(out_counts, o, (uint64_t)cnt[j]);
             ++o;
         }
     }

@@ -255,7 +255,7 @@ void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const uns
 // Result assembly
 // ---------------------------------------------------------------------------
 
-template <typename KT>
+template <typename KT, bool NARROW>
 __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict__ items,
                                                        uint32_t nitems, const ull *__restrict__ n_out,
                                                        const ull *__restrict__ dense_off,
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
         const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
         for (uint64_t j = threadIdx.x; j < n; j += 256) {
             dk[dst + j] = sk[src + j];
-            dc[dst + j] = sc[src + j];
+            dc[dst + j] = NARROW ? (uint64_t)reinterpret_cast<const uint32_t *>(sc)[src + j] : sc[src + j];
         }
     }
 }
@@ -278,18 +278,27 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts, uint64_t *dst_keys,
-                          uint64_t *dst_counts, bool wide, const unsigned long long *guard,
+                          uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
                           const unsigned long long *err) {
     if (!nitems) return;
-    const uint32_t grid = nitems < 8192u ? nitems : 8192u;
-    if (wide)
-        hipLaunchKernelGGL(k_compact_items<K128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
-                           dense_off, reinterpret_cast<const K128 *>(src_keys), src_counts,
-                           reinterpret_cast<K128 *>(dst_keys), dst_counts, guard, err);
+    const dim3 g(nitems < 8192u ? nitems : 8192u), b(256);
+    hipStream_t s = (hipStream_t)stream;
+    const K128 *sk2 = reinterpret_cast<const K128 *>(src_keys);
+    K128 *dk2 = reinterpret_cast<K128 *>(dst_keys);
+    const ull *sk1 = reinterpret_cast<const ull *>(src_keys);
+    ull *dk1 = reinterpret_cast<ull *>(dst_keys);
+    if (wide && narrow)
+        hipLaunchKernelGGL((k_compact_items<K128, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk2, src_counts,
+                           dk2, dst_counts, guard, err);
+    else if (wide)
+        hipLaunchKernelGGL((k_compact_items<K128, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk2,
+                           src_counts, dk2, dst_counts, guard, err);
+    else if (narrow)
+        hipLaunchKernelGGL((k_compact_items<ull, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk1, src_counts,
+                           dk1, dst_counts, guard, err);
     else
-        hipLaunchKernelGGL(k_compact_items<ull>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, nitems, n_out,
-                           dense_off, reinterpret_cast<const ull *>(src_keys), src_counts,
-                           reinterpret_cast<ull *>(dst_keys), dst_counts, guard, err);
+        hipLaunchKernelGGL((k_compact_items<ull, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk1,
+                           src_counts, dk1, dst_counts, guard, err);
 }
 
 constexpr int kFilterBlock = 256;

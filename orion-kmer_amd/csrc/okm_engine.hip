@@ -801,7 +801,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     if (!one_pass) (void)hipGetLastError();  // the exact-size path below
     if (one_pass) {
         c->timer.begin(c->stream);
-        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, guard, c->flag);
+        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, !weighted, guard,
+                             c->flag);
         c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
         HIP_TRY(hipGetLastError());
     }
@@ -826,9 +827,11 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     }
     if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     const uint64_t nd = hv[0];
+    const double staged = 8.0 * c->kw + (weighted ? 8.0 : 4.0);  // per distinct key: staged (key, count)
+    const double dense = 8.0 * c->kw + 8.0;                      // ... and its dense result entry
     if (!c->timer.stats.empty()) {
-        c->timer.stats[c->timer.id_of("count_items")].alg_bytes += 16.0 * (double)nd;
-        if (one_pass) c->timer.add_bytes("compact_items", 32.0 * (double)nd);
+        c->timer.stats[c->timer.id_of("count_items")].alg_bytes += staged * (double)nd;
+        if (one_pass) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
     }
     if (one_pass) {
         c->res_keys = rk;
@@ -838,8 +841,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts,
-                             c->wide);
-        c->timer.end(c->stream, "compact_items", 32.0 * (double)nd);
+                             c->wide, !weighted);
+        c->timer.end(c->stream, "compact_items", (staged + dense) * (double)nd);
         HIP_TRY(hipGetLastError());
         OKM_TRY(sync(c));
     }

@@ -108,7 +108,7 @@ void launch_exclusive_scan(void *stream, const unsigned long long *in, unsigned 
                            uint64_t n, unsigned long long *tmp);
 
 // LDS counting of partitions (okm_count.hip); writes sorted distinct
-// (key,count) at out_off and n_out[item].  ctl[0] = error word, ctl[1] =
+// (key,count) at out_off and n_out[item] (counts u32 unless weighted).  ctl[0] = error word, ctl[1] =
 // deferred-item count (both zeroed before the launch).  An item holds at most count_item_capacity() instances unless
 // its rem_bits <= count_dense_bits() (direct-address counting, any size).
 uint32_t count_item_capacity();
@@ -159,11 +159,12 @@ void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t npar
 void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off);
 
 // Gather the per-item results into dense arrays given exclusive offsets
-// (nothing when a guard word or *err is set).
+// (nothing when a guard word or *err is set).  narrow: the per-item counts
+// are u32 (unweighted count launches), widened to u64 here.
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts,
-                          uint64_t *dst_keys, uint64_t *dst_counts, bool wide,
+                          uint64_t *dst_keys, uint64_t *dst_counts, bool wide, bool narrow,
                           const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr);
 
 // Filter (count >= min) with order preserved; flags/scan in tmp.
