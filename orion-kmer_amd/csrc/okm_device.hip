@@ -117,9 +117,10 @@ void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t 
                        parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw);
 }
 
-// Sampled partition capacities: est = H[b] * scale of b's parent; the slot
-// gets est + 1% + 6 sigma (sigma = scale * sqrt(H[b]), the sampling error)
-// + 64 keys, rounded up to 16 keys.
+// Sampled partition capacities: the slot of bin b gets scale * (sqrt(s) + 3)^2
+// keys (s = H[b], the bin's sampled count; (sqrt(s) + 3)^2 = s + 6 sqrt(s) + 9
+// bounds the Poisson mean that an observed s allows at ~6 sigma, also when s
+// came out low), + 1% + 64, rounded up to 16 keys.
 __global__ __launch_bounds__(256) void k_part_capacity(ull *__restrict__ H, uint32_t nout,
                                                        const DevCapParent *__restrict__ parents, uint32_t nparents,
                                                        double mul) {
@@ -131,7 +132,8 @@ __global__ __launch_bounds__(256) void k_part_capacity(ull *__restrict__ H, uint
         if (parents[mid].out_base <= i) lo = mid; else hi = mid;
     }
     const double scale = parents[lo].scale, s = (double)H[i];
-    const double c = (s * scale * 1.01 + 6.0 * scale * sqrt(s) + 64.0) * mul;
+    const double r = sqrt(s) + 3.0;
+    const double c = (r * r * scale * 1.01 + 64.0) * mul;
     H[i] = ((ull)c + 15) & ~15ull;
 }
 

@@ -281,6 +281,7 @@ struct okm_ctx {
     size_t Hg_cap = 0;
     unsigned long long *flag = nullptr;  // overflow word
     unsigned long long *l1cap = nullptr; // sampled L1: cap_end | start | overflow
+    unsigned long long *curpad = nullptr;  // sampled L1 claim cursors, OKM_L1_CUR_STRIDE apart
     uint8_t *staging = nullptr;          // device copy of a host batch
     size_t staging_cap = 0;
     uint8_t *pinned = nullptr;           // pinned host staging
@@ -356,6 +357,18 @@ static okm_status sync(okm_ctx *c) {
     return OKM_OK;
 }
 
+// Several small host tables laid out in one buffer (256-B aligned), so that
+// they reach the device in a single copy.
+struct TablePack {
+    std::vector<uint8_t> bytes;
+    template <typename T> size_t add(const std::vector<T> &v) {
+        const size_t at = (bytes.size() + 255) & ~size_t(255);
+        bytes.resize(at + v.size() * sizeof(T));
+        if (!v.empty()) memcpy(bytes.data() + at, v.data(), v.size() * sizeof(T));
+        return at;
+    }
+};
+
 // Host-to-device copy of a small table, staged in pinned memory so that the
 // DMA reads it directly (a pageable source takes a bounce copy and a blit).
 static okm_status h2d(okm_ctx *c, void *dst, const void *src, size_t bytes) {
@@ -415,26 +428,33 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     const double scale = (double)n / (double)sbytes;
     const char *dbg = getenv("OKM_L1_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
     const double mul = dbg ? atof(dbg) : 1.0;
-    // sum_b est_b <= n (windows <= bytes); sum_b sqrt(s_b) <= sqrt(nb * sbytes)
-    const uint64_t limit = (uint64_t)(1.01 * (double)n + 6.0 * scale * std::sqrt((double)nb * (double)sbytes) +
+    // sum_b scale s_b <= n (windows <= bytes); sum_b sqrt(s_b) <= sqrt(nb * sbytes)
+    const uint64_t limit = (uint64_t)(1.01 * ((double)n + 6.0 * scale * std::sqrt((double)nb * (double)sbytes) +
+                                              9.0 * scale * nb) +
                                       (double)nb * (256.0 + align)) + 64;
     OKM_TRY(ensure_hg(c, nb));
     HIP_TRY(hipMemsetAsync(c->Hg, 0, nb * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     launch_extract_hist(c->stream, d_seq, gs, nullptr, c->Hg);
     c->timer.end(c->stream, "extract_sample", (double)sbytes);
-    launch_l1_capacity(c->stream, c->Hg, nb, scale, mul, align, limit, c->cursor, c->l1cap);
+    // l1cap: cap_end[nb] | start[nb + 1] | overflow; the claim cursors stay in
+    // their own (line-aligned) array: placing them beside the other words slowed
+    // the claims by 25 %
+    unsigned long long *cur = c->curpad;
+    launch_l1_capacity(c->stream, c->Hg, nb, scale, mul, align, limit, cur, c->l1cap);
     HIP_TRY(hipGetLastError());
     Run run;
     OKM_TRY(pool_get(c->pool, limit * c->kw, &run.keys));
     c->timer.begin(c->stream);
-    launch_extract_scatter(c->stream, d_seq, g, nullptr, c->cursor, run.keys, c->l1cap, c->l1cap + 2 * nb + 1);
+    launch_extract_scatter(c->stream, d_seq, g, nullptr, cur, run.keys, c->l1cap, c->l1cap + 2 * nb + 1);
     c->timer.end(c->stream, "extract_scatter", (double)n);
+    launch_fill_line_tails(c->stream, cur, nb, run.keys, c->wide, c->l1cap);
     HIP_TRY(hipGetLastError());
-    unsigned long long *ends = c->hres, *cap = c->hres + nb;  // nb + 2 nb + 2 <= 1024 words
-    HIP_TRY(hipMemcpyAsync(ends, c->cursor, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    unsigned long long *cap = c->hres, *ends = c->hres + 2 * nb + 2;  // 3 nb + 2 <= 1024 words
     HIP_TRY(hipMemcpyAsync(cap, c->l1cap, (2 * nb + 2) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
+    HIP_TRY(hipMemcpy2DAsync(ends, sizeof(unsigned long long), cur, OKM_L1_CUR_STRIDE * sizeof(unsigned long long),
+                             sizeof(unsigned long long), nb, hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     if (cap[2 * nb + 1]) {  // some bin outgrew its sampled capacity: redo exactly
         c->pool.put(run.keys);
@@ -454,8 +474,6 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
         c->pool.put(run.keys);
         return OKM_OK;
     }
-    launch_fill_line_tails(c->stream, c->cursor, nb, run.keys, c->wide);
-    HIP_TRY(hipGetLastError());
     c->runs.push_back(std::move(run));
     c->info.kmers += total;
     c->hprof.mark("l1.sampled");
@@ -651,26 +669,28 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
         }
         const double scale = sl ? (double)len / (double)sl : 1.0;
         cp[t] = DevCapParent{L.out_base[t], 0, scale};
-        // sum_b est_b <= len; sum_b sqrt(s_b) <= sqrt(2^bits * sl); + 80 per bin (64 + rounding)
+        // sum_b scale (sqrt(s_b) + 3)^2 <= scale (sl + 6 sqrt(2^bits * sl) + 9 * 2^bits) (s_b sum to <= sl);
+        // + 80 per bin (64 + rounding)
         const double nl = (double)(1u << bits[t]);
-        limit += 1.01 * (double)len + 6.0 * scale * std::sqrt(nl * (double)sl) + 80.0 * nl;
+        limit += 1.01 * scale * ((double)sl + 6.0 * std::sqrt(nl * (double)sl) + 9.0 * nl) + 80.0 * nl;
     }
     const char *dbg = getenv("OKM_PART_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
     const double mul = dbg ? atof(dbg) : 1.0;
-    DevSeg *d_segs;
-    DevChunk *d_chunks, *d_sample;
-    DevCapParent *d_cp;
+    // the four host tables travel in one copy
+    TablePack pack;
+    const size_t o_segs = pack.add(psegs), o_chunks = pack.add(chunks), o_sample = pack.add(sample),
+                 o_cp = pack.add(cp);
+    uint8_t *blob;
     unsigned long long *scan_tmp;
-    OKM_TRY(pool_get(c->pool, psegs.size(), &d_segs));
-    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
-    OKM_TRY(pool_get(c->pool, sample.size(), &d_sample));
-    OKM_TRY(pool_get(c->pool, cp.size(), &d_cp));
+    OKM_TRY(pool_get(c->pool, pack.bytes.size(), &blob));
     OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
     OKM_TRY(pool_get(c->pool, (size_t)nout, &L.d_ends));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
-    for (void *p : {(void *)d_segs, (void *)d_chunks, (void *)d_sample, (void *)d_cp, (void *)L.d_offs,
-                    (void *)L.d_ends, (void *)scan_tmp})
-        level_bufs.push_back(p);
+    for (void *p : {(void *)blob, (void *)L.d_offs, (void *)L.d_ends, (void *)scan_tmp}) level_bufs.push_back(p);
+    DevSeg *d_segs = reinterpret_cast<DevSeg *>(blob + o_segs);
+    DevChunk *d_chunks = reinterpret_cast<DevChunk *>(blob + o_chunks);
+    DevChunk *d_sample = reinterpret_cast<DevChunk *>(blob + o_sample);
+    DevCapParent *d_cp = reinterpret_cast<DevCapParent *>(blob + o_cp);
     L.padded = (uint64_t)limit;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &L.lk));
     level_bufs.push_back(L.lk);
@@ -678,10 +698,7 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &L.lc));
         level_bufs.push_back(L.lc);
     }
-    OKM_TRY(h2d(c, d_segs, psegs.data(), psegs.size() * sizeof(DevSeg)));
-    OKM_TRY(h2d(c, d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk)));
-    OKM_TRY(h2d(c, d_sample, sample.data(), sample.size() * sizeof(DevChunk)));
-    OKM_TRY(h2d(c, d_cp, cp.data(), cp.size() * sizeof(DevCapParent)));
+    OKM_TRY(h2d(c, blob, pack.bytes.data(), pack.bytes.size()));
     HIP_TRY(hipMemsetAsync(c->Hg, 0, ((size_t)nout + 1) * sizeof(unsigned long long), c->stream));
     uint64_t sampled_keys = 0;
     for (const DevChunk &ch : sample) sampled_keys += ch.len;
@@ -1269,6 +1286,7 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->curpad, (size_t)c->nbins * OKM_L1_CUR_STRIDE * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&c->hpin, kHpinBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->hres, kHresWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -1290,6 +1308,7 @@ void okm_destroy(okm_ctx *c) {
     if (c->cursor) (void)hipFree(c->cursor);
     if (c->flag) (void)hipFree(c->flag);
     if (c->l1cap) (void)hipFree(c->l1cap);
+    if (c->curpad) (void)hipFree(c->curpad);
     if (c->hpin) (void)hipHostFree(c->hpin);
     if (c->hres) (void)hipHostFree(c->hres);
     if (c->staging) (void)hipFree(c->staging);

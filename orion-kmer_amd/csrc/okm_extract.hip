@@ -186,7 +186,7 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
         const uint32_t h = hist[t];
         ull g = ~0ull;
         if (h) {
-            const ull p = atomicAdd(&cursor[t], (ull)h);
+            const ull p = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)h);
             if (p + h <= cap_end[t])
                 g = p;
             else
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
             ull cp = 0;
             if (!HC && t < nb) {
                 ch = hist[t];
-                if (ch) cp = atomicAdd(&cursor[t], (ull)ch);
+                if (ch) cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);
             }
             __syncthreads();
 #pragma unroll
@@ -295,14 +295,13 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
 }
 
 __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__ end, uint32_t nbins,
-                                                         uint64_t *__restrict__ keys) {
+                                                         uint64_t *__restrict__ keys, const ull *__restrict__ cap) {
     const uint32_t b = blockIdx.x * 16 + (threadIdx.x >> 4), j = threadIdx.x & 15;
     if (b >= nbins) return;
-    const ull e = end[b];
+    const ull e = end[cap ? b * OKM_L1_CUR_STRIDE : b];
+    if (cap && e > cap[b]) return;  // an overflowed bin (the batch is redone)
     if (e + j < ((e + 15) & ~15ull)) keys[e + j] = kEmptyKey;
 }
-
-void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide);
 
 // ---------------------------------------------------------------------------
 // k in 33..64: two-u64 keys (K128, MSB-first over 2k bits), runtime k
@@ -440,10 +439,11 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
 }
 
 __global__ __launch_bounds__(256) void k_fill_line_tails_wide(const ull *__restrict__ end, uint32_t nbins,
-                                                              K128 *__restrict__ keys) {
+                                                              K128 *__restrict__ keys, const ull *__restrict__ cap) {
     const uint32_t b = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
     if (b >= nbins) return;
-    const ull e = end[b];
+    const ull e = end[cap ? b * OKM_L1_CUR_STRIDE : b];
+    if (cap && e > cap[b]) return;
     if (e + j < ((e + 7) & ~7ull)) keys[e + j] = KeyOps<K128>::empty();
 }
 
@@ -492,19 +492,20 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
     }
 }
 
-void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide) {
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide,
+                            const unsigned long long *cap) {
     if (wide)
         hipLaunchKernelGGL(k_fill_line_tails_wide, dim3((nbins + 31) / 32), dim3(256), 0, (hipStream_t)stream, end,
-                           nbins, reinterpret_cast<K128 *>(keys));
+                           nbins, reinterpret_cast<K128 *>(keys), cap);
     else
         hipLaunchKernelGGL(k_fill_line_tails, dim3((nbins + 15) / 16), dim3(256), 0, (hipStream_t)stream, end,
-                           nbins, keys);
+                           nbins, keys, cap);
 }
 
 // Sampled L1 capacities (one block, nb <= kMaxL1Bins): Hs holds the window
-// counts of a sample of the tiles; est_b = Hs[b] * scale, and bin b gets
-// est + 6 sigma (sigma = scale * sqrt(Hs[b]), the sampling error) + 1% + 256
-// keys, rounded up to `align` keys.  Starts are exclusive sums (line
+// counts of a sample of the tiles; bin b gets scale * (sqrt(s) + 3)^2 keys
+// (s = Hs[b]; s + 6 sqrt(s) + 9 bounds the Poisson mean an observed s allows
+// at ~6 sigma) + 1% + 256, rounded up to `align` keys.  Starts are exclusive sums (line
 // aligned); l1cap = [cap_end(nb) | start(nb + 1) | overflow flag].
 __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs, uint32_t nb, double scale,
                                                      double mul, uint32_t align, ull limit, ull *__restrict__ cursor,
@@ -513,8 +514,8 @@ __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs,
     const uint32_t t = threadIdx.x;
     if (t < nb) {
         const double s = (double)Hs[t];
-        const double est = s * scale;
-        const double c = (est * 1.01 + 6.0 * scale * sqrt(s) + 256.0) * mul;
+        const double r = sqrt(s) + 3.0;  // (sqrt(s) + 3)^2: the Poisson mean s allows at ~6 sigma
+        const double c = (r * r * scale * 1.01 + 256.0) * mul;
         cap[t] = ((ull)c + align - 1) / align * align;
     }
     __syncthreads();
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs,
             const ull st = o < limit ? o : limit;
             o += cap[b];
             const ull en = o < limit ? o : limit;
-            cursor[b] = st;
+            cursor[b * OKM_L1_CUR_STRIDE] = st;
             l1cap[b] = en;
             l1cap[nb + b] = st;
         }

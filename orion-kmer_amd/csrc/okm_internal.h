@@ -50,6 +50,12 @@ struct DevItem {
     uint32_t pad;
 };
 
+// Sampled L1 placement: bin b's claim cursor lives at cursor[b * OKM_L1_CUR_STRIDE]
+// (a stride > 1 puts every cursor on its own 128-B line).
+#ifndef OKM_L1_CUR_STRIDE
+#define OKM_L1_CUR_STRIDE 1
+#endif
+
 struct ExtractGeom {
     uint64_t n;        // bytes in the batch
     uint32_t k;
@@ -97,7 +103,9 @@ void launch_part_capacity(void *stream, unsigned long long *H, uint32_t nout, co
                           uint32_t nparents, double mul);
 // Pads [end[b], roundup(end[b], line)) of every bin with the empty key (bins
 // start on 128-B lines: 16 u64 / 8 K128 keys; end = the cursor after the scatter).
-void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide);
+// cap (optional): skip bins whose end passed cap[b] (an overflowed sampled placement).
+void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide,
+                            const unsigned long long *cap = nullptr);
 uint32_t extract_tile();
 uint32_t extract_max_bins();
 uint32_t part_max_bins(bool weighted);
