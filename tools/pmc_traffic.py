@@ -21,7 +21,9 @@ from collections import defaultdict
 
 def engine_name(kname: str) -> str:
     n = re.sub(r"^(void )?okm::k_", "", kname).split("<")[0].split("(")[0]
-    return "count_items" if n == "count_slow" else n
+    # k_extract_hist / k_part_hist run as the samplers (timer names extract_sample /
+    # part_sample) in the sampled placements and as exact passes otherwise
+    return {"count_slow": "count_items", "part_scatter_tile": "part_scatter"}.get(n, n)
 
 
 def load(path, counter):
