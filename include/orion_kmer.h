@@ -171,6 +171,61 @@ okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint6
                                      uint64_t nb, int device, uint64_t *out);
 
 /* ------------------------------------------------------------------------
+ * Device k-mer sets — the read-only callers of the counting path.
+ *
+ * okm_kset replaces the unified HashSet<u64> of a database
+ * (db_types.rs:43-48 get_all_kmers_unified, built at query.rs:36) and its
+ * HashSet::contains probes (query.rs:88): an open-addressing table in HBM
+ * (load <= 1/2, grows by rehash).  k in 1..=32 as the reference (query.rs:30-32).
+ * ---------------------------------------------------------------------- */
+typedef struct okm_kset okm_kset;
+/* capacity_hint: expected distinct keys (sizing only). */
+okm_status okm_kset_create(okm_kset **out, uint8_t k, int device, uint64_t capacity_hint);
+void okm_kset_destroy(okm_kset *s);
+/* HashSet::extend of a reference's keys (db_types.rs:46).  keys_on_device!=0:
+ * `keys` is a device pointer.  *n_new (optional) = keys not present before. */
+okm_status okm_kset_insert(okm_kset *s, const uint64_t *keys, uint64_t n, int keys_on_device,
+                           uint64_t *n_new);
+/* HashSet::len() (db_types.rs:50-53 total_unique_kmers). */
+okm_status okm_kset_size(const okm_kset *s, uint64_t *n);
+/* out[i] = 1 if keys[i] is in the set (host buffers). */
+okm_status okm_kset_contains(okm_kset *s, const uint64_t *keys, uint64_t n, uint8_t *out);
+
+/* query.rs:81-99, per record: hits[r] = number of k-windows of the RAW record
+ * bytes (record.sequence(), no normalize: only A/C/G/T in either case are
+ * valid, so U/u, N and line breaks of multi-line FASTA kill windows) whose
+ * canonical k-mer is in the set.  Record r is seq[offsets[r]..offsets[r+1])
+ * (host memory); hits has n_records entries.  The caller applies the
+ * reference's `len < k -> no output` and `hits >= min_hits` tests. */
+okm_status okm_query_hits(okm_kset *s, const uint8_t *seq, const uint64_t *offsets, uint64_t n_records,
+                          uint32_t *hits);
+/* Same over a DEVICE batch: records joined by OKM_RECORD_SEPARATOR (a
+ * separator after the last record is optional; no other '\n' may occur),
+ * n_records = number of records, d_hits a device array of n_records u32. */
+okm_status okm_query_hits_device(okm_kset *s, const uint8_t *d_seq, uint64_t n_bytes, uint64_t n_records,
+                                 uint32_t *d_hits);
+
+/* classify.rs:176-308 on the device.  okm_classifier_create takes a COUNT
+ * context holding the input's k-mers (classify.rs:135-181, counted with
+ * okm_add_batch + okm_count), keeps the entries with count >=
+ * min_kmer_frequency (classify.rs:195-199) in a device map, and returns
+ * their number (total_unique_kmers_in_input) in *n_input_kmers.  The context
+ * may be destroyed afterwards. */
+typedef struct okm_classifier okm_classifier;
+okm_status okm_classifier_create(okm_classifier **out, okm_ctx *input, uint64_t min_kmer_frequency,
+                                 uint64_t *n_input_kmers);
+void okm_classifier_destroy(okm_classifier *c);
+/* One database (classify.rs:215-308): reference r owns
+ * keys[ref_offsets[r] .. ref_offsets[r+1]) (a HashSet: no duplicates).
+ * ref_matched[r] / ref_sum_depth[r] = input k-mers in reference r and the sum
+ * of their counts (classify.rs:228-236); *db_union = |union of references|
+ * (db_types.rs:50-53); *db_matched / *db_sum_depth = the same two numbers over
+ * the union (classify.rs:237,268-272).  Host buffers. */
+okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, const uint64_t *ref_offsets,
+                                   uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
+                                   uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth);
+
+/* ------------------------------------------------------------------------
  * Instrumentation (bench.py measures kernels with HIP events on the
  * context's own stream).
  * ---------------------------------------------------------------------- */
@@ -234,6 +289,16 @@ okm_key128 okm_canonical_u128(okm_key128 v, uint8_t k);
  * (utils.rs:157-161, raw bytes).  needletail's own gzip/bzip2/xz magic
  * sniffing is applied after that in both cases. */
 okm_status okm_reader_open(okm_reader **out, const char *path, int decompress_by_extension);
+/* okm_reader_open with flags: OKM_READ_RAW = record.sequence() bytes as they
+ * are in the file, no normalize (query.rs:66; multi-line FASTA keeps its
+ * interior line breaks), OKM_READ_IDS = also keep each record's id()
+ * (query.rs:70: the header line after '>'/'@', CR trimmed). */
+#define OKM_READ_RAW 1
+#define OKM_READ_IDS 2
+okm_status okm_reader_open2(okm_reader **out, const char *path, int decompress_by_extension, int flags);
+/* Ids of the records of the last okm_reader_next batch: record r's id is
+ * ids[id_offsets[r] .. id_offsets[r+1]).  Valid until the next call. */
+okm_status okm_reader_ids(const okm_reader *r, const uint8_t **ids, const uint64_t **id_offsets);
 /* Next batch of at most ~max_bytes sequence bytes (at least one record).
  * Pointers stay valid until the next call.  *n_records == 0 at end. */
 okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **seq,

@@ -69,8 +69,23 @@ def load() -> ctypes.CDLL:
     lib.oracle_counter_wide_windows.argtypes = [c_void_p]
     lib.oracle_counter_wide_result.restype = c_uint64
     lib.oracle_counter_wide_result.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]
+    lib.oracle_query_hits.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint8, c_void_p]
     _lib = lib
     return lib
+
+
+def query_hits(seqs: Sequence[bytes], set_keys: np.ndarray, k: int) -> np.ndarray:
+    """query.rs:81-99 restated in C: per-record hit counts over RAW bytes
+    against a sorted unique key array."""
+    lib = load()
+    data = np.frombuffer(b"".join(seqs), dtype=np.uint8) if seqs else np.zeros(0, np.uint8)
+    offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    np.cumsum([len(s) for s in seqs], out=offs[1:])
+    keys = np.ascontiguousarray(set_keys, dtype=np.uint64)
+    hits = np.zeros(len(seqs), dtype=np.uint32)
+    lib.oracle_query_hits(data.ctypes.data, offs.ctypes.data, len(seqs), keys.ctypes.data, len(keys), k,
+                          hits.ctypes.data)
+    return hits
 
 
 class OracleCounter:

@@ -145,16 +145,22 @@ def parse_fastx(data: bytes) -> List[Tuple[bytes, bytes]]:
     if first == b">":
         cur_id = None
         cur_seq: List[bytes] = []
+        def raw_seq(lines_: List[bytes]) -> bytes:
+            # needletail raw_seq()/sequence(): the lines with their interior
+            # line breaks, one trailing CR trimmed
+            sq = b"\n".join(lines_)
+            return sq[:-1] if sq.endswith(b"\r") else sq
+
         for ln in lines:
             if ln.startswith(b">"):
                 if cur_id is not None:
-                    recs.append((cur_id, b"\n".join(cur_seq)))
+                    recs.append((cur_id, raw_seq(cur_seq)))
                 cur_id = ln[1:].rstrip(b"\r")
                 cur_seq = []
             else:
                 cur_seq.append(ln)
         if cur_id is not None:
-            recs.append((cur_id, b"\n".join(cur_seq)))
+            recs.append((cur_id, raw_seq(cur_seq)))
         return recs
     if first == b"@":
         # trailing blank lines after the last record are tolerated
@@ -321,3 +327,175 @@ def compare_sets(k1: int, refs1: Dict[str, set], k2: int, refs2: Dict[str, set],
 def compare_json(d: Dict[str, object]) -> str:
     """serde_json::to_writer_pretty output (2-space indent, no trailing newline)."""
     return json.dumps(d, indent=2, ensure_ascii=False)
+
+
+# --------------------------------------------------------------------------
+# query — query.rs
+# --------------------------------------------------------------------------
+
+def query_hits(seq: bytes, k: int, db_all: set) -> int:
+    """query.rs:86-93 — windows of the RAW sequence (no normalize) whose
+    canonical k-mer is in the unified DB set."""
+    hits = 0
+    for i in range(len(seq) - k + 1):
+        v = seq_to_u64(seq[i:i + k], k)
+        if v is not None and canonical_u64(v, k) in db_all:
+            hits += 1
+    return hits
+
+
+def run_query_bytes(k: int, refs: Dict[str, set], reads_path: str, reads_raw: bytes,
+                    min_hits: int = 1) -> bytes:
+    """query.rs:24-134 on an in-memory reads file; returns the output bytes
+    (matching read ids, input order, one per line)."""
+    if k == 0 or k > 32:  # query.rs:30-32
+        raise OracleError(f"Invalid K-mer size: {k}. Must be between 1 and 32.")
+    db_all = set().union(*refs.values()) if refs else set()  # db_types.rs:43-48
+    data = decompress_by_extension(reads_path, reads_raw)    # query.rs:45
+    try:
+        recs = parse_fastx(data)
+    except OracleError as e:
+        if str(e) == "parse":
+            raise OracleError(f"Failed to parse FASTQ content from: {reads_path!r}")
+        raise OracleError(f"Error reading record from {reads_path!r}")
+    out = []
+    for rid, seq in recs:  # query.rs:63-71 (record.sequence(): raw)
+        if len(seq) < k:    # query.rs:83-85
+            continue
+        if query_hits(seq, k, db_all) >= min_hits:  # query.rs:97
+            out.append(rid + b"\n")
+    return b"".join(out)
+
+
+# --------------------------------------------------------------------------
+# classify — classify.rs
+# --------------------------------------------------------------------------
+
+def rust_f64(x: float) -> str:
+    """serde_json's f64 text (ryu: shortest round-trip digits, decimal for
+    1e-5 <= |x| < 1e16 else d.ddde±x without padding, integers get '.0')."""
+    if x == 0:
+        return "-0.0" if str(x).startswith("-") else "0.0"
+    r = repr(abs(x))
+    neg = x < 0
+    if "e" in r:
+        mant, ex = r.split("e")
+        exp10 = int(ex)
+    else:
+        mant, exp10 = r, 0
+    if "." in mant:
+        ip, fp = mant.split(".")
+    else:
+        ip, fp = mant, ""
+    digits = (ip + fp).lstrip("0")
+    # value = 0.ip fp ... normalise: position of the decimal point
+    lead_zeros = len(ip + fp) - len((ip + fp).lstrip("0"))
+    point = len(ip) - lead_zeros + exp10  # digits * 10^(point - len(digits))
+    digits = digits.rstrip("0") or "0"
+    n = len(digits)
+    kk = point
+    if kk - n >= 0 and kk <= 16:
+        o = digits + "0" * (kk - n) + ".0"
+    elif 0 < kk <= 16:
+        o = digits[:kk] + "." + digits[kk:]
+    elif -5 < kk <= 0:
+        o = "0." + "0" * (-kk) + digits
+    elif n == 1:
+        o = digits + "e" + str(kk - 1)
+    else:
+        o = digits[0] + "." + digits[1:] + "e" + str(kk - 1)
+    return ("-" if neg else "") + o
+
+
+def _ratio(a: int, b: int) -> float:
+    return a / b if b > 0 else 0.0
+
+
+def run_classify_bytes(input_path: str, input_raw: bytes,
+                       dbs: List[Tuple[str, int, List[Tuple[str, set]]]],
+                       user_k: Optional[int] = None, min_freq: int = 1,
+                       min_cov: float = 0.0) -> Tuple[str, str]:
+    """classify.rs:58-385 on in-memory inputs.  ``dbs`` = [(path, k,
+    [(reference name, key set), ...])] in file order.  Returns (JSON text,
+    TSV text).  References are listed in DB order (the reference iterates a
+    HashMap: its order is random, classify.rs:215)."""
+    final_k = None
+    if user_k is not None:  # classify.rs:71-78
+        if user_k == 0 or user_k > 32:
+            raise OracleError(f"Invalid K-mer size: {user_k}. Must be between 1 and 32.")
+        final_k = user_k
+    for path, dk, _refs in dbs:  # classify.rs:80-117
+        if final_k is not None:
+            if dk != final_k:
+                if user_k is not None:
+                    raise OracleError(f"User-provided k-mer size {final_k} does not match k-mer size "
+                                      f"{dk} from database: {path!r}")
+                raise OracleError(f"Effective k-mer size {final_k} (from first database) does not "
+                                  f"match k-mer size {dk} from database: {path!r}")
+        else:
+            if dk == 0 or dk > 32:
+                raise OracleError(f"Invalid K-mer size: {dk}. Must be between 1 and 32.")
+            final_k = dk
+    k = final_k
+    try:  # classify.rs:135-181: raw file (needletail sniffs compression), normalize
+        recs = parse_fastx(input_raw)
+    except OracleError as e:
+        if str(e) == "parse":
+            raise OracleError(f"Failed to parse FASTA/Q content from: {input_path!r}")
+        raise OracleError(f"Error reading record from input file: {input_path!r}")
+    counts: Dict[int, int] = {}
+    for _id, seq in recs:
+        process_sequence_chunk(normalize(seq), k, counts)
+    filt = {key: c for key, c in counts.items() if c >= min_freq}  # classify.rs:195-199
+    n_in = len(filt)
+
+    tsv = ["InputFile\tDatabase\tReference\tTotalKmersInReference\tInputKmersHittingReference\t"
+           "SumDepthMatchedKmers\tAvgDepthMatchedKmers\tProportionInputKmersHittingReference\t"
+           "ReferenceBreadthOfCoverage\n"]
+    db_blocks = []
+    for path, dk, refs in dbs:  # classify.rs:206-308
+        overall: set = set()
+        ref_blocks = []
+        for name, rset in refs:
+            matched = {kk for kk in filt if kk in rset}
+            sd = sum(filt[kk] for kk in matched)
+            overall |= matched
+            nm, tot = len(matched), len(rset)
+            breadth = _ratio(nm, tot)
+            if breadth >= min_cov:
+                avg, prop = _ratio(sd, nm), _ratio(nm, n_in)
+                ref_blocks.append(
+                    "        {\n"
+                    f"          \"reference_name\": {json.dumps(name, ensure_ascii=False)},\n"
+                    f"          \"total_kmers_in_reference\": {tot},\n"
+                    f"          \"input_kmers_hitting_reference\": {nm},\n"
+                    f"          \"sum_depth_of_matched_kmers_in_input\": {sd},\n"
+                    f"          \"avg_depth_of_matched_kmers_in_input\": {rust_f64(avg)},\n"
+                    f"          \"proportion_input_kmers_hitting_reference\": {rust_f64(prop)},\n"
+                    f"          \"reference_breadth_of_coverage\": {rust_f64(breadth)}\n"
+                    "        }")
+                tsv.append(f"{input_path}\t{path}\t{name}\t{tot}\t{nm}\t{sd}\t{avg:.4f}\t{prop:.4f}\t{breadth:.4f}\n")
+        osd = sum(filt[kk] for kk in overall)
+        union = len(set().union(*[r for _n, r in refs])) if refs else 0
+        no = len(overall)
+        refs_txt = "[\n" + ",\n".join(ref_blocks) + "\n      ]" if ref_blocks else "[]"
+        db_blocks.append(
+            "    {\n"
+            f"      \"database_path\": {json.dumps(path, ensure_ascii=False)},\n"
+            f"      \"database_kmer_size\": {dk},\n"
+            f"      \"total_unique_kmers_in_db_across_references\": {union},\n"
+            f"      \"overall_input_kmers_matched_in_db\": {no},\n"
+            f"      \"overall_sum_depth_of_matched_kmers_in_input\": {osd},\n"
+            f"      \"overall_avg_depth_of_matched_kmers_in_input\": {rust_f64(_ratio(osd, no))},\n"
+            f"      \"proportion_input_kmers_in_db_overall\": {rust_f64(_ratio(no, n_in))},\n"
+            f"      \"proportion_db_kmers_covered_overall\": {rust_f64(_ratio(no, union))},\n"
+            f"      \"references\": {refs_txt}\n"
+            "    }")
+    dbs_txt = "[\n" + ",\n".join(db_blocks) + "\n  ]" if db_blocks else "[]"
+    js = ("{\n"
+          f"  \"input_file_path\": {json.dumps(input_path, ensure_ascii=False)},\n"
+          f"  \"total_unique_kmers_in_input\": {n_in},\n"
+          f"  \"min_kmer_frequency_filter\": {min_freq},\n"
+          f"  \"databases_analyzed\": {dbs_txt}\n"
+          "}")
+    return js, "".join(tsv)

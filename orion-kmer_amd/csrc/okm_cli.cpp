@@ -1,5 +1,5 @@
 // okm_cli.cpp — `orion-kmer` command line, a drop-in for the reference's
-// count / build / compare subcommands (cli.rs:4-189, main.rs:7-16,
+// count / build / compare / query / classify subcommands (cli.rs:4-189, main.rs:7-16,
 // commands/mod.rs:10-33), driving the MI355X engine through the C ABI only.
 //
 // Same flags (clap-derived names, cli.rs:38-95), same outputs (count.rs:127-135
@@ -202,6 +202,10 @@ static void print_help(const std::string &cmd) {
         printf("Build a unique k-mer database from genome assemblies\n\nUsage: orion-kmer build [OPTIONS] --kmer-size <KMER_SIZE> --genomes <GENOME_FILES>... --output-file <OUTPUT_FILE>\n");
     else if (cmd == "compare")
         printf("Compare two k-mer databases\n\nUsage: orion-kmer compare [OPTIONS] --db1 <DB1> --db2 <DB2> --output-file <OUTPUT_FILE>\n");
+    else if (cmd == "query")
+        printf("Query short reads against a k-mer database\n\nUsage: orion-kmer query [OPTIONS] --database <DATABASE_FILE> --reads <READS_FILE> --output-file <OUTPUT_FILE>\n\nOptions:\n  -d, --database <DATABASE_FILE>  K-mer database to query against. Supports .gz, .xz, .zst compression.\n  -r, --reads <READS_FILE>        Short-read file (FASTQ). Supports .gz, .xz, .zst compression.\n  -o, --output-file <OUTPUT_FILE>  Output file for the IDs of matching reads. Supports .gz, .xz, .zst compression based on extension.\n  -c, --min-hits <MIN_HITS>       Minimum number of k-mer hits to report a read [default: 1]\n  -h, --help                      Print help\n");
+    else if (cmd == "classify")
+        printf("Classify sequences against k-mer databases and report coverage statistics\n\nUsage: orion-kmer classify [OPTIONS] --input-file <INPUT_FILE> --databases <DATABASE_FILES>... --output-file <OUTPUT_FILE>\n\nOptions:\n  -i, --input-file <INPUT_FILE>  Input genome (FASTA) or reads (FASTQ) file.\n  -d, --databases <DATABASE_FILES>...  One or more k-mer database files (.db).\n  -o, --output-file <OUTPUT_FILE>  Output file for classification results (JSON format).\n  -k, --kmer-size <KMER_SIZE>    Optional: K-mer size to validate against databases.\n      --min-kmer-frequency <MIN_KMER_FREQUENCY>  [default: 1]\n      --min-coverage <MIN_COVERAGE>  [default: 0]\n      --output-tsv <OUTPUT_TSV>  Optional: Output file path for a TSV summary.\n  -h, --help                     Print help\n");
     else
         printf("Usage: orion-kmer [OPTIONS] <COMMAND>\n\nCommands:\n  count     Count k-mers in FASTA/FASTQ files\n  build     Build a unique k-mer database from genome assemblies\n  compare   Compare two k-mer databases\n  query     Query short reads against a k-mer database\n  classify  Classify sequences against k-mer databases and report coverage statistics\n  help      Print this message or the help of the given subcommand(s)\n\nOptions:\n  -t, --threads <THREADS>  Number of threads to use (0 for all logical cores) [default: 0]\n  -v, --verbose...         Verbosity level (e.g., -v, -vv)\n      --device <DEVICE>    GPU ordinal (MI355X engine) [default: 0]\n  -h, --help               Print help\n  -V, --version            Print version\n");
 }
@@ -481,6 +485,314 @@ static int run_compare(const Args &a) {
     return 0;
 }
 
+// query.rs:24-134: reads whose canonical k-mer hits in the database's unified
+// set reach min_hits, ids written in input order.
+static int run_query(const Args &a) {
+    std::string dbp, reads, out, mh;
+    if (!get_one(a, "database", dbp)) return usage_error("the following required arguments were not provided:\n  --database <DATABASE_FILE>");
+    if (!get_one(a, "reads", reads)) return usage_error("the following required arguments were not provided:\n  --reads <READS_FILE>");
+    if (!get_one(a, "output-file", out)) return usage_error("the following required arguments were not provided:\n  --output-file <OUTPUT_FILE>");
+    uint64_t min_hits = 1;
+    if (get_one(a, "min-hits", mh) && !parse_u64(mh, min_hits))
+        return usage_error("invalid value '" + mh + "' for '--min-hits <MIN_HITS>'");
+    okm_db *db = nullptr;
+    okm_status s = okm_db_read(&db, dbp.c_str());  // query.rs:28 (utils.rs:37-55)
+    if (s == OKM_E_IO) return die("Failed to get input reader for k-mer database: " + dbg_path(dbp));
+    if (s != OKM_OK) return die("Failed to deserialize KmerDbV2 from " + dbg_path(dbp));
+    const uint8_t k = okm_db_k(db);
+    if (k == 0 || k > 32) {  // query.rs:30-32
+        okm_db_free(db);
+        return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and 32.");
+    }
+    // query.rs:36 get_all_kmers_unified -> a device set
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < okm_db_num_references(db); ++i) {
+        uint64_t n;
+        okm_db_reference(db, i, nullptr, nullptr, &n);
+        total += n;
+    }
+    okm_kset *set = nullptr;
+    s = okm_kset_create(&set, k, g_device, total);
+    if (s != OKM_OK) {
+        okm_db_free(db);
+        return die("MI355X engine unavailable: " + err_detail());
+    }
+    for (uint64_t i = 0; i < okm_db_num_references(db); ++i) {
+        const uint64_t *keys;
+        uint64_t n;
+        okm_db_reference(db, i, nullptr, &keys, &n);
+        if (n && okm_kset_insert(set, keys, n, 0, nullptr) != OKM_OK) {
+            std::string d = err_detail();
+            okm_kset_destroy(set);
+            okm_db_free(db);
+            return die("GPU engine failure while querying: " + d);
+        }
+    }
+    okm_db_free(db);
+    uint64_t nset = 0;
+    okm_kset_size(set, &nset);
+    info("orion_kmer::commands::query", "Querying reads from " + dbg_path(reads) + " against database with k=" + std::to_string(k) + " (" + std::to_string(nset) + " unique k-mers in DB)");
+    okm_reader *r = nullptr;
+    s = okm_reader_open2(&r, reads.c_str(), 1, OKM_READ_RAW | OKM_READ_IDS);  // query.rs:45-52
+    if (s == OKM_E_IO) {
+        okm_kset_destroy(set);
+        return die("Failed to get input reader for reads file: " + dbg_path(reads));
+    }
+    if (s != OKM_OK) {
+        okm_kset_destroy(set);
+        return die("Failed to parse FASTQ content from: " + dbg_path(reads));
+    }
+    {  // query.rs:55-61: the output writer is created before any record is read
+        FILE *f = fopen(out.c_str(), "wb");
+        if (!f) {
+            okm_reader_close(r);
+            okm_kset_destroy(set);
+            return die("Failed to get output writer for matching reads: " + dbg_path(out));
+        }
+        fclose(f);
+    }
+    std::string ids_out;
+    std::vector<uint32_t> hits;
+    uint64_t n_match = 0;
+    for (;;) {
+        const uint8_t *seq, *ids;
+        const uint64_t *off, *ioff;
+        uint64_t n;
+        s = okm_reader_next(r, 256ull << 20, &seq, &off, &n);
+        if (s != OKM_OK) {
+            okm_reader_close(r);
+            okm_kset_destroy(set);
+            return die("Error reading record from " + dbg_path(reads));  // query.rs:69-70
+        }
+        if (n == 0) break;
+        okm_reader_ids(r, &ids, &ioff);
+        hits.resize(n);
+        if (okm_query_hits(set, seq, off, n, hits.data()) != OKM_OK) {
+            std::string d = err_detail();
+            okm_reader_close(r);
+            okm_kset_destroy(set);
+            return die("GPU engine failure while querying: " + d);
+        }
+        for (uint64_t i = 0; i < n; ++i) {
+            if (off[i + 1] - off[i] < k) continue;  // query.rs:83-85
+            if (hits[i] < min_hits) continue;       // query.rs:97
+            ids_out.append((const char *)ids + ioff[i], ioff[i + 1] - ioff[i]);
+            ids_out += '\n';
+            ++n_match;
+        }
+    }
+    okm_reader_close(r);
+    okm_kset_destroy(set);
+    info("orion_kmer::commands::query", "Found " + std::to_string(n_match) + " reads matching criteria (min_hits: " + std::to_string(min_hits) + "). Writing to output...");
+    if (okm_write_file(out.c_str(), (const uint8_t *)ids_out.data(), ids_out.size()) != OKM_OK)
+        return die("Failed to get output writer for matching reads: " + dbg_path(out));
+    return 0;
+}
+
+// csv crate (QuoteStyle::Necessary, '\t' delimiter): quote a field holding the
+// delimiter, a quote or a line break.
+static std::string tsv_field(const std::string &f) {
+    if (f.find_first_of("\t\"\r\n") == std::string::npos) return f;
+    std::string o = "\"";
+    for (char ch : f) {
+        if (ch == '"') o += '"';
+        o += ch;
+    }
+    return o + "\"";
+}
+
+static std::string fmt4(double x) {  // Rust format!("{:.4}", x)
+    char b[64];
+    snprintf(b, sizeof(b), "%.4f", x);
+    return b;
+}
+
+static double ratio(uint64_t a, uint64_t b) { return b > 0 ? (double)a / (double)b : 0.0; }
+
+// classify.rs:58-385
+static int run_classify(const Args &a) {
+    std::string input, out, ks, mf, mc, tsv;
+    if (!get_one(a, "input-file", input)) return usage_error("the following required arguments were not provided:\n  --input-file <INPUT_FILE>");
+    auto dbs = get_all(a, "databases");
+    if (dbs.empty()) return usage_error("the following required arguments were not provided:\n  --databases <DATABASE_FILES>...");
+    if (!get_one(a, "output-file", out)) return usage_error("the following required arguments were not provided:\n  --output-file <OUTPUT_FILE>");
+    const bool have_user_k = get_one(a, "kmer-size", ks);
+    uint64_t user_k = 0, min_freq = 1;
+    if (have_user_k && (!parse_u64(ks, user_k) || user_k > 255))
+        return usage_error("invalid value '" + ks + "' for '--kmer-size <KMER_SIZE>': invalid digit found in string");
+    if (get_one(a, "min-kmer-frequency", mf) && !parse_u64(mf, min_freq))
+        return usage_error("invalid value '" + mf + "' for '--min-kmer-frequency <MIN_KMER_FREQUENCY>'");
+    double min_cov = 0.0;
+    if (get_one(a, "min-coverage", mc)) {
+        char *end = nullptr;
+        min_cov = strtod(mc.c_str(), &end);
+        if (mc.empty() || *end) return usage_error("invalid value '" + mc + "' for '--min-coverage <MIN_COVERAGE>'");
+    }
+    const bool want_tsv = get_one(a, "output-tsv", tsv);
+    // classify.rs:59-64 (unconditional eprintln)
+    fprintf(stderr, "DEBUG: Entered run_classify. Input file: %s, Num DBs: %zu, Output: %s\n", dbg_path(input).c_str(),
+            dbs.size(), dbg_path(out).c_str());
+    // --- 1. databases and k (classify.rs:67-132)
+    int final_k = -1;
+    if (have_user_k) {
+        if (user_k == 0 || user_k > 32) return die("Invalid K-mer size: " + std::to_string(user_k) + ". Must be between 1 and 32.");
+        final_k = (int)user_k;
+    }
+    std::vector<okm_db *> loaded;
+    auto free_dbs = [&]() {
+        for (auto *d : loaded) okm_db_free(d);
+        loaded.clear();
+    };
+    for (auto &p : dbs) {
+        okm_db *d = nullptr;
+        if (okm_db_read(&d, p.c_str()) != OKM_OK) {
+            free_dbs();
+            return die("Failed to load database: " + dbg_path(p));
+        }
+        const int dk = okm_db_k(d);
+        if (final_k >= 0) {
+            if (dk != final_k) {
+                okm_db_free(d);
+                free_dbs();
+                if (have_user_k)
+                    return die("User-provided k-mer size " + std::to_string(final_k) + " does not match k-mer size " + std::to_string(dk) + " from database: " + dbg_path(p));
+                return die("Effective k-mer size " + std::to_string(final_k) + " (from first database) does not match k-mer size " + std::to_string(dk) + " from database: " + dbg_path(p));
+            }
+        } else {
+            if (dk == 0 || dk > 32) {
+                okm_db_free(d);
+                free_dbs();
+                return die("Invalid K-mer size: " + std::to_string(dk) + ". Must be between 1 and 32.");
+            }
+            final_k = dk;
+        }
+        loaded.push_back(d);
+    }
+    const uint8_t k = (uint8_t)final_k;
+    // --- 2. input k-mer counts (classify.rs:135-199), on the device
+    okm_ctx *ctx = nullptr;
+    int rc;
+    if ((rc = open_engine(&ctx, k, OKM_MODE_COUNT))) {
+        free_dbs();
+        return rc;
+    }
+    {
+        okm_reader *r = nullptr;
+        okm_status s = okm_reader_open(&r, input.c_str(), 0);  // utils.rs:157-161: no extension decompression
+        if (s == OKM_E_IO) {
+            okm_destroy(ctx);
+            free_dbs();
+            return die("Failed to get buffered file reader for file: " + dbg_path(input));
+        }
+        if (s != OKM_OK) {
+            okm_destroy(ctx);
+            free_dbs();
+            return die("Failed to parse FASTA/Q content from: " + dbg_path(input));
+        }
+        for (;;) {
+            const uint8_t *seq;
+            const uint64_t *off;
+            uint64_t n;
+            s = okm_reader_next(r, 256ull << 20, &seq, &off, &n);
+            if (s != OKM_OK) {
+                okm_reader_close(r);
+                okm_destroy(ctx);
+                free_dbs();
+                return die("Error reading record from input file: " + dbg_path(input));
+            }
+            if (n == 0) break;
+            if (okm_add_batch(ctx, seq, off, n, 1) != OKM_OK) {
+                std::string d = err_detail();
+                okm_reader_close(r);
+                okm_destroy(ctx);
+                free_dbs();
+                return die("GPU engine failure on " + input + ": " + d);
+            }
+        }
+        okm_reader_close(r);
+    }
+    okm_classifier *cls = nullptr;
+    uint64_t n_input = 0;
+    if (okm_classifier_create(&cls, ctx, min_freq, &n_input) != OKM_OK) {
+        std::string d = err_detail();
+        okm_destroy(ctx);
+        free_dbs();
+        return die("GPU engine failure while classifying: " + d);
+    }
+    okm_destroy(ctx);
+    info("orion_kmer::commands::classify", "After applying min_kmer_frequency filter (>= " + std::to_string(min_freq) + "), " + std::to_string(n_input) + " unique k-mers remain in input.");
+    // --- 3. per database (classify.rs:206-308)
+    std::string js = "{\n";
+    js += "  \"input_file_path\": " + json_str(input) + ",\n";
+    js += "  \"total_unique_kmers_in_input\": " + std::to_string(n_input) + ",\n";
+    js += "  \"min_kmer_frequency_filter\": " + std::to_string(min_freq) + ",\n";
+    js += "  \"databases_analyzed\": [";
+    std::string tsv_out = "InputFile\tDatabase\tReference\tTotalKmersInReference\tInputKmersHittingReference\tSumDepthMatchedKmers\tAvgDepthMatchedKmers\tProportionInputKmersHittingReference\tReferenceBreadthOfCoverage\n";
+    for (size_t di = 0; di < loaded.size(); ++di) {
+        okm_db *d = loaded[di];
+        const uint64_t nref = okm_db_num_references(d);
+        std::vector<uint64_t> off(1, 0), keys;
+        std::vector<std::string> names;
+        for (uint64_t i = 0; i < nref; ++i) {
+            const char *nm;
+            const uint64_t *kk;
+            uint64_t n;
+            okm_db_reference(d, i, &nm, &kk, &n);
+            names.emplace_back(nm);
+            keys.insert(keys.end(), kk, kk + n);
+            off.push_back(keys.size());
+        }
+        std::vector<uint64_t> rm(nref), rs(nref);
+        uint64_t du = 0, dm = 0, ds = 0;
+        if (okm_classifier_probe_db(cls, keys.data(), off.data(), nref, rm.data(), rs.data(), &du, &dm, &ds) != OKM_OK) {
+            std::string e = err_detail();
+            okm_classifier_destroy(cls);
+            free_dbs();
+            return die("GPU engine failure while classifying: " + e);
+        }
+        std::string refs;
+        size_t nref_out = 0;
+        for (uint64_t i = 0; i < nref; ++i) {
+            const uint64_t tot = off[i + 1] - off[i];
+            const double breadth = ratio(rm[i], tot);
+            if (!(breadth >= min_cov)) continue;  // classify.rs:240
+            const double avg = ratio(rs[i], rm[i]), prop = ratio(rm[i], n_input);
+            refs += std::string(nref_out ? ",\n" : "\n") + "        {\n";
+            refs += "          \"reference_name\": " + json_str(names[i]) + ",\n";
+            refs += "          \"total_kmers_in_reference\": " + std::to_string(tot) + ",\n";
+            refs += "          \"input_kmers_hitting_reference\": " + std::to_string(rm[i]) + ",\n";
+            refs += "          \"sum_depth_of_matched_kmers_in_input\": " + std::to_string(rs[i]) + ",\n";
+            refs += "          \"avg_depth_of_matched_kmers_in_input\": " + fmt_f64(avg) + ",\n";
+            refs += "          \"proportion_input_kmers_hitting_reference\": " + fmt_f64(prop) + ",\n";
+            refs += "          \"reference_breadth_of_coverage\": " + fmt_f64(breadth) + "\n";
+            refs += "        }";
+            ++nref_out;
+            tsv_out += tsv_field(input) + "\t" + tsv_field(dbs[di]) + "\t" + tsv_field(names[i]) + "\t" +
+                       std::to_string(tot) + "\t" + std::to_string(rm[i]) + "\t" + std::to_string(rs[i]) + "\t" +
+                       fmt4(avg) + "\t" + fmt4(prop) + "\t" + fmt4(breadth) + "\n";
+        }
+        js += std::string(di ? ",\n" : "\n") + "    {\n";
+        js += "      \"database_path\": " + json_str(dbs[di]) + ",\n";
+        js += "      \"database_kmer_size\": " + std::to_string((int)okm_db_k(d)) + ",\n";
+        js += "      \"total_unique_kmers_in_db_across_references\": " + std::to_string(du) + ",\n";
+        js += "      \"overall_input_kmers_matched_in_db\": " + std::to_string(dm) + ",\n";
+        js += "      \"overall_sum_depth_of_matched_kmers_in_input\": " + std::to_string(ds) + ",\n";
+        js += "      \"overall_avg_depth_of_matched_kmers_in_input\": " + fmt_f64(ratio(ds, dm)) + ",\n";
+        js += "      \"proportion_input_kmers_in_db_overall\": " + fmt_f64(ratio(dm, n_input)) + ",\n";
+        js += "      \"proportion_db_kmers_covered_overall\": " + fmt_f64(ratio(dm, du)) + ",\n";
+        js += "      \"references\": [" + refs + (nref_out ? "\n      ]" : "]") + "\n    }";
+    }
+    js += loaded.empty() ? "]\n}" : "\n  ]\n}";
+    okm_classifier_destroy(cls);
+    free_dbs();
+    // --- 4./5. outputs (classify.rs:320-381)
+    if (okm_write_file(out.c_str(), (const uint8_t *)js.data(), js.size()) != OKM_OK)
+        return die("Failed to get output writer for JSON file: " + dbg_path(out));
+    if (want_tsv && okm_write_file(tsv.c_str(), (const uint8_t *)tsv_out.data(), tsv_out.size()) != OKM_OK)
+        return die("Failed to get output writer for TSV file: " + dbg_path(tsv));
+    return 0;
+}
+
 int main(int argc, char **argv) {
     static const std::vector<OptSpec> global = {
         {"threads", 't', true, false}, {"verbose", 'v', false, false}, {"device", 0, true, false}};
@@ -525,8 +837,19 @@ int main(int argc, char **argv) {
     } else if (cmd == "help") {
         print_help(ci + 1 < argc ? argv[ci + 1] : "");
         return 0;
-    } else if (cmd == "query" || cmd == "classify") {
-        return die("the '" + cmd + "' subcommand is outside this engine's scope (see DESIGN.md)");
+    } else if (cmd == "query") {
+        spec.push_back({"database", 'd', true, false});
+        spec.push_back({"reads", 'r', true, false});
+        spec.push_back({"output-file", 'o', true, false});
+        spec.push_back({"min-hits", 'c', true, false});
+    } else if (cmd == "classify") {
+        spec.push_back({"input-file", 'i', true, false});
+        spec.push_back({"databases", 'd', true, true});
+        spec.push_back({"output-file", 'o', true, false});
+        spec.push_back({"kmer-size", 'k', true, false});
+        spec.push_back({"min-kmer-frequency", 0, true, false});
+        spec.push_back({"min-coverage", 0, true, false});
+        spec.push_back({"output-tsv", 0, true, false});
     } else {
         return usage_error("unrecognized subcommand '" + cmd + "'");
     }
@@ -551,5 +874,7 @@ int main(int argc, char **argv) {
     if (get_one(pre, "device", dev) || get_one(a, "device", dev)) g_device = atoi(dev.c_str());
     if (cmd == "count") return run_count(a);
     if (cmd == "build") return run_build(a);
+    if (cmd == "query") return run_query(a);
+    if (cmd == "classify") return run_classify(a);
     return run_compare(a);
 }

@@ -299,6 +299,9 @@ struct okm_ctx {
 
 namespace okm {
 
+int ctx_device(const okm_ctx *c) { return c->device; }
+bool ctx_is_wide(const okm_ctx *c) { return c->wide; }
+
 static okm_status ensure_hc(okm_ctx *c, size_t n_u32) {
     if (n_u32 <= c->HC_cap) return OKM_OK;
     if (c->HC) (void)hipFree(c->HC);

@@ -23,19 +23,9 @@
 // their within-bin ranks, returned by the histogram atomic) in registers and
 // computes each k-mer ONCE; the generic kernel computes them twice.  Emits are
 // branch-free: an invalid window counts into a dummy bin.
-#include "okm_dev_common.h"
+#include "okm_scan.h"
 
 namespace okm {
-
-// Valid bytes after needletail normalize(false) + dna_base_to_u64:
-// A/a C/c G/g T/t U/u (kmer.rs:14-17; U->T is normalize's).  c & 0xDF folds
-// case and has exactly {X, X|0x20} as preimages of an upper-case letter X.
-__device__ __forceinline__ bool base_valid(uint32_t c) {
-    const uint32_t u = c & 0xDFu;
-    return (u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'U');
-}
-// A=0 C=1 G=2 T=3 (and U=3) for either case: ((c>>1) ^ (c>>2)) & 3.
-__device__ __forceinline__ uint32_t base_code(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
 
 __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
     return shift >= 64 ? 0u : (uint32_t)(key >> shift);
@@ -71,42 +61,6 @@ uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
 // is a compile-time constant after unrolling; K = 0: runtime k, runtime j).
 // Bytes at or beyond n read as 0 (invalid), so windows never run off the end;
 // record separators are invalid bytes, so windows never cross records.
-template <int SEG> struct WinWords {
-    static constexpr int kLoad = SEG + 32;  // bytes: covers SEG + k - 1 for k <= 32 (16-B multiple)
-    uint32_t w[kLoad / 4];
-};
-
-// The bytes of windows [w0, w0 + SEG) (bytes at or beyond n read as 0).
-template <int SEG>
-__device__ __forceinline__ void load_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
-                                             WinWords<SEG> &ww) {
-    constexpr int LOAD = WinWords<SEG>::kLoad;
-    uint32_t *w = ww.w;
-    if (w0 + LOAD <= n) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
-#pragma unroll
-        for (int q = 0; q < LOAD / 16; ++q) {
-            const uint4 v = p[q];
-            w[4 * q + 0] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < LOAD / 4; ++q) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint64_t idx = w0 + 4 * q + b;
-                const uint32_t c = idx < n ? (uint32_t)seq[idx] : 0u;
-                x |= c << (8 * b);
-            }
-            w[q] = x;
-        }
-    }
-}
-
 template <int SEG, int K, typename Emit>
 __device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_rt, Emit &&emit) {
     constexpr int LOAD = WinWords<SEG>::kLoad;

@@ -59,7 +59,28 @@ struct Parser {
     std::vector<uint8_t> data;
     size_t pos = 0;
     bool fastq = false;
+    bool raw = false;   // query.rs:66: record.sequence() as is (no normalize)
+    bool want_ids = false;
     uint64_t records = 0;
+    std::vector<uint8_t> ids;     // ids of the records read by the current batch
+    std::vector<uint64_t> id_off;
+
+    void add_id(size_t b, size_t e) {  // needletail id(): header after the marker, CR trimmed
+        e = rstrip_cr(data, b, e);
+        ids.insert(ids.end(), data.begin() + b, data.begin() + e);
+        id_off.push_back(ids.size());
+    }
+
+    // raw_seq: the sequence bytes with their line breaks (multi-line FASTA
+    // keeps its interior '\n'; the record's final line terminator and one
+    // trailing CR dropped).
+    void append_seq(size_t b, size_t e, std::vector<uint8_t> &seq) {
+        if (!raw) {
+            normalize_append(data.data() + b, e - b, seq);
+            return;
+        }
+        seq.insert(seq.end(), data.begin() + b, data.begin() + e);
+    }
 
     okm_status init() {
         okm_status s = sniff_decompress(data);
@@ -95,6 +116,7 @@ struct Parser {
             if (data[pos] != '>') return fail(OKM_E_RECORD, "expected '>' at the start of a FASTA record");
             size_t b, e;
             line(b, e);  // header
+            if (want_ids) add_id(b + 1, e);
             const size_t s0 = pos;
             // the sequence runs to the next "\n>" (a line starting with '>')
             size_t end = data.size();
@@ -108,7 +130,14 @@ struct Parser {
                 if (!nl) break;
                 p = (size_t)(nl - data.data()) + 1;
             }
-            normalize_append(data.data() + s0, end - s0, seq);
+            if (raw) {
+                size_t se = end;
+                if (se > s0 && data[se - 1] == '\n') --se;  // the record's last line terminator
+                if (se > s0 && data[se - 1] == '\r') --se;
+                append_seq(s0, se, seq);
+            } else {
+                append_seq(s0, end, seq);
+            }
             pos = end;
             ++records;
             *got = true;
@@ -129,7 +158,8 @@ struct Parser {
         se = rstrip_cr(data, sb, se);
         qe = rstrip_cr(data, qb, qe);
         if (se - sb != qe - qb) return fail(OKM_E_RECORD, "sequence and quality lengths differ");
-        normalize_append(data.data() + sb, se - sb, seq);
+        if (want_ids) add_id(hb + 1, he);
+        append_seq(sb, se, seq);
         ++records;
         *got = true;
         return OKM_OK;
@@ -149,6 +179,10 @@ struct okm_reader {
 extern "C" {
 
 okm_status okm_reader_open(okm_reader **out, const char *path, int decompress_by_ext) {
+    return okm_reader_open2(out, path, decompress_by_ext, 0);
+}
+
+okm_status okm_reader_open2(okm_reader **out, const char *path, int decompress_by_ext, int flags) {
     if (!out || !path) return fail(OKM_E_ARG, "null argument");
     *out = nullptr;
     okm_reader *r = new okm_reader();
@@ -166,6 +200,8 @@ okm_status okm_reader_open(okm_reader **out, const char *path, int decompress_by
         delete r;
         return s;
     }
+    r->p.raw = (flags & OKM_READ_RAW) != 0;
+    r->p.want_ids = (flags & OKM_READ_IDS) != 0;
     *out = r;
     return OKM_OK;
 }
@@ -175,6 +211,8 @@ okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **se
     if (!r || !seq || !offsets || !n_records) return fail(OKM_E_ARG, "null argument");
     r->seq.clear();
     r->off.assign(1, 0);
+    r->p.ids.clear();
+    r->p.id_off.assign(1, 0);
     for (;;) {
         bool got = false;
         okm_status s = r->p.next(r->seq, &got);
@@ -186,6 +224,14 @@ okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **se
     *seq = r->seq.data();
     *offsets = r->off.data();
     *n_records = r->off.size() - 1;
+    return OKM_OK;
+}
+
+okm_status okm_reader_ids(const okm_reader *r, const uint8_t **ids, const uint64_t **id_offsets) {
+    if (!r || !ids || !id_offsets) return fail(OKM_E_ARG, "null argument");
+    if (!r->p.want_ids) return fail(OKM_E_STATE, "reader opened without OKM_READ_IDS");
+    *ids = r->p.ids.data();
+    *id_offsets = r->p.id_off.data();
     return OKM_OK;
 }
 

@@ -15,7 +15,11 @@ namespace okm {
 void set_error(const std::string &msg);
 okm_status fail(okm_status s, const std::string &msg);
 
-constexpr uint64_t kEmptyKey = ~0ull;  // never a canonical key
+constexpr uint64_t kEmptyKey = ~0ull;
+
+// Context accessors for the other translation units (okm_probe.hip).
+int ctx_device(const okm_ctx *c);
+bool ctx_is_wide(const okm_ctx *c);  // never a canonical key
 
 // ----------------------------------------------------------------------------
 // Device-side launchers (okm_device.hip).  All take a hipStream_t as void*.

@@ -1,8 +1,9 @@
 """okm — Python host layer over the MI355X k-mer engine (liborion_kmer.so).
 
 Mirrors the reference's library surface (``orion_kmer::kmer`` pub fns,
-``kmer.rs:37-106``) and its ``count``/``build``/``compare`` drivers
-(``commands/count.rs:40-141``, ``build.rs:80-160``, ``compare.rs:29-97``) so
+``kmer.rs:37-106``) and its ``count``/``build``/``compare``/``query``/``classify``
+drivers (``commands/count.rs:40-141``, ``build.rs:80-160``, ``compare.rs:29-97``,
+``query.rs:24-134``, ``classify.rs:58-385``) so
 tests read like the reference's own.  All compute goes through the C ABI; the
 engine itself is HIP on gfx950 and has no CPU fallback.
 """
@@ -25,6 +26,7 @@ __all__ = [
     "KmerCounter", "DeviceBuffer", "device_count", "device_arch", "pack_records",
     "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads",
     "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
+    "KmerSet", "Classifier", "run_query", "run_classify", "read_fastx_records",
 ]
 
 
@@ -463,3 +465,169 @@ def run_compare(db1: KmerDb, db2: KmerDb, device: int = 0) -> Dict[str, object]:
     return {"kmer_size": db1.k, "db1_total_unique_kmers_across_references": len(a),
             "db2_total_unique_kmers_across_references": len(b), "intersection_size": inter,
             "union_size": union, "jaccard_index": 0.0 if union == 0 else inter / union}
+
+
+# ---------------------------------------------------------------------------
+# query / classify (query.rs, classify.rs) — device sets and probes
+# ---------------------------------------------------------------------------
+
+def read_fastx_records(path: str, decompress_by_extension: bool = True, raw: bool = False
+                       ) -> List[Tuple[bytes, bytes]]:
+    """(id, sequence) of every record; raw=True keeps record.sequence() as in
+    the file (query.rs:66), otherwise normalize(false) is applied."""
+    r = c_void_p()
+    flags = _lib.OKM_READ_IDS | (_lib.OKM_READ_RAW if raw else 0)
+    check(lib().okm_reader_open2(byref(r), path.encode(), 1 if decompress_by_extension else 0, flags),
+          "okm_reader_open2")
+    out: List[Tuple[bytes, bytes]] = []
+    try:
+        while True:
+            seq, offs, n = c_void_p(), c_void_p(), c_uint64()
+            check(lib().okm_reader_next(r, 256 << 20, byref(seq), byref(offs), byref(n)), "okm_reader_next")
+            if n.value == 0:
+                break
+            ids, ioff = c_void_p(), c_void_p()
+            check(lib().okm_reader_ids(r, byref(ids), byref(ioff)), "okm_reader_ids")
+            o = np.ctypeslib.as_array(ctypes.cast(offs, POINTER(c_uint64)), shape=(n.value + 1,))
+            io = np.ctypeslib.as_array(ctypes.cast(ioff, POINTER(c_uint64)), shape=(n.value + 1,))
+            sb = ctypes.string_at(seq, int(o[-1])) if o[-1] else b""
+            ib = ctypes.string_at(ids, int(io[-1])) if io[-1] else b""
+            for i in range(n.value):
+                out.append((ib[io[i]:io[i + 1]], sb[o[i]:o[i + 1]]))
+    finally:
+        lib().okm_reader_close(r)
+    return out
+
+
+class KmerSet:
+    """Device hash set of canonical k-mers: the unified ``HashSet<u64>`` of a
+    database (db_types.rs:43-48) and its ``contains`` probes (query.rs:88)."""
+
+    def __init__(self, k: int, device: int = 0, capacity_hint: int = 0):
+        self.k = k
+        self.h = c_void_p()
+        check(lib().okm_kset_create(byref(self.h), k, device, capacity_hint), "okm_kset_create")
+
+    def close(self) -> None:
+        if self.h:
+            lib().okm_kset_destroy(self.h)
+            self.h = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def insert(self, keys: np.ndarray) -> int:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        n_new = c_uint64()
+        check(lib().okm_kset_insert(self.h, keys.ctypes.data, len(keys), 0, byref(n_new)), "okm_kset_insert")
+        return n_new.value
+
+    def insert_device(self, d_keys: int, n: int) -> int:
+        n_new = c_uint64()
+        check(lib().okm_kset_insert(self.h, c_void_p(d_keys), n, 1, byref(n_new)), "okm_kset_insert")
+        return n_new.value
+
+    def __len__(self) -> int:
+        n = c_uint64()
+        check(lib().okm_kset_size(self.h, byref(n)), "okm_kset_size")
+        return n.value
+
+    def contains(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), dtype=np.uint8)
+        check(lib().okm_kset_contains(self.h, keys.ctypes.data, len(keys), out.ctypes.data), "okm_kset_contains")
+        return out.astype(bool)
+
+    def query_hits(self, seqs: Sequence[bytes]) -> np.ndarray:
+        """query.rs:86-93 per record over RAW bytes."""
+        data, offs = pack_records(list(seqs))
+        hits = np.zeros(len(seqs), dtype=np.uint32)
+        if len(seqs):
+            check(lib().okm_query_hits(self.h, data.ctypes.data, offs.ctypes.data, len(seqs), hits.ctypes.data),
+                  "okm_query_hits")
+        return hits
+
+    def query_hits_device(self, d_seq: int, nbytes: int, n_records: int, d_hits: int) -> None:
+        check(lib().okm_query_hits_device(self.h, c_void_p(d_seq), nbytes, n_records, c_void_p(d_hits)),
+              "okm_query_hits_device")
+
+
+class Classifier:
+    """classify.rs:176-308: the filtered input counts as a device map, probed
+    by every reference key of a database."""
+
+    def __init__(self, counter: KmerCounter, min_kmer_frequency: int = 1):
+        self.h = c_void_p()
+        n = c_uint64()
+        check(lib().okm_classifier_create(byref(self.h), counter.ctx, min_kmer_frequency, byref(n)),
+              "okm_classifier_create")
+        self.n_input = n.value
+
+    def close(self) -> None:
+        if self.h:
+            lib().okm_classifier_destroy(self.h)
+            self.h = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def probe_db(self, refs: Sequence[np.ndarray]) -> Dict[str, object]:
+        offs = np.zeros(len(refs) + 1, dtype=np.uint64)
+        if refs:
+            offs[1:] = np.cumsum([len(r) for r in refs])
+        keys = np.concatenate([np.asarray(r, dtype=np.uint64) for r in refs]) if refs else np.zeros(0, np.uint64)
+        keys = np.ascontiguousarray(keys)
+        rm = np.zeros(len(refs), dtype=np.uint64)
+        rs = np.zeros(len(refs), dtype=np.uint64)
+        du, dm, ds = c_uint64(), c_uint64(), c_uint64()
+        check(lib().okm_classifier_probe_db(self.h, keys.ctypes.data, offs.ctypes.data, len(refs), rm.ctypes.data,
+                                            rs.ctypes.data, byref(du), byref(dm), byref(ds)),
+              "okm_classifier_probe_db")
+        return {"ref_matched": rm, "ref_sum_depth": rs, "union": du.value, "matched": dm.value,
+                "sum_depth": ds.value}
+
+
+def run_query(db: KmerDb, reads_file: str, min_hits: int = 1, device: int = 0) -> List[bytes]:
+    """query.rs:24-134: ids of reads (input order) with >= min_hits windows in
+    the DB's unified set; reads shorter than k never match."""
+    k = db.k
+    if k == 0 or k > 32:
+        raise OkmError(OKM_E_INVALID_K, f"Invalid K-mer size: {k}. Must be between 1 and 32.")
+    recs = read_fastx_records(reads_file, True, raw=True)
+    total = sum(len(v) for v in db.references.values())
+    with KmerSet(k, device, total) as s:
+        for v in db.references.values():
+            if len(v):
+                s.insert(v)
+        hits = s.query_hits([q for _i, q in recs])
+    return [rid for (rid, q), h in zip(recs, hits) if len(q) >= k and h >= min_hits]
+
+
+def run_classify(input_file: str, dbs: Sequence[KmerDb], min_kmer_frequency: int = 1,
+                 device: int = 0) -> Dict[str, object]:
+    """classify.rs:135-308 statistics (numbers only; the CLI writes the JSON)."""
+    k = dbs[0].k
+    with KmerCounter(k, "count", device) as c:
+        c.add_records([q for _i, q in read_fastx_records(input_file, False)], normalized=True)
+        with Classifier(c, min_kmer_frequency) as cl:
+            per_db = [dict(cl.probe_db(list(db.references.values())), names=list(db.references))
+                      for db in dbs]
+            return {"total_unique_kmers_in_input": cl.n_input, "databases": per_db}

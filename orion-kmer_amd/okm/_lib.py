@@ -36,6 +36,8 @@ OKM_MODE_COUNT = 0
 OKM_MODE_SET = 1
 OKM_MODE_WIDE = 0x100  # flag: k in 33..64 (two-u64 keys)
 RECORD_SEPARATOR = ord("\n")
+OKM_READ_RAW = 1
+OKM_READ_IDS = 2
 
 
 class OkmError(RuntimeError):
@@ -118,6 +120,19 @@ PROTOTYPES = {
     "okm_db_num_references": (c_uint64, [c_void_p]),
     "okm_db_reference": (c_int, [c_void_p, c_uint64, POINTER(c_char_p), POINTER(c_void_p), _P64]),
     "okm_db_free": (None, [c_void_p]),
+    "okm_reader_open2": (c_int, [POINTER(c_void_p), c_char_p, c_int, c_int]),
+    "okm_reader_ids": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "okm_kset_create": (c_int, [POINTER(c_void_p), c_uint8, c_int, c_uint64]),
+    "okm_kset_destroy": (None, [c_void_p]),
+    "okm_kset_insert": (c_int, [c_void_p, c_void_p, c_uint64, c_int, _P64]),
+    "okm_kset_size": (c_int, [c_void_p, _P64]),
+    "okm_kset_contains": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "okm_query_hits": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "okm_query_hits_device": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p]),
+    "okm_classifier_create": (c_int, [POINTER(c_void_p), c_void_p, c_uint64, _P64]),
+    "okm_classifier_destroy": (None, [c_void_p]),
+    "okm_classifier_probe_db": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, _P64, _P64,
+                                        _P64]),
     "okm_synth_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                 c_double, c_void_p, c_int]),
 }

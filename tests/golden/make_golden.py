@@ -129,17 +129,106 @@ def compare_cases():
     return out
 
 
+QUERY_READS = ("@read1_match_many\nACGTACGTTT\n+\n!!!!!!!!!!\n@read2_match_one\nTTGCXXXXXX\n+\n!!!!!!!!!!\n"
+               "@read3_no_match\nCCCCCCCCCC\n+\n!!!!!!!!!!\n@read4_match_kmer_short_read\nACG\n+\n!!!\n"
+               "@read5_match_multiple_hits_but_one_kmer\nACGTACGTACGT\n+\n!!!!!!!!!!!!\n")
+QUERY_DB = ">ref_genome_segment\nACGTACGTTTGCATC"
+
+
+def query_cases():
+    """query.rs:24-134.  Output = the matching ids file (placeholder-free)."""
+    rng = random.Random(99)
+    genome = rand_seq(rng, 3000)
+    reads_fq = "".join(f"@q{i} extra words\n{s}\n+\n{'I' * len(s)}\n" for i, s in (
+        (i, genome[o:o + 150] if i % 3 else rand_seq(rng, 150))
+        for i, o in ((i, rng.randint(0, 2850)) for i in range(50))))
+    cases = [
+        ("ref_query_basic_k4", 4, [text_file("db.fa", QUERY_DB)], text_file("query_reads.fastq", QUERY_READS), 1),
+        ("ref_query_min2_k4", 4, [text_file("db.fa", QUERY_DB)], text_file("query_reads.fastq", QUERY_READS), 2),
+        ("ref_query_min8_k4", 4, [text_file("db.fa", QUERY_DB)], text_file("query_reads.fastq", QUERY_READS), 8),
+        ("ref_query_min10_k4", 4, [text_file("db.fa", QUERY_DB)], text_file("query_reads.fastq", QUERY_READS), 10),
+        ("query_min0_keeps_zero_hit_reads", 4, [text_file("db.fa", QUERY_DB)],
+         text_file("query_reads.fastq", QUERY_READS), 0),
+        # restatement-defined: no normalize on this path (query.rs:66)
+        ("query_raw_lower_U_multiline", 4, [text_file("db.fa", QUERY_DB)],
+         text_file("r.fa", ">l lower\nacgtacgttt\n>u has U\nACGUACGTTT\n>m multi\nACG\nTACGTTT\n"
+                           ">crlf\r\nACGTAC\r\nGTTTGC\r\n>empty\n>n\nACGTNACGT\n"), 1),
+        ("query_fixture_gz_k6", 6, [data_file("test_input2.fastq.xz")], data_file("test_input2.fastq.gz"), 1),
+        ("query_fixture_fasta_zst_k5", 5, [data_file("test_input1.fasta.gz")], data_file("test_input1.fasta.zst"), 2),
+        ("query_random_k31", 31, [text_file("g1.fa", ">g1\n" + genome[:1500]), text_file("g2.fa", ">g2\n" + genome[1400:])],
+         text_file("reads.fastq", reads_fq), 1),
+        ("query_random_k31_min60", 31, [text_file("g.fa", ">g\n" + genome)], text_file("reads.fastq", reads_fq), 60),
+        ("query_random_k21_min0", 21, [text_file("g.fa", ">g\n" + genome[:500])], text_file("reads.fastq", reads_fq), 0),
+    ]
+    out = []
+    for name, k, dbf, reads, mh in cases:
+        refs = R.build_sets([(f["name"], load_bytes(f)) for f in dbf], k)
+        res = R.run_query_bytes(k, refs, reads["name"], load_bytes(reads), mh)
+        out.append({"name": name, "k": k, "db_files": dbf, "reads": reads, "min_hits": mh,
+                    "expected_output": res.decode()})
+    return out
+
+
+CL_INPUT = ">input_seq1\nACGTACGT\n>input_seq2\nACGTACGT\n>input_seq3\nTTTTGGGG"
+CL_A = ">db1_refA\nACGTACGTACGT"
+CL_B = ">db1_refB\nGGGAAAAATTTT"
+CL_C = ">db2_refC\nACGTTACGTT"
+
+
+def classify_cases():
+    """classify.rs:58-385.  JSON/TSV carry the placeholder paths INPUT and
+    DB<i>; tests substitute the real paths."""
+    rng = random.Random(7)
+    genome = rand_seq(rng, 4000)
+    reads = "".join(f"@r{i}\n{genome[o:o + 100]}\n+\n{'I' * 100}\n"
+                    for i, o in ((i, rng.randint(0, 3900)) for i in range(200)))
+    cases = [
+        ("ref_classify_basic_k4", text_file("input.fa", CL_INPUT),
+         [[text_file("db1_refA.fa", CL_A), text_file("db1_refB.fa", CL_B)], [text_file("db2_refC.fa", CL_C)]], 4, 1, 0.0),
+        ("ref_classify_minfreq2_k4", text_file("input.fa", ">S1\nACGTACGT\n>S2\nACGTGGGG"),
+         [[text_file("db_ref.fa", CL_A)]], 4, 2, 0.0),
+        ("ref_classify_mincov05_k4", text_file("input.fa", CL_INPUT),
+         [[text_file("db_refA.fa", CL_A), text_file("db_refB.fa", CL_B)]], 4, 1, 0.5),
+        ("ref_classify_mincov01_k4", text_file("input.fa", CL_INPUT),
+         [[text_file("db_refA.fa", CL_A), text_file("db_refB.fa", CL_B)]], None, 1, 0.1),
+        ("classify_empty_reference_k4", text_file("input.fa", CL_INPUT),
+         [[text_file("empty.fa", ">nothing\n"), text_file("db1_refA.fa", CL_A)]], None, 1, 0.0),
+        ("classify_no_match_k5", text_file("input.fq", "@r\nAAAAAAAAAA\n+\nIIIIIIIIII\n"),
+         [[text_file("c.fa", ">c\nCGCGCGCGTA")]], 5, 1, 0.0),
+        ("classify_fixture_gz_input_k5", data_file("test_input1.fasta.gz"),
+         [[data_file("test_input2.fastq.gz")]], 5, 1, 0.0),
+        ("classify_random_reads_k21", text_file("reads.fq", reads),
+         [[text_file("g1.fa", ">g1\n" + genome[:2000]), text_file("g2.fa", ">g2\n" + genome[1800:]),
+           text_file("other.fa", ">o\n" + rand_seq(rng, 1000))],
+          [text_file("g.fa", ">g\n" + genome)]], 21, 2, 0.3),
+    ]
+    out = []
+    for name, inp, dbs, uk, mf, mc in cases:
+        k = uk or 4 if name != "classify_random_reads_k21" else 21
+        dbl = []
+        for i, files in enumerate(dbs):
+            refs = R.build_sets([(f["name"], load_bytes(f)) for f in files], k)
+            dbl.append((f"DB{i}", k, [(f["name"], refs[f["name"]]) for f in files]))
+        js, tsv = R.run_classify_bytes("INPUT", load_bytes(inp), dbl, uk, mf, mc)
+        out.append({"name": name, "input": inp, "k": k, "dbs": dbs, "user_k": uk, "min_freq": mf, "min_cov": mc,
+                    "expected_json": js, "expected_tsv": tsv})
+    return out
+
+
 def main():
     doc = {
         "generator": "tests/golden/make_golden.py (oracle/restate.py)",
         "count": count_cases(),
         "build": build_cases(),
         "compare": compare_cases(),
+        "query": query_cases(),
+        "classify": classify_cases(),
     }
     with open(os.path.join(HERE, "cases.json"), "w") as fh:
         json.dump(doc, fh, indent=1, sort_keys=False)
         fh.write("\n")
-    print(f"wrote {len(doc['count'])} count, {len(doc['build'])} build, {len(doc['compare'])} compare cases")
+    print(f"wrote {len(doc['count'])} count, {len(doc['build'])} build, {len(doc['compare'])} compare, "
+          f"{len(doc['query'])} query, {len(doc['classify'])} classify cases")
 
 
 if __name__ == "__main__":

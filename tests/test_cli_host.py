@@ -1,7 +1,10 @@
 """The orion-kmer CLI's host-side contract (cli.rs / main.rs): flags, usage
 errors (exit 2), the reference's error strings (exit 1), no GPU needed."""
 
+import os
 import subprocess
+
+import numpy as np
 
 import pytest
 
@@ -46,9 +49,41 @@ def test_usage_errors_exit_2(tmp_path):
     assert run().returncode == 2
 
 
-def test_out_of_scope_subcommands_are_explicit():
-    r = run("query", "-d", "x", "-r", "y", "-o", "z")
-    assert r.returncode == 1 and "outside this engine's scope" in r.stderr
+def test_query_host_side_errors(tmp_path):
+    # utils.rs:40-41 / :46-47 contexts (query.rs:28 loads the DB first)
+    r = run("query", "-d", str(tmp_path / "missing.db"), "-r", "y", "-o", str(tmp_path / "o.txt"))
+    assert r.returncode == 1 and "Failed to get input reader for k-mer database" in r.stderr
+    bad = tmp_path / "bad.db"
+    bad.write_bytes(b"\x04\x01")
+    r = run("query", "-d", str(bad), "-r", "y", "-o", str(tmp_path / "o.txt"))
+    assert r.returncode == 1 and "Failed to deserialize KmerDbV2 from" in r.stderr
+    import okm
+    db33 = tmp_path / "k33.db"
+    okm.KmerDb(33, {"a": np.array([1, 2], np.uint64)}).write(str(db33))
+    r = run("query", "-d", str(db33), "-r", "y", "-o", str(tmp_path / "o.txt"))
+    assert r.returncode == 1 and "Invalid K-mer size: 33. Must be between 1 and 32." in r.stderr
+    assert run("query", "-d", str(db33)).returncode == 2  # clap: missing required args
+
+
+def test_classify_host_side_errors(tmp_path):
+    import okm
+    p4, p3 = tmp_path / "k4.db", tmp_path / "k3.db"
+    okm.KmerDb(4, {"dbk4.fa": np.array([27], np.uint64)}).write(str(p4))
+    okm.KmerDb(3, {"dbk3.fa": np.array([6], np.uint64)}).write(str(p3))
+    out = str(tmp_path / "o.json")
+    # classify_tests.rs:480-508, :510-547 — fail before the input is read
+    r = run("classify", "-i", "dummy_input.fa", "-d", str(p4), "--kmer-size", "3", "-o", out)
+    assert r.returncode == 1
+    assert "User-provided k-mer size 3 does not match k-mer size 4 from database" in r.stderr
+    r = run("classify", "-i", "dummy_input.fa", "-d", str(p4), "-d", str(p3), "-o", out)
+    assert r.returncode == 1
+    assert "Effective k-mer size 4 (from first database) does not match k-mer size 3 from database" in r.stderr
+    r = run("classify", "-i", "dummy_input.fa", "-d", str(p4), "--kmer-size", "40", "-o", out)
+    assert r.returncode == 1 and "Invalid K-mer size: 40. Must be between 1 and 32." in r.stderr
+    r = run("classify", "-i", "dummy_input.fa", "-d", str(tmp_path / "nope.db"), "-o", out)
+    assert r.returncode == 1 and "Failed to load database:" in r.stderr
+    assert "DEBUG: Entered run_classify." in r.stderr  # classify.rs:59-64
+    assert not os.path.exists(out)
 
 
 @pytest.mark.skipif(has_gpu(), reason="a HIP device is visible")

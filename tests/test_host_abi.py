@@ -199,3 +199,18 @@ def test_invalid_k_rejected_before_device():
             okm.KmerCounter(k)
         assert ei.value.status == _lib.OKM_E_INVALID_K
         assert f"Invalid K-mer size: {k}. Must be between 1 and 32." in str(ei.value)
+
+
+def test_reader_raw_ids_match_restate(golden_cases, tmp_path):
+    """query.rs:63-71: record.id() + raw record.sequence() (no normalize)."""
+    import restate as R
+    from conftest import case_file_bytes
+    for c in golden_cases["query"]:
+        f = c["reads"]
+        p = tmp_path / f["name"]
+        p.write_bytes(case_file_bytes(f))
+        got = okm.read_fastx_records(str(p), True, raw=True)
+        exp = R.parse_fastx(R.decompress_by_extension(f["name"], case_file_bytes(f)))
+        assert got == exp, c["name"]
+        norm = okm.read_fastx_records(str(p), True, raw=False)
+        assert [s for _i, s in norm] == [R.normalize(s) for _i, s in exp], c["name"]

@@ -156,3 +156,93 @@ def test_c_oracle_pairs_merge():
     k, c = a.result(1)
     assert k.tolist() == [3, 5] and c.tolist() == [2, 11]
     assert a.result(3)[0].tolist() == [5]
+
+
+# --------------------------------------------------------------------------
+# query / classify: restatement vs the reference's tests
+# --------------------------------------------------------------------------
+
+def _db(files, k):
+    return R.build_sets([(n, t.encode()) for n, t in files], k)
+
+
+def test_restate_query_matches_reference_tests(reference_expectations):
+    for c in reference_expectations["query"]:
+        refs = _db(c["db_files"], c["k"])
+        out = R.run_query_bytes(c["k"], refs, "query_reads.fastq", c["reads"].encode(), c["min_hits"])
+        ids = set(out.decode().splitlines())
+        assert ids == set(c["expected_ids"]), c["src"]
+
+
+def test_restate_query_hits_comment_values():
+    # query_tests.rs:119-124: per-read hits 7 / 1 / 0 / (too short) / 9
+    refs = _db([("db.fa", ">ref_genome_segment\nACGTACGTTTGCATC")], 4)
+    allk = set().union(*refs.values())
+    assert [R.query_hits(s, 4, allk) for s in (b"ACGTACGTTT", b"TTGCXXXXXX", b"CCCCCCCCCC", b"ACGTACGTACGT")] == \
+        [7, 1, 0, 9]
+
+
+def _classify(c, user_k="default", min_freq=None, min_cov=None):
+    dbs = []
+    for i, files in enumerate(c["dbs"]):
+        refs = _db(files, c["k"])
+        dbs.append((f"db{i}.db", c["k"], [(n, refs[n]) for n, _t in files]))
+    return R.run_classify_bytes("input.fa", c["input"].encode(), dbs,
+                                c.get("user_k") if user_k == "default" else user_k,
+                                c.get("min_freq", 1) if min_freq is None else min_freq,
+                                c.get("min_cov", 0.0) if min_cov is None else min_cov)
+
+
+def test_restate_classify_matches_reference_tests(reference_expectations):
+    import json
+    for c in reference_expectations["classify"]:
+        js, _tsv = _classify(c)
+        res = json.loads(js)
+        assert res["total_unique_kmers_in_input"] == c["total_unique_kmers_in_input"], c["src"]
+        assert res["min_kmer_frequency_filter"] == c["min_freq"]
+        assert len(res["databases_analyzed"]) == len(c["databases"])
+        for got, exp in zip(res["databases_analyzed"], c["databases"]):
+            assert got["database_kmer_size"] == c["k"]
+            if "references_listed" in exp:
+                assert [r["reference_name"] for r in got["references"]] == exp["references_listed"], c["src"]
+                continue
+            assert got["total_unique_kmers_in_db_across_references"] == exp["union"], c["src"]
+            assert got["overall_input_kmers_matched_in_db"] == exp["matched"], c["src"]
+            assert got["overall_sum_depth_of_matched_kmers_in_input"] == exp["sum_depth"], c["src"]
+            m, sd, u, n_in = exp["matched"], exp["sum_depth"], exp["union"], c["total_unique_kmers_in_input"]
+            assert abs(got["overall_avg_depth_of_matched_kmers_in_input"] - sd / m) < 1e-12
+            assert abs(got["proportion_input_kmers_in_db_overall"] - m / n_in) < 1e-12
+            assert abs(got["proportion_db_kmers_covered_overall"] - m / u) < 1e-12
+            refs = {r["reference_name"]: r for r in got["references"]}
+            assert set(refs) == set(exp["references"])
+            for name, (tot, hit, depth) in exp["references"].items():
+                r = refs[name]
+                assert (r["total_kmers_in_reference"], r["input_kmers_hitting_reference"],
+                        r["sum_depth_of_matched_kmers_in_input"]) == (tot, hit, depth), (c["src"], name)
+                assert abs(r["reference_breadth_of_coverage"] - hit / tot) < 1e-12
+
+
+def test_restate_classify_tsv_matches_reference_tests(reference_expectations):
+    for c in reference_expectations["classify_tsv"]:
+        _js, tsv = _classify(c, user_k=c["k"], min_freq=1)
+        lines = tsv.splitlines()
+        assert lines[0].split("\t")[0] == "InputFile"
+        rows = [ln.split("\t") for ln in lines[1:]]
+        assert [r[2:] for r in rows] == c["rows"], c["src"]
+        assert all(r[0] == "input.fa" for r in rows)
+
+
+def test_restate_classify_errors(reference_expectations):
+    for c in reference_expectations["classify_errors"]:
+        dbs = [(f"db{i}.db", k, []) for i, k in enumerate(c["db_ks"])]
+        with pytest.raises(R.OracleError) as ei:
+            R.run_classify_bytes("dummy_input.fa", b">a\nACGT\n", dbs, c["user_k"])
+        assert c["stderr_contains"] in str(ei.value), c["src"]
+
+
+def test_rust_f64_format():
+    # serde_json / ryu layout (what compare.rs and classify.rs write)
+    cases = {0.0: "0.0", 1.0: "1.0", 0.375: "0.375", 1 / 3: "0.3333333333333333", 1e-5: "0.00001",
+             1e-6: "1e-6", 1.5e-7: "1.5e-7", 1e16: "1e16", 123.0: "123.0", 2.5e15: "2500000000000000.0"}
+    for x, s in cases.items():
+        assert R.rust_f64(x) == s, x
