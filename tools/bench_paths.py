@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Secondary measurements of the §8 rows next to the headline count bench
+(bench.py): one JSON line per workload, same conventions (device-resident
+input, warmup then timed steps bracketed by device syncs).
+
+  --workload query   query.rs:81-99 — per-read hit counts of the BASELINE
+                     configs[1] batch (3,355,443 x 150 bp, k=31) against a
+                     device set of the canonical k-mers of the first half of
+                     those reads (okm_query_hits_device).
+  --workload build   build.rs:46-58 — set-mode counting (DashSet) of the same
+                     batch (okm_add_batch_device + okm_count in OKM_MODE_SET).
+  --workload wide    BASELINE configs[3] shape — k=63 (two-u64 keys) over
+                     ONT-like lognormal reads (median 2,891 bp, sigma 1.085,
+                     clipped 200..100k, 5 % substitutions); --gbases sets the
+                     size (configs[3] is ~5.36 Gbases).
+  --workload classify classify.rs:215-308 — probe a 32-reference database
+                     (the genome split in 32 slices, ~100 M keys) against the
+                     counted table of the batch (okm_classifier_probe_db).
+
+The CPU baseline is the C restatement (oracle/) on a bounded sample, 1 thread.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "orion-kmer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+import okm  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+READS, READ_LEN, GENOME_BP = 3_355_443, 150, 100_000_000
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def c2_batch():
+    t = time.time()
+    b = okm.synth_reads(READS, READ_LEN, genome_len=GENOME_BP, genome_seed=2, seed=2, sub_rate=0.001,
+                        n_rate=0.0001)
+    log(f"synthetic C2 batch: {len(b)} bytes ({time.time() - t:.1f}s)")
+    return b
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    return (time.perf_counter() - t) / steps
+
+
+def valid_windows(batch: np.ndarray, k: int, valid=b"ACGTacgt") -> int:
+    ok = np.zeros(256, bool)
+    ok[list(valid)] = True
+    bad = ~ok[batch]
+    c = np.concatenate([[0], np.cumsum(bad, dtype=np.int64)])
+    return int(((c[k:] - c[:-k]) == 0).sum())
+
+
+def wl_query(args):
+    k = 31
+    batch = c2_batch()
+    half = (READS // 2) * (READ_LEN + 1)
+    dbuf = okm.DeviceBuffer(len(batch))
+    hbuf = okm.DeviceBuffer(4 * READS)
+    dbuf.upload(batch)
+    with okm.KmerCounter(k, "set") as c:
+        c.add_device_batch(dbuf.address, half)
+        db_keys, _ = c.result(1)
+    s = okm.KmerSet(k, 0, len(db_keys))
+    s.insert(db_keys)
+    windows = valid_windows(batch, k)
+    dt = timed(lambda: s.query_hits_device(dbuf.address, len(batch), READS, hbuf.address), args.steps, args.warmup)
+    hits = np.zeros(READS, np.uint32)
+    hbuf.download(hits)
+    bases = READS * READ_LEN
+    alg = len(batch) + 8 * windows  # 1 B/base + one 8-B slot read per valid window
+    # CPU baseline: the C restatement (O(k) per window + binary search) on a sample
+    import oracle
+    m = min(args.cpu_sample_reads, READS)
+    recs = batch[:m * (READ_LEN + 1)].reshape(m, READ_LEN + 1)[:, :READ_LEN]
+    tc = time.perf_counter()
+    exp = oracle.query_hits([r.tobytes() for r in recs], db_keys, k)
+    tcpu = time.perf_counter() - tc
+    assert np.array_equal(exp, hits[:m]), "engine != oracle on the CPU sample"
+    return {
+        "metric": "bases/sec queried (k=31, query.rs per-read hits) on one MI355X",
+        "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u64",
+        "data": "synthetic (BASELINE configs[1] reads, device-resident)",
+        "config": {"workload": "query: 3,355,443 x 150 bp reads vs the k-mer set of the first half of them",
+                   "k": k, "db_unique_kmers": int(len(db_keys)), "valid_windows": windows,
+                   "reads_with_hits": int((hits > 0).sum()), "hits": int(hits.sum(dtype=np.uint64))},
+        "roofline": {"bound": "hbm", "kernel": "k_query_hits<31> (+ k_sep_count, scan)",
+                     "achieved_wall": round(alg / dt / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "alg_bytes_per_step": alg, "frac_wall": round(alg / dt / 1e9 / HBM_PEAK_GBS, 4)},
+        "cpu_baseline": {"value": round(m * READ_LEN / tcpu, 1), "unit": "bases/s", "cores": 1, "kind": "port",
+                         "sample": f"first {m} reads, oracle_query_hits (O(k) encode per window + binary "
+                                   f"search, 1 thread; the reference runs rayon over reads), {tcpu:.1f} s"},
+    }
+
+
+def wl_build(args):
+    k = 31
+    batch = c2_batch()
+    dbuf = okm.DeviceBuffer(len(batch))
+    dbuf.upload(batch)
+    c = okm.KmerCounter(k, "set")
+
+    def step():
+        c.reset()
+        c.add_device_batch(dbuf.address, len(batch))
+        return c.count()
+
+    dt = timed(step, args.steps, args.warmup)
+    n = step()
+    bases = READS * READ_LEN
+    return {"metric": "bases/sec k-mer set built (k=31, build.rs DashSet) on one MI355X",
+            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u64",
+            "data": "synthetic (BASELINE configs[1] reads, device-resident)",
+            "config": {"workload": "build: set of canonical 31-mers of 3,355,443 x 150 bp reads", "k": k,
+                       "distinct": int(n)}}
+
+
+def ont_batch(gbases: float, seed: int = 4):
+    """ONT-like reads: lognormal lengths, 5 % substitutions."""
+    rng = np.random.default_rng(seed)
+    target = int(gbases * 1e9)
+    genome = rng.integers(0, 4, size=min(target // 4 + 200_000, 1_000_000_000), dtype=np.uint8)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    lens = []
+    tot = 0
+    while tot < target:
+        L = rng.lognormal(np.log(2891.0), 1.085, size=65536).clip(200, 100_000).astype(np.int64)
+        lens.append(L)
+        tot += int(L.sum())
+    lens = np.concatenate(lens)
+    lens = lens[:np.searchsorted(np.cumsum(lens), target) + 1]
+    n = len(lens)
+    starts = rng.integers(0, len(genome) - 100_001, size=n)
+    out = np.empty(int(lens.sum()) + n, np.uint8)
+    o = 0
+    for i in range(n):
+        L = int(lens[i])
+        r = genome[starts[i]:starts[i] + L].copy()
+        m = rng.random(L) < 0.05
+        r[m] = rng.integers(0, 4, size=int(m.sum()), dtype=np.uint8)
+        out[o:o + L] = acgt[r]
+        out[o + L] = ord("\n")
+        o += L + 1
+    return out, n
+
+
+def wl_wide(args):
+    k = 63
+    t = time.time()
+    batch, n = ont_batch(args.gbases)
+    bases = len(batch) - n
+    log(f"ONT-like batch: {n} reads, {bases} bases ({time.time() - t:.1f}s)")
+    dbuf = okm.DeviceBuffer(len(batch))
+    dbuf.upload(batch)
+    c = okm.KmerCounter(k, "count", wide=True)
+
+    def step():
+        c.reset()
+        c.add_device_batch(dbuf.address, len(batch))
+        return c.count()
+
+    dt = timed(step, args.steps, args.warmup)
+    info = c.engine_info()
+    return {"metric": "bases/sec k-mer-counted (k=63, two-u64 keys) on one MI355X",
+            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "u128 (two u64)", "data": "synthetic ONT-like (device-resident)",
+            "config": {"workload": f"BASELINE configs[3] shape at {args.gbases} Gbases: lognormal read "
+                                   "lengths (median 2891, sigma 1.085, 200..100k), 5 % substitutions",
+                       "k": k, "reads": n, "bases": bases, "kmers": int(info["kmers"]),
+                       "distinct": int(info["distinct"])},
+            "engine": info}
+
+
+def wl_classify(args):
+    k = 31
+    batch = c2_batch()
+    dbuf = okm.DeviceBuffer(len(batch))
+    dbuf.upload(batch)
+    c = okm.KmerCounter(k, "count")
+    c.add_device_batch(dbuf.address, len(batch))
+    c.count()
+    # 32 references: the k-mers of 32 disjoint slices of the reads' own set
+    keys, _ = c.result(1)
+    rng = np.random.default_rng(5)
+    perm = keys[rng.permutation(len(keys))]
+    refs = np.array_split(perm, 32)
+    cl = okm.Classifier(c, 2)
+    dt = timed(lambda: cl.probe_db(refs), args.steps, args.warmup)
+    r = cl.probe_db(refs)
+    nkeys = len(keys)
+    return {"metric": "reference k-mers/sec probed (classify.rs per-reference stats, k=31) on one MI355X",
+            "value": round(nkeys / dt, 1), "unit": "kmers/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u64",
+            "data": "synthetic (BASELINE configs[1] reads, device-resident counts)",
+            "config": {"workload": "classify: 32 references (~110 M keys from host memory) vs the counted "
+                                   "table of 3,355,443 x 150 bp reads, --min-kmer-frequency 2",
+                       "k": k, "db_keys": nkeys, "input_kmers_after_filter": cl.n_input,
+                       "union": r["union"], "matched": r["matched"]},
+            "note": "per step: host->device copy of the keys (880 MB) + one probe/insert kernel"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["query", "build", "wide", "classify"], required=True)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gbases", type=float, default=1.0)
+    ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
+    args = ap.parse_args()
+    out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify}[args.workload](args)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
