@@ -1,12 +1,12 @@
 // okm_extract.hip — L1 pass: batch bytes -> canonical k-mers -> key-range bins.
 //
 // Restates on the device:
-//   kmer.rs:12-20   dna_base_to_u64      -> base_code / base_valid (+ U/u->T of
-//                                          needletail normalize, count.rs:71)
-//   kmer.rs:37-57   seq_to_u64           -> rolling forward word `fwd`
-//   kmer.rs:79-94   reverse_complement   -> rolling `rc`
+//   kmer.rs:12-20   dna_base_to_u64      -> pack4: SWAR codes + invalid mask (+ U/u->T
+//                                          of needletail normalize, count.rs:71)
+//   kmer.rs:37-57   seq_to_u64           -> fwd_top64: a slice of the packed codes
+//   kmer.rs:79-94   reverse_complement   -> rc_low64: a slice of the complemented codes
 //   kmer.rs:99-106  canonical_u64        -> min(fwd, rc)
-//   count.rs:23-38  window loop          -> scan_windows + valid-run counter
+//   count.rs:23-38  window loop          -> scan_words (okm_scan.h), invalid-mask test
 //
 // Two kernels per batch.  extract_hist counts, per persistent block, the keys
 // of each bin (top l1 bits of the 2k-bit key); the host turns the totals into
@@ -17,11 +17,12 @@
 // instead of 8-byte scattered stores (which cost 3.5x the bytes in HBM
 // writes).
 //
-// Both kernels are instantiated for common k (template K) besides the generic
-// runtime-k one: with K known, the window index of every byte step is a
-// compile-time constant, so extract_scatter keeps a thread's 32 keys (and
-// their within-bin ranks, returned by the histogram atomic) in registers and
-// computes each k-mer ONCE; the generic kernel computes them twice.  Emits are
+// Windows are extracted directly (okm_scan.h: every window's key is a slice
+// of SWAR-packed codes, no rolling state), so the window index is a
+// compile-time constant for every k and extract_scatter keeps a thread's 16
+// keys (and their within-bin ranks, returned by the histogram atomic) in
+// registers, computing each k-mer once.  Kernels are instantiated for common
+// k (template K: constant shifts) besides the runtime-k one.  Emits are
 // branch-free: an invalid window counts into a dummy bin.
 #include "okm_scan.h"
 
@@ -55,45 +56,6 @@ constexpr int kMaxL1Bins = 256;
 
 uint32_t extract_tile() { return (uint32_t)kHTile; }  // chunks are multiples of both tiles
 uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
-
-// Walk the windows starting in [w0, w0 + SEG) of a batch of n bytes and call
-// emit(j, key, valid) for each window start j = 0..SEG-1, in order (K > 0: j
-// is a compile-time constant after unrolling; K = 0: runtime k, runtime j).
-// Bytes at or beyond n read as 0 (invalid), so windows never run off the end;
-// record separators are invalid bytes, so windows never cross records.
-template <int SEG, int K, typename Emit>
-__device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_rt, Emit &&emit) {
-    constexpr int LOAD = WinWords<SEG>::kLoad;
-    const uint32_t k = K ? (uint32_t)K : k_rt;
-    const uint32_t *w = ww.w;
-    const uint64_t kmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1ull);
-    const uint32_t rcs = 2 * k - 2;
-    uint64_t fwd = 0, rc = 0;
-    uint32_t run = 0;
-    constexpr int STEPS = K ? SEG + K - 1 : LOAD - 1;
-#pragma unroll
-    for (int i = 0; i < STEPS; ++i) {
-        const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-        const uint32_t code = base_code(c);
-        fwd = ((fwd << 2) | code) & kmask;                    // kmer.rs:51, rolled
-        rc = (rc >> 2) | ((uint64_t)(code ^ 3u) << rcs);     // kmer.rs:87-91, rolled
-        run = base_valid(c) ? run + 1 : 0;
-        if (K) {
-            if (i >= K - 1) emit(i - K + 1, fwd < rc ? fwd : rc, run >= (uint32_t)K);  // kmer.rs:101
-        } else {
-            const int j = i - (int)k + 1;  // block-uniform condition
-            if (j >= 0 && j < SEG) emit(j, fwd < rc ? fwd : rc, run >= k);
-        }
-    }
-}
-
-template <int SEG, int K, typename Emit>
-__device__ __forceinline__ void scan_windows(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
-                                             uint32_t k_rt, Emit &&emit) {
-    WinWords<SEG> ww;
-    load_windows<SEG>(seq, n, w0, ww);
-    scan_words<SEG, K>(ww, k_rt, emit);
-}
 
 template <int K>
 __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq, ExtractGeom g,
@@ -157,7 +119,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                                                                    uint64_t *__restrict__ out,
                                                                    const ull *__restrict__ cap_end,
                                                                    ull *__restrict__ ovf) {
-    __shared__ ull stage[kTile + 64];        // + one dummy slot per lane for invalid windows (K > 0)
+    __shared__ ull stage[kTile + 64];        // + one dummy slot per lane for invalid windows
     __shared__ ull gcur[kMaxL1Bins];         // this block's next output index per bin
     __shared__ uint32_t hist[kMaxL1Bins + 1];
     __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
@@ -175,8 +137,8 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
     const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
-    WinWords<kSegS> ww;  // K > 0: this tile's bytes, loaded one tile ahead
-    if (K && OKM_EXTRACT_PREFETCH && beg + (uint64_t)t * kSegS < end)
+    WinWords<kSegS> ww;  // this tile's bytes, loaded one tile ahead
+    if (OKM_EXTRACT_PREFETCH && beg + (uint64_t)t * kSegS < end)
         load_windows<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
@@ -185,8 +147,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
         const bool live = w0 < end;
         uint32_t tile_n;
-        if (K) {
-            // one sweep: keys and their within-bin ranks stay in registers
+        {  // one sweep: keys and their within-bin ranks stay in registers
             ull kk[kSegS];
             uint32_t rk[kSegS];  // bin << 16 | rank; invalid: nb << 16
 #pragma unroll
@@ -221,19 +182,6 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                 if (ch && !fits) atomicOr(ovf, 1ull);
                 gcur[t] = fits ? cp : ~0ull;
             }
-        } else {
-            if (live)
-                scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
-                    atomicAdd(&hist[valid ? bin_of(key, shift) : nb], 1u);
-                });
-            __syncthreads();
-            tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
-            if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
-            __syncthreads();
-            if (live)
-                scan_windows<kSegS, 0>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
-                    if (valid) stage[atomicAdd(&lcur[bin_of(key, shift)], 1u)] = key;
-                });
         }
         __syncthreads();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
@@ -264,49 +212,22 @@ __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__
 constexpr int kSegW = 16;                       // scatter windows per thread
 constexpr int kTileW = kExtractBlock * kSegW;   // 4096 windows: 64 KiB stage
 
+// Windows [w0, w0 + SEG) with 2k-bit keys (direct extraction, okm_scan.h):
+// the forward key is the 2k code bits from base j (MSB-first) and the reverse
+// complement the 2k complemented bits from base j (LSB-first), over 128 bits.
 template <int SEG, typename Emit>
 __device__ __forceinline__ void scan_windows_wide(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
                                                   uint32_t k, Emit &&emit) {
-    constexpr int LOAD = SEG + 64;  // covers SEG + k - 1 for k <= 64
-    uint32_t w[LOAD / 4];
-    if (w0 + LOAD <= n) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(seq + w0);
+    WinWords<SEG, 64> ww;
+    load_windows<SEG, 64>(seq, n, w0, ww);
+    constexpr int NP = WinWords<SEG, 64>::kLoad / 16;
+    Codes<NP> c;
+    make_codes<NP, false>(ww.w, c);
 #pragma unroll
-        for (int q = 0; q < LOAD / 16; ++q) {
-            const uint4 v = p[q];
-            w[4 * q + 0] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < LOAD / 4; ++q) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint64_t idx = w0 + 4 * q + b;
-                x |= (idx < n ? (uint32_t)seq[idx] : 0u) << (8 * b);
-            }
-            w[q] = x;
-        }
-    }
-    const uint32_t hbits = 2 * k - 64;  // bits of the key in `hi` (k > 32)
-    const ull hmask = hbits >= 64 ? ~0ull : ((1ull << hbits) - 1ull);
-    const uint32_t rcs = 2 * k - 2 - 64;  // rc's new base lands in `hi`
-    K128 fwd{0, 0}, rc{0, 0};
-    uint32_t run = 0;
-#pragma unroll
-    for (int i = 0; i < LOAD - 1; ++i) {
-        const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-        const uint32_t code = base_code(c);
-        fwd.hi = ((fwd.hi << 2) | (fwd.lo >> 62)) & hmask;       // kmer.rs:51 over 2k bits
-        fwd.lo = (fwd.lo << 2) | code;
-        rc.lo = (rc.lo >> 2) | (rc.hi << 62);                     // kmer.rs:87-91 over 2k bits
-        rc.hi = (rc.hi >> 2) | ((ull)(code ^ 3u) << rcs);
-        run = base_valid(c) ? run + 1 : 0;
-        const int j = i - (int)k + 1;  // block-uniform condition
-        if (j >= 0 && j < SEG) emit(j, KeyOps<K128>::lt(fwd, rc) ? fwd : rc, run >= k);
+    for (int j = 0; j < SEG; ++j) {
+        bool valid;
+        const K128 key = window_key128(c, j, k, &valid);
+        emit(j, key, valid);
     }
 }
 

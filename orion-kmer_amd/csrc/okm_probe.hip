@@ -181,9 +181,9 @@ __device__ __forceinline__ void flush_hits(uint32_t *hits, uint64_t nrec, ull re
     if (cur && rec < nrec) atomicAdd(&hits[rec], cur);
 }
 
-// K > 0: k known at compile time (keys of the thread's SEG windows stay in
-// registers and their home-slot loads are all in flight together); K = 0:
-// runtime k, windows probed one at a time.
+// Keys of the thread's SEG windows stay in registers and their home-slot
+// loads are all in flight together.  K > 0: k known at compile time; K = 0:
+// runtime k.
 template <int K>
 __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__restrict__ seq, uint64_t n,
                                                             const ull *__restrict__ tile_pre, SetTab t,
@@ -200,66 +200,39 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
     if (w0 >= n) return;
 
     const uint32_t k = K ? (uint32_t)K : k_rt;
-    const uint64_t kmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1ull);
-    const uint32_t rcs = 2 * k - 2;
-    uint64_t fwd = 0, rc = 0;
-    uint32_t run = 0;
+    constexpr int NP = WinWords<kQSeg>::kLoad / 16;
+    Codes<NP> c;
+    make_codes<NP, true>(w, c);  // query.rs: raw bytes, U invalid
+    ull key[kQSeg];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int j = 0; j < kQSeg; ++j) {
+        bool valid;
+        key[j] = window_key(c, j, k, &valid);
+        vmask |= (valid ? 1u : 0u) << j;
+    }
+    // every valid window's home slot load in flight before any is consumed
+    ull first[kQSeg];
+    uint64_t home[kQSeg];
+#pragma unroll
+    for (int j = 0; j < kQSeg; ++j) {
+        home[j] = home_slot(key[j], t.shift);
+        first[j] = (vmask >> j) & 1u ? t.slots[home[j]] : kEmpty;
+    }
     ull rec = rec0;
     uint32_t cur = 0;
-    if (K) {
-        ull key[kQSeg];
-        uint32_t vmask = 0;
 #pragma unroll
-        for (int i = 0; i < kQSeg + K - 1; ++i) {
-            const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-            const uint32_t code = base_code(c);
-            fwd = ((fwd << 2) | code) & kmask;                 // kmer.rs:51, rolled
-            rc = (rc >> 2) | ((uint64_t)(code ^ 3u) << rcs);  // kmer.rs:87-91, rolled
-            run = base_valid_raw(c) ? run + 1 : 0;
-            if (i >= K - 1) {
-                const int j = i - K + 1;
-                key[j] = fwd < rc ? fwd : rc;  // kmer.rs:101
-                vmask |= (run >= (uint32_t)K ? 1u : 0u) << j;
-            }
+    for (int j = 0; j < kQSeg; ++j) {
+        if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
+            flush_hits(hits, nrec, rec, cur);
+            cur = 0;
+            ++rec;
         }
-        ull first[kQSeg];
-        uint64_t home[kQSeg];
-#pragma unroll
-        for (int j = 0; j < kQSeg; ++j) {
-            home[j] = home_slot(key[j], t.shift);
-            first[j] = (vmask >> j) & 1u ? t.slots[home[j]] : kEmpty;
-        }
-#pragma unroll
-        for (int j = 0; j < kQSeg; ++j) {
-            if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
-                flush_hits(hits, nrec, rec, cur);
-                cur = 0;
-                ++rec;
-            }
-            if ((vmask >> j) & 1u) {
-                const bool hit = first[j] == key[j] ? true
-                                 : first[j] == kEmpty ? false
-                                                      : set_probe_rest(t, key[j], home[j]);
-                cur += hit ? 1u : 0u;
-            }
-        }
-    } else {
-        for (int i = 0; i < WinWords<kQSeg>::kLoad - 1; ++i) {
-            const uint32_t c = (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-            const uint32_t code = base_code(c);
-            fwd = ((fwd << 2) | code) & kmask;
-            rc = (rc >> 2) | ((uint64_t)(code ^ 3u) << rcs);
-            run = base_valid_raw(c) ? run + 1 : 0;
-            const int j = i - (int)k + 1;
-            if (j >= 0 && j < kQSeg && run >= k) {
-                const ull r = rec0 + __popc(sepm & ((1u << j) - 1u));
-                if (r != rec) {
-                    flush_hits(hits, nrec, rec, cur);
-                    cur = 0;
-                    rec = r;
-                }
-                cur += set_contains(t, fwd < rc ? fwd : rc) ? 1u : 0u;
-            }
+        if ((vmask >> j) & 1u) {
+            const bool hit = first[j] == key[j] ? true
+                             : first[j] == kEmpty ? false
+                                                  : set_probe_rest(t, key[j], home[j]);
+            cur += hit ? 1u : 0u;
         }
     }
     flush_hits(hits, nrec, rec, cur);
