@@ -26,7 +26,7 @@ struct okm_db {
     std::vector<std::vector<uint64_t>> keys;
 };
 
-static void put_u64(std::vector<uint8_t> &b, uint64_t v) {
+static void put_u64(Bytes &b, uint64_t v) {
     for (int i = 0; i < 8; ++i) b.push_back((uint8_t)(v >> (8 * i)));
 }
 
@@ -58,7 +58,7 @@ okm_status okm_db_write(const okm_db *db, const char *path) {
     OutWriter w;
     okm_status s = w.open(path);
     if (s != OKM_OK) return s;
-    std::vector<uint8_t> b;
+    Bytes b;
     b.push_back(db->k);
     put_u64(b, db->names.size());
     for (size_t i = 0; i < db->names.size(); ++i) {
@@ -82,7 +82,7 @@ okm_status okm_db_write(const okm_db *db, const char *path) {
 okm_status okm_db_read(okm_db **out, const char *path) {
     if (!out || !path) return fail(OKM_E_ARG, "null argument");
     *out = nullptr;
-    std::vector<uint8_t> d;
+    Bytes d;
     okm_status s = read_whole_file(path, d);
     if (s != OKM_OK) return s;
     if (decompress_by_extension(path, d) != OKM_OK) return fail(OKM_E_FORMAT, okm_last_error());

@@ -15,7 +15,11 @@
 //    from …");
 //  - normalize(false): A C G T kept, a c g t upper-cased, U/u -> T,
 //    '.', '~' -> '-', space/tab/CR/LF removed, every other byte -> 'N'.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <chrono>
 
 #include <string>
 #include <vector>
@@ -40,29 +44,14 @@ static const uint8_t *norm_table() {
     return t;
 }
 
-// Append normalize(src[0..n)) to out.
-static void normalize_append(const uint8_t *src, size_t n, std::vector<uint8_t> &out) {
-    const uint8_t *t = norm_table();
-    const size_t base = out.size();
-    out.resize(base + n);
-    uint8_t *d = out.data() + base;
-    size_t o = 0;
-    for (size_t i = 0; i < n; ++i) {
-        const uint8_t v = t[src[i]];
-        d[o] = v;
-        o += v != 0;
-    }
-    out.resize(base + o);
-}
-
 struct Parser {
-    std::vector<uint8_t> data;
+    Bytes data;
     size_t pos = 0;
     bool fastq = false;
     bool raw = false;   // query.rs:66: record.sequence() as is (no normalize)
     bool want_ids = false;
     uint64_t records = 0;
-    std::vector<uint8_t> ids;     // ids of the records read by the current batch
+    Bytes ids;     // ids of the records read by the current batch
     std::vector<uint64_t> id_off;
 
     void add_id(size_t b, size_t e) {  // needletail id(): header after the marker, CR trimmed
@@ -71,15 +60,57 @@ struct Parser {
         id_off.push_back(ids.size());
     }
 
-    // raw_seq: the sequence bytes with their line breaks (multi-line FASTA
-    // keeps its interior '\n'; the record's final line terminator and one
-    // trailing CR dropped).
-    void append_seq(size_t b, size_t e, std::vector<uint8_t> &seq) {
-        if (!raw) {
-            normalize_append(data.data() + b, e - b, seq);
-            return;
+    // Append the sequences of records spans[i] = [b, e) to seq / off: raw
+    // bytes (record.sequence(): multi-line FASTA keeps its interior '\n'; the
+    // record's final line terminator and one trailing CR dropped) or their
+    // normalize(false).  Groups of records are normalised on parallel threads
+    // straight into seq, each group at the offset its raw byte count bounds;
+    // groups that shrank (removed whitespace) are then slid down in order.
+    void emit(const std::vector<std::pair<size_t, size_t>> &spans, Bytes &seq,
+              std::vector<uint64_t> &off) {
+        const size_t n = spans.size();
+        if (!n) return;
+        size_t total = 0;
+        for (auto &sp : spans) total += sp.second - sp.first;
+        const size_t ng = total < (4u << 20) ? 1 : std::min<size_t>(4 * (size_t)host_threads(), n);
+        std::vector<size_t> gb(ng + 1), ub(ng + 1, seq.size()), got(ng);
+        for (size_t g = 0; g <= ng; ++g) gb[g] = n * g / ng;
+        for (size_t g = 0; g < ng; ++g) {
+            size_t want = 0;
+            for (size_t i = gb[g]; i < gb[g + 1]; ++i) want += spans[i].second - spans[i].first;
+            ub[g + 1] = ub[g] + want;
         }
-        seq.insert(seq.end(), data.begin() + b, data.begin() + e);
+        seq.resize(ub[ng]);
+        const size_t rec0 = off.size();
+        off.resize(rec0 + n);
+        const uint8_t *t = norm_table();
+        parallel_for(ng, [&](size_t g) {
+            uint8_t *d = seq.data() + ub[g];
+            size_t o = 0;
+            for (size_t i = gb[g]; i < gb[g + 1]; ++i) {
+                const uint8_t *src = data.data() + spans[i].first;
+                const size_t len = spans[i].second - spans[i].first;
+                if (raw) {
+                    memcpy(d + o, src, len);
+                    o += len;
+                } else {
+                    for (size_t j = 0; j < len; ++j) {
+                        const uint8_t v = t[src[j]];
+                        d[o] = v;
+                        o += v != 0;
+                    }
+                }
+                off[rec0 + i] = o;  // group-relative end, rebased below
+            }
+            got[g] = o;
+        });
+        size_t at = ub[0];
+        for (size_t g = 0; g < ng; ++g) {
+            if (at != ub[g]) memmove(seq.data() + at, seq.data() + ub[g], got[g]);
+            for (size_t i = gb[g]; i < gb[g + 1]; ++i) off[rec0 + i] += at;
+            at += got[g];
+        }
+        seq.resize(at);
     }
 
     okm_status init() {
@@ -90,26 +121,60 @@ struct Parser {
         else if (data[0] == '@') fastq = true;
         else return fail(OKM_E_PARSE, "expected '>' or '@' at the start of the input");
         pos = 0;
+        index_lines();
         return OKM_OK;
+    }
+
+    // Positions of every '\n' (context-free, so found by parallel threads over
+    // chunks); the record walk then costs O(1) per line.
+    std::vector<uint64_t> nl;
+    size_t li = 0;  // index of the first newline at or after pos
+
+    void index_lines() {
+        const size_t n = data.size(), chunk = (size_t)16 << 20;
+        const size_t nc = (n + chunk - 1) / chunk;
+        std::vector<std::vector<uint64_t>> part(nc);
+        parallel_for(nc, [&](size_t c) {
+            const uint8_t *d = data.data();
+            const size_t b = c * chunk, e = std::min(n, b + chunk);
+            auto &v = part[c];
+            v.reserve((e - b) / 64);
+            for (const uint8_t *q = d + b; q < d + e;) {
+                const uint8_t *f = (const uint8_t *)memchr(q, '\n', (size_t)(d + e - q));
+                if (!f) break;
+                v.push_back((uint64_t)(f - d));
+                q = f + 1;
+            }
+        });
+        size_t tot = 0;
+        for (auto &v : part) tot += v.size();
+        nl.clear();
+        nl.reserve(tot);
+        for (auto &v : part) nl.insert(nl.end(), v.begin(), v.end());
+        li = 0;
     }
 
     // line [pos, eol) ; returns false at end of data
     bool line(size_t &b, size_t &e) {
         if (pos >= data.size()) return false;
         b = pos;
-        const uint8_t *nl = (const uint8_t *)memchr(data.data() + pos, '\n', data.size() - pos);
-        e = nl ? (size_t)(nl - data.data()) : data.size();
-        pos = nl ? e + 1 : data.size();
+        if (li < nl.size()) {
+            e = nl[li++];
+            pos = e + 1;
+        } else {
+            e = pos = data.size();
+        }
         return true;
     }
 
-    static size_t rstrip_cr(const std::vector<uint8_t> &d, size_t b, size_t e) {
+    static size_t rstrip_cr(const Bytes &d, size_t b, size_t e) {
         while (e > b && d[e - 1] == '\r') --e;
         return e;
     }
 
-    // Next record: appends its normalised sequence to seq. *got=false at end.
-    okm_status next(std::vector<uint8_t> &seq, bool *got) {
+    // Next record: its sequence bytes are data[*sb, *se) (raw; normalize()
+    // applies to them unless `raw`).  *got=false at end.
+    okm_status next_span(size_t *osb, size_t *ose, bool *got) {
         *got = false;
         if (!fastq) {
             if (pos >= data.size()) return OKM_OK;
@@ -120,24 +185,22 @@ struct Parser {
             const size_t s0 = pos;
             // the sequence runs to the next "\n>" (a line starting with '>')
             size_t end = data.size();
-            size_t p = s0;
+            size_t p = s0;  // every p below is a line start
             while (p < data.size()) {
-                if (data[p] == '>' && (p == s0 || data[p - 1] == '\n')) {
+                if (data[p] == '>') {
                     end = p;
                     break;
                 }
-                const uint8_t *nl = (const uint8_t *)memchr(data.data() + p, '\n', data.size() - p);
-                if (!nl) break;
-                p = (size_t)(nl - data.data()) + 1;
+                if (li >= nl.size()) break;
+                p = nl[li++] + 1;
             }
+            size_t se = end;
             if (raw) {
-                size_t se = end;
                 if (se > s0 && data[se - 1] == '\n') --se;  // the record's last line terminator
                 if (se > s0 && data[se - 1] == '\r') --se;
-                append_seq(s0, se, seq);
-            } else {
-                append_seq(s0, end, seq);
             }
+            *osb = s0;
+            *ose = se;
             pos = end;
             ++records;
             *got = true;
@@ -148,6 +211,7 @@ struct Parser {
         while (q < data.size() && (data[q] == '\n' || data[q] == '\r')) ++q;
         if (q >= data.size()) {
             pos = data.size();
+            li = nl.size();
             return OKM_OK;
         }
         size_t hb, he, sb, se, pb, pe, qb, qe;
@@ -159,7 +223,8 @@ struct Parser {
         qe = rstrip_cr(data, qb, qe);
         if (se - sb != qe - qb) return fail(OKM_E_RECORD, "sequence and quality lengths differ");
         if (want_ids) add_id(hb + 1, he);
-        append_seq(sb, se, seq);
+        *osb = sb;
+        *ose = se;
         ++records;
         *got = true;
         return OKM_OK;
@@ -172,7 +237,7 @@ using namespace okm;
 
 struct okm_reader {
     Parser p;
-    std::vector<uint8_t> seq;
+    Bytes seq;
     std::vector<uint64_t> off;
 };
 
@@ -213,14 +278,26 @@ okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **se
     r->off.assign(1, 0);
     r->p.ids.clear();
     r->p.id_off.assign(1, 0);
+    std::vector<std::pair<size_t, size_t>> spans;
+    uint64_t bytes = 0;
+    auto T0 = std::chrono::steady_clock::now();
     for (;;) {
         bool got = false;
-        okm_status s = r->p.next(r->seq, &got);
+        size_t b = 0, e = 0;
+        okm_status s = r->p.next_span(&b, &e, &got);
         if (s != OKM_OK) return s;
         if (!got) break;
-        r->off.push_back(r->seq.size());
-        if (r->seq.size() >= max_bytes) break;
+        spans.emplace_back(b, e);
+        bytes += e - b;
+        if (bytes >= max_bytes) break;
     }
+    auto T1 = std::chrono::steady_clock::now();
+    r->p.emit(spans, r->seq, r->off);
+    auto T2 = std::chrono::steady_clock::now();
+    if (getenv("OKM_PROF_READER"))
+        fprintf(stderr, "reader: spans %.3f ms emit %.3f ms (%zu records)\n",
+                std::chrono::duration<double, std::milli>(T1 - T0).count(),
+                std::chrono::duration<double, std::milli>(T2 - T1).count(), spans.size());
     *seq = r->seq.data();
     *offsets = r->off.data();
     *n_records = r->off.size() - 1;
@@ -246,15 +323,18 @@ okm_status okm_parse_buffer(const uint8_t *data, uint64_t n, uint8_t **seq, uint
     p.data.assign(data, data + n);
     okm_status s = p.init();
     if (s != OKM_OK) return s;
-    std::vector<uint8_t> sq;
+    Bytes sq;
     std::vector<uint64_t> off(1, 0);
+    std::vector<std::pair<size_t, size_t>> spans;
     for (;;) {
         bool got = false;
-        s = p.next(sq, &got);
+        size_t b = 0, e = 0;
+        s = p.next_span(&b, &e, &got);
         if (s != OKM_OK) return s;
         if (!got) break;
-        off.push_back(sq.size());
+        spans.emplace_back(b, e);
     }
+    p.emit(spans, sq, off);
     *seq = (uint8_t *)malloc(sq.size() ? sq.size() : 1);
     *offsets = (uint64_t *)malloc(off.size() * sizeof(uint64_t));
     if (!*seq || !*offsets) return fail(OKM_E_NOMEM, "host allocation");

@@ -9,11 +9,20 @@
 // and needletail 0.5.1's compression sniffing (gzip/bzip2/xz magic; its
 // Cargo features have no zstd, Cargo.lock:580-591).
 //
-// zlib is linked; liblzma, libzstd and libbz2 exist in the image only as
-// runtime libraries (no headers), so they are bound with dlopen() and the few
-// stable prototypes/structs of their public C APIs are declared here.
+// zlib is linked; liblzma, libzstd, libbz2 and libdeflate exist in the image
+// only as runtime libraries (no headers), so they are bound with dlopen() and
+// the few stable prototypes/structs of their public C APIs are declared here.
+//
+// Host feed: gzip input is inflated with libdeflate when present
+// (BGZF members in parallel), .gz output is written as parallel-compressed
+// gzip members (flate2's MultiGzDecoder and every gzip reader take them; the
+// parity unit is the decompressed text), TSV lines are formatted in parallel
+// chunks, and files are read with one sized read().
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <stdio.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
@@ -135,14 +144,131 @@ static Bz2 *bz2_lib() {
     return B.h ? &B : nullptr;
 }
 
+struct Deflate {  // libdeflate 1.x
+    void *h = nullptr;
+    void *(*alloc_decompressor)() = nullptr;
+    void (*free_decompressor)(void *) = nullptr;
+    int (*gzip_decompress_ex)(void *, const void *, size_t, void *, size_t, size_t *, size_t *) = nullptr;
+    int (*deflate_decompress)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    void *(*alloc_compressor)(int) = nullptr;
+    void (*free_compressor)(void *) = nullptr;
+    size_t (*gzip_compress)(void *, const void *, size_t, void *, size_t) = nullptr;
+    size_t (*gzip_compress_bound)(void *, size_t) = nullptr;
+};
+
+static Deflate *deflate_lib() {
+    static Deflate D;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        if (!getenv("OKM_NO_LIBDEFLATE")) D.h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (D.h && !(bind(D.h, "libdeflate_alloc_decompressor", D.alloc_decompressor) &&
+                     bind(D.h, "libdeflate_free_decompressor", D.free_decompressor) &&
+                     bind(D.h, "libdeflate_gzip_decompress_ex", D.gzip_decompress_ex) &&
+                     bind(D.h, "libdeflate_deflate_decompress", D.deflate_decompress) &&
+                     bind(D.h, "libdeflate_alloc_compressor", D.alloc_compressor) &&
+                     bind(D.h, "libdeflate_free_compressor", D.free_compressor) &&
+                     bind(D.h, "libdeflate_gzip_compress", D.gzip_compress) &&
+                     bind(D.h, "libdeflate_gzip_compress_bound", D.gzip_compress_bound)))
+            D.h = nullptr;
+    }
+    return D.h ? &D : nullptr;
+}
+
 // ---------------------------------------------------------------------------
 // decoders (whole buffer -> whole buffer)
 // ---------------------------------------------------------------------------
-static okm_status gunzip(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
+
+// BGZF (blocked gzip: every member carries its size in a 'BC' extra field and
+// its ISIZE in the trailer) -> member list, or false for plain gzip.
+static bool bgzf_members(const uint8_t *in, size_t n, std::vector<size_t> &mb, std::vector<size_t> &ob) {
+    mb.assign(1, 0);
+    ob.assign(1, 0);
+    size_t pos = 0;
+    while (pos < n) {
+        if (n - pos < 18 || in[pos] != 0x1f || in[pos + 1] != 0x8b || in[pos + 2] != 8 || !(in[pos + 3] & 4))
+            return false;
+        const size_t xlen = in[pos + 10] | ((size_t)in[pos + 11] << 8);
+        size_t bsize = 0;
+        for (size_t x = pos + 12; x + 4 <= pos + 12 + xlen && x + 4 <= n;) {
+            const size_t slen = in[x + 2] | ((size_t)in[x + 3] << 8);
+            if (in[x] == 'B' && in[x + 1] == 'C' && slen == 2 && x + 6 <= n) bsize = (in[x + 4] | ((size_t)in[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize || pos + bsize > n || bsize < 26) return false;
+        const uint8_t *t = in + pos + bsize - 4;
+        const size_t isize = t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+        pos += bsize;
+        mb.push_back(pos);
+        ob.push_back(ob.back() + isize);
+    }
+    return mb.size() > 1;
+}
+
+static okm_status gunzip_libdeflate(Deflate *D, const uint8_t *in, size_t n, Bytes &out) {
+    std::vector<size_t> mb, ob;
+    if (bgzf_members(in, n, mb, ob)) {  // members are independent: inflate them in parallel
+        out.resize(ob.back());
+        std::atomic<int> bad{0};
+        const size_t nm = mb.size() - 1, per = 64;
+        parallel_for((nm + per - 1) / per, [&](size_t g) {
+            void *d = D->alloc_decompressor();
+            for (size_t m = g * per; m < std::min(nm, (g + 1) * per) && d; ++m) {
+                size_t used = 0, got = 0;
+                if (D->gzip_decompress_ex(d, in + mb[m], mb[m + 1] - mb[m], out.data() + ob[m], ob[m + 1] - ob[m],
+                                          &used, &got) != 0 || got != ob[m + 1] - ob[m])
+                    bad = 1;
+            }
+            if (d) D->free_decompressor(d);
+            else bad = 1;
+        });
+        if (bad) return fail(OKM_E_IO, "invalid gzip data");
+        return OKM_OK;
+    }
+    // flate2::read::MultiGzDecoder: every concatenated member, in order
+    void *d = D->alloc_decompressor();
+    if (!d) return fail(OKM_E_NOMEM, "libdeflate allocation");
+    out.clear();
+    size_t pos = 0;
+    okm_status st = OKM_OK;
+    while (pos < n) {
+        // a single-member file's ISIZE (mod 2^32) sizes the output exactly
+        size_t cap = std::max<size_t>(n - pos, 1 << 16) * 4;
+        const uint8_t *t = in + n - 4;
+        const size_t isz = t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+        if (pos == 0 && isz > cap) cap = isz + 1;
+        for (;;) {
+            const size_t base = out.size();
+            out.resize(base + cap);
+            size_t used = 0, got = 0;
+            const int rc = D->gzip_decompress_ex(d, in + pos, n - pos, out.data() + base, cap, &used, &got);
+            if (rc == 0) {
+                out.resize(base + got);
+                pos += used;
+                break;
+            }
+            out.resize(base);
+            if (rc != 3 /*LIBDEFLATE_INSUFFICIENT_SPACE*/ || cap > ((size_t)1 << 40)) {
+                st = fail(OKM_E_IO, rc == 2 ? "truncated gzip data" : "invalid gzip data");
+                break;
+            }
+            cap *= 2;
+        }
+        if (st != OKM_OK) break;
+        size_t p = pos;  // trailing zero padding after the last member is tolerated
+        while (p < n && in[p] == 0) ++p;
+        if (p == n) break;
+    }
+    D->free_decompressor(d);
+    return st;
+}
+
+static okm_status gunzip(const uint8_t *in, size_t n, Bytes &out) {
+    if (Deflate *D = deflate_lib()) return gunzip_libdeflate(D, in, n, out);
     // flate2::read::MultiGzDecoder: decode every concatenated gzip member
     out.clear();
     size_t pos = 0;
-    std::vector<uint8_t> buf(1 << 20);
+    Bytes buf(1 << 20);
     while (pos < n) {
         z_stream z;
         memset(&z, 0, sizeof(z));
@@ -174,14 +300,14 @@ static okm_status gunzip(const uint8_t *in, size_t n, std::vector<uint8_t> &out)
     return OKM_OK;
 }
 
-static okm_status unxz(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
+static okm_status unxz(const uint8_t *in, size_t n, Bytes &out) {
     Lzma *L = lzma_lib();
     if (!L) return fail(OKM_E_IO, "liblzma.so.5 not available");
     LzmaStream s;
     memset(&s, 0, sizeof(s));
     if (L->stream_decoder(&s, UINT64_MAX, 0x08 /*LZMA_CONCATENATED*/) != 0)
         return fail(OKM_E_IO, "lzma decoder init failed");
-    std::vector<uint8_t> buf(1 << 20);
+    Bytes buf(1 << 20);
     s.next_in = in;
     s.avail_in = n;
     out.clear();
@@ -200,13 +326,13 @@ static okm_status unxz(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
     return OKM_OK;
 }
 
-static okm_status unzstd(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
+static okm_status unzstd(const uint8_t *in, size_t n, Bytes &out) {
     Zstd *Z = zstd_lib();
     if (!Z) return fail(OKM_E_IO, "libzstd.so.1 not available");
     void *ds = Z->createDStream();
     Z->initDStream(ds);
     ZstdInBuf ib{in, n, 0};
-    std::vector<uint8_t> buf(1 << 20);
+    Bytes buf(1 << 20);
     out.clear();
     for (;;) {
         ZstdOutBuf ob{buf.data(), buf.size(), 0};
@@ -222,12 +348,12 @@ static okm_status unzstd(const uint8_t *in, size_t n, std::vector<uint8_t> &out)
     return OKM_OK;
 }
 
-static okm_status unbz2(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
+static okm_status unbz2(const uint8_t *in, size_t n, Bytes &out) {
     Bz2 *B = bz2_lib();
     if (!B) return fail(OKM_E_IO, "libbz2.so.1 not available");
     out.clear();
     size_t pos = 0;
-    std::vector<uint8_t> buf(1 << 20);
+    Bytes buf(1 << 20);
     while (pos < n) {  // concatenated streams
         BzStream s;
         memset(&s, 0, sizeof(s));
@@ -267,22 +393,66 @@ std::string lower_extension(const std::string &path) {
     return e;
 }
 
-okm_status read_whole_file(const std::string &path, std::vector<uint8_t> &data) {
-    FILE *f = fopen(path.c_str(), "rb");
-    if (!f) return fail(OKM_E_IO, "cannot open " + path);
-    data.clear();
-    std::vector<uint8_t> buf(1 << 22);
-    size_t got;
-    while ((got = fread(buf.data(), 1, buf.size(), f)) > 0) data.insert(data.end(), buf.data(), buf.data() + got);
-    const bool err = ferror(f);
-    fclose(f);
-    if (err) return fail(OKM_E_IO, "read error on " + path);
-    return OKM_OK;
+int host_threads() {
+    static int n = 0;
+    if (!n) {
+        const char *e = getenv("OKM_HOST_THREADS");
+        if (!e || !*e) e = getenv("OMP_NUM_THREADS");
+        int v = e && *e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        n = std::max(1, std::min(v > 0 ? v : 1, 16));
+    }
+    return n;
 }
 
-okm_status decompress_by_extension(const std::string &path, std::vector<uint8_t> &data) {
+okm_status read_whole_file(const std::string &path, Bytes &data) {
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return fail(OKM_E_IO, "cannot open " + path);
+    struct stat st;
+    data.clear();
+    okm_status s = OKM_OK;
+    if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {  // one sized buffer, parallel pread()s
+        // (the destination pages are first touched by the reading threads)
+        const size_t size = (size_t)st.st_size, chunk = (size_t)64 << 20;
+        data.resize(size);
+        const size_t nc = (size + chunk - 1) / chunk;
+        std::vector<size_t> got(nc, 0);
+        std::atomic<int> bad{0};
+        parallel_for(nc, [&](size_t c) {
+            const size_t b = c * chunk, e = std::min(size, b + chunk);
+            size_t o = b;
+            while (o < e) {
+                const ssize_t r = ::pread(fd, data.data() + o, e - o, (off_t)o);
+                if (r < 0) {
+                    bad = 1;
+                    break;
+                }
+                if (r == 0) break;
+                o += (size_t)r;
+            }
+            got[c] = o - b;
+        });
+        size_t o = 0;  // a file that shrank while being read: keep the prefix that was read
+        for (size_t c = 0; c < nc; ++c) {
+            o += got[c];
+            if (got[c] < std::min(chunk, size - c * chunk)) break;
+        }
+        if (bad) s = fail(OKM_E_IO, "read error on " + path);
+        data.resize(o);
+        if (s == OKM_OK && lseek(fd, (off_t)o, SEEK_SET) < 0) s = fail(OKM_E_IO, "read error on " + path);
+    }
+    if (s == OKM_OK) {  // anything the size did not cover (pipes, growing files)
+        Bytes buf(1 << 22);
+        ssize_t r;
+        while ((r = ::read(fd, buf.data(), buf.size())) > 0) data.insert(data.end(), buf.data(), buf.data() + r);
+        if (r < 0) s = fail(OKM_E_IO, "read error on " + path);
+    }
+    ::close(fd);
+    return s;
+}
+
+okm_status decompress_by_extension(const std::string &path, Bytes &data) {
     const std::string e = lower_extension(path);
-    std::vector<uint8_t> out;
+    Bytes out;
     if (e == "gz") {
         okm_status s = gunzip(data.data(), data.size(), out);
         if (s != OKM_OK) return s;
@@ -299,8 +469,8 @@ okm_status decompress_by_extension(const std::string &path, std::vector<uint8_t>
     return OKM_OK;
 }
 
-okm_status sniff_decompress(std::vector<uint8_t> &data) {
-    std::vector<uint8_t> out;
+okm_status sniff_decompress(Bytes &data) {
+    Bytes out;
     const size_t n = data.size();
     const uint8_t *d = data.data();
     okm_status s = OKM_OK;
@@ -319,11 +489,12 @@ okm_status sniff_decompress(std::vector<uint8_t> &data) {
 // ---------------------------------------------------------------------------
 struct OutWriter::Impl {
     FILE *f = nullptr;
-    int kind = 0;  // 0 plain 1 gz 2 xz 3 zst
+    int kind = 0;  // 0 plain 1 gz (zlib stream) 2 xz 3 zst 4 gz (parallel libdeflate members)
+    bool wrote = false;
     z_stream z;
     LzmaStream lz;
     void *zc = nullptr;
-    std::vector<uint8_t> obuf;
+    Bytes obuf;
     bool ok = true;
 };
 
@@ -338,7 +509,9 @@ okm_status OutWriter::open(const std::string &path) {
     if (!p_->f) return fail(OKM_E_IO, "cannot create " + path);
     const std::string e = lower_extension(path);
     p_->obuf.resize(1 << 20);
-    if (e == "gz") {
+    if (e == "gz" && deflate_lib()) {
+        p_->kind = 4;
+    } else if (e == "gz") {
         p_->kind = 1;
         memset(&p_->z, 0, sizeof(p_->z));
         if (deflateInit2(&p_->z, 6 /*flate2 Compression::default()*/, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
@@ -364,6 +537,12 @@ okm_status OutWriter::write(const void *data, size_t n) {
     if (!I.f) return fail(OKM_E_STATE, "writer not open");
     if (n == 0) return OKM_OK;
     switch (I.kind) {
+    case 4: {
+        const size_t piece = (size_t)4 << 20;
+        std::vector<std::pair<const uint8_t *, size_t>> blocks;
+        for (size_t o = 0; o < n; o += piece) blocks.emplace_back((const uint8_t *)data + o, std::min(piece, n - o));
+        return write_blocks(blocks);
+    }
     case 0:
         if (fwrite(data, 1, n, I.f) != n) return fail(OKM_E_IO, "write failed");
         return OKM_OK;
@@ -405,10 +584,61 @@ okm_status OutWriter::write(const void *data, size_t n) {
     return OKM_OK;
 }
 
+// Blocks in order.  Kind 4 compresses each block into its own gzip member on
+// parallel threads (level 6, flate2's default) and writes the members in
+// order: the concatenation decompresses to the blocks' concatenation
+// (MultiGzDecoder, gzip -d, zcat).
+okm_status OutWriter::write_blocks(const std::vector<std::pair<const uint8_t *, size_t>> &blocks) {
+    Impl &I = *p_;
+    if (!I.f) return fail(OKM_E_STATE, "writer not open");
+    if (I.kind != 4) {
+        for (auto &b : blocks) {
+            okm_status s = write(b.first, b.second);
+            if (s != OKM_OK) return s;
+        }
+        return OKM_OK;
+    }
+    Deflate *D = deflate_lib();
+    const size_t nb = blocks.size();
+    std::vector<Bytes> out(nb);
+    std::atomic<int> bad{0};
+    const size_t nt = std::min<size_t>(nb, (size_t)host_threads());
+    parallel_for(nt, [&](size_t t) {
+        void *c = D->alloc_compressor(6);
+        if (!c) {
+            bad = 1;
+            return;
+        }
+        for (size_t i = t; i < nb; i += nt) {
+            if (!blocks[i].second) continue;
+            out[i].resize(D->gzip_compress_bound(c, blocks[i].second));
+            const size_t m = D->gzip_compress(c, blocks[i].first, blocks[i].second, out[i].data(), out[i].size());
+            if (!m) bad = 1;
+            out[i].resize(m);
+        }
+        D->free_compressor(c);
+    });
+    if (bad) return fail(OKM_E_IO, "gzip compression failed");
+    for (auto &o : out) {
+        if (o.empty()) continue;
+        if (fwrite(o.data(), 1, o.size(), I.f) != o.size()) return fail(OKM_E_IO, "write failed");
+        I.wrote = true;
+    }
+    return OKM_OK;
+}
+
 okm_status OutWriter::close() {
     Impl &I = *p_;
     if (!I.f) return OKM_OK;
     okm_status st = OKM_OK;
+    if (I.kind == 4 && !I.wrote) {  // an empty output is still one (empty) gzip member
+        Deflate *D = deflate_lib();
+        void *c = D->alloc_compressor(6);
+        Bytes o(c ? D->gzip_compress_bound(c, 0) : 0);
+        const size_t m = c ? D->gzip_compress(c, "", 0, o.data(), o.size()) : 0;
+        if (c) D->free_compressor(c);
+        if (!m || fwrite(o.data(), 1, m, I.f) != m) st = fail(OKM_E_IO, "gzip compression failed");
+    }
     if (I.kind == 1) {
         int rc;
         do {
@@ -531,12 +761,20 @@ okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *key
     OutWriter w;
     okm_status s = w.open(path);
     if (s != OKM_OK) return s;
-    std::string buf;
-    const uint64_t step = 1 << 20;
-    for (uint64_t o = 0; o < n; o += step) {
-        const uint64_t m = std::min(step, n - o);
-        format_counts_tsv(k, keys + o * (k > 32 ? 2 : 1), counts + o, m, buf);
-        s = w.write(buf.data(), buf.size());
+    // Blocks of `step` lines formatted on parallel threads, a round of
+    // 2 x host_threads() blocks at a time, written in order.
+    const uint64_t step = 1 << 17;
+    const size_t per_round = 2 * (size_t)host_threads();
+    std::vector<std::string> buf(per_round);
+    for (uint64_t o = 0; o < n; o += step * per_round) {
+        const size_t nb = (size_t)std::min<uint64_t>(per_round, (n - o + step - 1) / step);
+        parallel_for(nb, [&](size_t b) {
+            const uint64_t at = o + b * step, m = std::min(step, n - at);
+            format_counts_tsv(k, keys + at * (k > 32 ? 2 : 1), counts + at, m, buf[b]);
+        });
+        std::vector<std::pair<const uint8_t *, size_t>> blocks;
+        for (size_t b = 0; b < nb; ++b) blocks.emplace_back((const uint8_t *)buf[b].data(), buf[b].size());
+        s = w.write_blocks(blocks);
         if (s != OKM_OK) return s;
     }
     return w.close();
@@ -554,7 +792,7 @@ okm_status okm_write_file(const char *path, const uint8_t *data, uint64_t n) {
 
 okm_status okm_read_file(const char *path, int decompress_by_ext, uint8_t **data, uint64_t *n) {
     if (!path || !data || !n) return fail(OKM_E_ARG, "null argument");
-    std::vector<uint8_t> v;
+    Bytes v;
     okm_status s = read_whole_file(path, v);
     if (s != OKM_OK) return s;
     if (decompress_by_ext) {

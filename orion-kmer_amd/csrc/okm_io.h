@@ -2,19 +2,60 @@
 #pragma once
 
 #include <stdint.h>
+
+#include <algorithm>
+#include <memory>
+#include <utility>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orion_kmer.h"
 
 namespace okm {
 
+// Byte buffers whose resize() does not zero-fill: the feed overwrites every
+// byte it grows into, and leaving the first touch to the (parallel) writers
+// keeps page faults off one thread.
+template <typename T> struct DefaultInitAlloc : std::allocator<T> {
+    template <typename U> struct rebind { using other = DefaultInitAlloc<U>; };
+    DefaultInitAlloc() = default;
+    template <typename U> DefaultInitAlloc(const DefaultInitAlloc<U> &) noexcept {}
+    template <typename U> void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <typename U, typename... A> void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, DefaultInitAlloc<uint8_t>>;
+
+// Host worker threads for the feed (parse, normalise, (de)compress, format):
+// OKM_HOST_THREADS, else OMP_NUM_THREADS, else the hardware's, capped at 16.
+int host_threads();
+
+// Run f(i) for i in [0, n) on up to host_threads() threads (dynamic).
+template <typename F> void parallel_for(size_t n, F &&f) {
+    const size_t nt = std::min<size_t>(n, (size_t)host_threads());
+    if (nt <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> ts;
+    ts.reserve(nt);
+    for (size_t t = 0; t < nt; ++t)
+        ts.emplace_back([&]() {
+            for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+        });
+    for (auto &th : ts) th.join();
+}
+
 std::string lower_extension(const std::string &path);
-okm_status read_whole_file(const std::string &path, std::vector<uint8_t> &data);
+okm_status read_whole_file(const std::string &path, Bytes &data);
 // utils.rs:125-152: .gz/.xz/.zst/.zstd by lower-cased last extension.
-okm_status decompress_by_extension(const std::string &path, std::vector<uint8_t> &data);
+okm_status decompress_by_extension(const std::string &path, Bytes &data);
 // needletail 0.5.1 sniffing: gzip / bzip2 / xz magic bytes.
-okm_status sniff_decompress(std::vector<uint8_t> &data);
+okm_status sniff_decompress(Bytes &data);
 size_t format_counts_tsv(uint8_t k, const uint64_t *keys, const uint64_t *counts, size_t n, std::string &out);
 
 // utils.rs:167-198 get_output_writer: compressor chosen by extension.
@@ -24,6 +65,8 @@ class OutWriter {
     ~OutWriter();
     okm_status open(const std::string &path);
     okm_status write(const void *data, size_t n);
+    // Several blocks at once (.gz: compressed in parallel, one member each).
+    okm_status write_blocks(const std::vector<std::pair<const uint8_t *, size_t>> &blocks);
     okm_status close();
 
   private:
