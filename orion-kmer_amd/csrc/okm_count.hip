@@ -561,7 +561,11 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         PMARK(0);
         const DevItem it = items[item];
-        const uint64_t total = item_total(it, segs);
+        const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
+        if (total == 0) {  // an empty fan-out slot (block-uniform)
+            if (t == 0) n_out[item] = 0;
+            continue;
+        }
         uint32_t written = kDeferred;
         if (it.rem_bits > (uint32_t)kDenseBits && total <= (uint64_t)kCapI) {
             ull kk[kPer];
@@ -601,8 +605,12 @@ __global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ 
     for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
         const uint32_t item = defer ? defer[j] : j;
         const DevItem it = items[item];
-        const uint64_t total = item_total(it, segs);
+        const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
         uint32_t written = 0;
+        if (total == 0) {  // an empty fan-out slot (block-uniform)
+            if (threadIdx.x == 0) n_out[item] = 0;
+            continue;
+        }
         if (it.rem_bits <= (uint32_t)kDenseBits) {
             written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum);
         } else if (total <= (uint64_t)kCapI) {
@@ -630,7 +638,7 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
     if (wide) {  // every item through the full / dense modes
-        const uint32_t grid = nitems < 4096u ? nitems : 4096u;
+        const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                                out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
@@ -639,8 +647,8 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                                out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
         return;
     }
-    const uint32_t grid = nitems < 4096u ? nitems : 4096u;
-    const uint32_t sgrid = nitems < 1024u ? nitems : 1024u;  // exits at once when nothing was deferred
+    const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
+    const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
         hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer, guard);

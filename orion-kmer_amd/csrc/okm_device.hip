@@ -76,7 +76,8 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
                                                     const uint64_t *__restrict__ lk,
                                                     const uint64_t *__restrict__ lc, DevItem *__restrict__ items,
                                                     DevSeg *__restrict__ segs, uint64_t item_max,
-                                                    uint32_t capbits, ull *__restrict__ flags, uint32_t kw) {
+                                                    uint32_t capbits, ull *__restrict__ flags, uint32_t kw,
+                                                    FanOut fan) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nout) return;
     // parent = last part whose first output bin is <= i
@@ -87,34 +88,187 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     }
     const uint32_t rem = parents[lo].rem;
     const ull o = offs[i], len = (ends ? ends[i] : offs[i + 1]) - o;
-    DevSeg s;
-    s.keys = lk + o * kw;
-    s.counts = lc ? lc + o : nullptr;
-    s.len = len;
-    s.key_base = 0;
-    s.out_base = 0;
-    s.shift = kSingleBin;
-    s.nlocal = 1;
-    s.pad = 0;
-    segs[i] = s;
-    DevItem it;
-    it.seg_begin = i;
-    it.seg_count = 1;
-    it.out_off = o;  // distinct <= instances: the bin's own range is a safe output slot
-    it.rem_bits = rem;
-    it.pad = 0;
-    items[i] = it;
-    if (len > item_max && rem > capbits) atomicAdd(&flags[0], 1ull);
+    const uint32_t F = 1u << fan.bits;  // item slots per child (in key order)
+    uint32_t b = 0;                     // this child's own fan-out
+    if (len > item_max && rem > capbits) {
+        if (fan.bits && len <= fan.split_max) {
+            b = 1;
+            while (b < fan.bits && b < rem && (len >> b) > fan.target) ++b;
+        } else {
+            atomicAdd(&flags[0], 1ull);  // still too big: the host plans another round
+        }
+    }
     if (len >= (1ull << 32)) atomicOr(&flags[1], 2ull);  // u32 LDS counts could overflow: count weighted
-    atomicMax(&flags[2], len);
+    for (uint32_t j = 0; j < F; ++j) {
+        if (b && j < (1u << b)) continue;  // written by k_fan_split
+        DevSeg s;
+        s.keys = lk + o * kw;
+        s.counts = lc ? lc + o : nullptr;
+        s.len = j == 0 ? len : 0;  // slots past the child's own are empty items
+        s.key_base = 0;
+        s.out_base = 0;
+        s.shift = kSingleBin;
+        s.nlocal = 1;
+        s.pad = 0;
+        segs[(uint64_t)i * F + j] = s;
+        DevItem it;
+        it.seg_begin = i * F + j;
+        it.seg_count = 1;
+        it.out_off = o;  // distinct <= instances: the bin's own range is a safe output slot
+        it.rem_bits = rem;
+        it.pad = j == 0 ? 0u : kItemEmpty;
+        items[(uint64_t)i * F + j] = it;
+    }
+    if (b) {
+        const ull jb = atomicAdd(&flags[3], 1ull);
+        fan.jobs[jb] = DevFanJob{o, len, i * F, b, rem, 0};
+    } else {
+        atomicMax(&flags[2], len);
+    }
 }
 
 void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t nout, const DevParent *parents,
                        uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
-                       uint64_t item_max, uint32_t capbits, ull *flags, uint32_t kw) {
+                       uint64_t item_max, uint32_t capbits, ull *flags, uint32_t kw, const FanOut &fan) {
     if (!nout) return;
     hipLaunchKernelGGL(k_make_items, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, offs, ends, nout,
-                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw);
+                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw, fan);
+}
+
+// Fan-out split of one oversized child per job: its keys (<= kFanBlock *
+// kFanPer, held in registers) are counting-sorted by the next `bits` key bits
+// into the same index range of `dk` (order inside a sub-range is free: items
+// are multisets), and each sub-range becomes the item slot item0 + j.  Ranks
+// come from wave ballots (no LDS atomics on the 2..8 counters).
+constexpr int kFanBlock = 1024;
+constexpr int kFanPer = 16;
+constexpr int kFanWaves = kFanBlock / 64;
+uint64_t fan_split_max() { return (uint64_t)kFanBlock * kFanPer; }
+
+template <typename KT, bool W>
+__global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__restrict__ jobs,
+                                                         const ull *__restrict__ flags, const KT *__restrict__ sk,
+                                                         const uint64_t *__restrict__ sc, KT *__restrict__ dk,
+                                                         uint64_t *__restrict__ dc, DevItem *__restrict__ items,
+                                                         DevSeg *__restrict__ segs, uint64_t item_max,
+                                                         uint32_t capbits, ull *__restrict__ oflags) {
+    __shared__ uint32_t wtot[kFanWaves][8];
+    __shared__ uint32_t btot[8], bbase[8];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
+    for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
+        const DevFanJob jb = jobs[jx];
+        const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
+        uint32_t br[kFanPer];  // bin << 16 | rank within (wave, bin); ~0 = none
+        uint32_t run[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform running counts per bin
+        const ull lt = (1ull << lane) - 1ull;
+        // pass 1: bins and ranks (keys are read again below, from L2: a job's
+        // range is <= 256 KiB, and keeping them in registers would spill)
+        const uint32_t rows = (uint32_t)((jb.len + kFanBlock - 1) / kFanBlock);  // block-uniform
+#pragma unroll
+        for (int u = 0; u < kFanPer; ++u) {
+            br[u] = ~0u;
+            if ((uint32_t)u >= rows) continue;
+            const uint64_t idx = (uint64_t)u * kFanBlock + t;
+            const KT key = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+            const bool v = !KeyOps<KT>::is_empty(key);
+            const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(key, shift) & (nb - 1)) : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                if (q >= nb) break;
+                const ull m = __ballot(v && b == q);
+                if (v && b == q) br[u] = (q << 16) | (run[q] + (uint32_t)__popcll(m & lt));
+                run[q] += (uint32_t)__popcll(m);
+            }
+        }
+        {
+            uint32_t mine = run[0];  // lane q publishes the wave's count of bin q (no dynamic register index)
+#pragma unroll
+            for (uint32_t z = 1; z < 8; ++z) mine = lane == z ? run[z] : mine;
+            if (lane < 8) wtot[wv][lane] = lane < nb ? mine : 0u;
+        }
+        __syncthreads();
+        if (t < nb) {
+            uint32_t s = 0;
+            for (int w = 0; w < kFanWaves; ++w) s += wtot[w][t];
+            btot[t] = s;
+        }
+        __syncthreads();
+        if (t < nb) {
+            uint32_t a = 0;
+            for (uint32_t q = 0; q < t; ++q) a += btot[q];
+            bbase[t] = a;
+            const ull o = jb.off + a, len = btot[t];
+            DevSeg s;
+            s.keys = reinterpret_cast<const uint64_t *>(dk + o);
+            s.counts = W ? dc + o : nullptr;
+            s.len = len;
+            s.key_base = 0;
+            s.out_base = 0;
+            s.shift = kSingleBin;
+            s.nlocal = 1;
+            s.pad = 0;
+            segs[jb.item0 + t] = s;
+            DevItem it;
+            it.seg_begin = jb.item0 + t;
+            it.seg_count = 1;
+            it.out_off = o;
+            it.rem_bits = jb.rem - jb.bits;
+            it.pad = len ? 0u : kItemEmpty;
+            items[jb.item0 + t] = it;
+            if (len > item_max && it.rem_bits > capbits) atomicAdd(&oflags[0], 1ull);
+            atomicMax(&oflags[2], len);
+        }
+        // this wave's start in each bin: the bin's base + the earlier waves' counts
+        __syncthreads();
+        uint32_t wb[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            uint32_t a = q < nb ? bbase[q] : 0u;
+            for (uint32_t w = 0; w < wv; ++w) a += q < nb ? wtot[w][q] : 0u;
+            wb[q] = a;
+        }
+#pragma unroll
+        for (int u = 0; u < kFanPer; ++u) {
+            if (br[u] == ~0u) continue;
+            const uint64_t idx = (uint64_t)u * kFanBlock + t;
+            const uint32_t q = br[u] >> 16;
+            uint32_t base = wb[0];
+#pragma unroll
+            for (uint32_t z = 1; z < 8; ++z) base = q == z ? wb[z] : base;
+            const ull o = jb.off + base + (br[u] & 0xFFFFu);
+            dk[o] = sk[jb.off + idx];
+            if (W) dc[o] = sc ? sc[jb.off + idx] : 1ull;
+        }
+        __syncthreads();  // wtot / bbase reuse by the next job
+    }
+}
+
+void launch_fan_split(void *stream, const DevFanJob *jobs, uint32_t max_jobs, const ull *flags, const uint64_t *sk,
+                      const uint64_t *sc, uint64_t *dk, uint64_t *dc, DevItem *items, DevSeg *segs,
+                      uint64_t item_max, uint32_t capbits, ull *oflags, bool wide) {
+    if (!max_jobs) return;
+    const dim3 g(max_jobs < 2048u ? max_jobs : 2048u), b(kFanBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (wide) {
+        const K128 *a = reinterpret_cast<const K128 *>(sk);
+        K128 *d = reinterpret_cast<K128 *>(dk);
+        if (sc)
+            hipLaunchKernelGGL((k_fan_split<K128, true>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
+                               item_max, capbits, oflags);
+        else
+            hipLaunchKernelGGL((k_fan_split<K128, false>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
+                               item_max, capbits, oflags);
+    } else {
+        const ull *a = reinterpret_cast<const ull *>(sk);
+        ull *d = reinterpret_cast<ull *>(dk);
+        if (sc)
+            hipLaunchKernelGGL((k_fan_split<ull, true>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
+                               item_max, capbits, oflags);
+        else
+            hipLaunchKernelGGL((k_fan_split<ull, false>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
+                               item_max, capbits, oflags);
+    }
 }
 
 // Sampled partition capacities: the slot of bin b gets scale * (sqrt(s) + 3)^2
@@ -283,7 +437,7 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
                           const unsigned long long *err) {
     if (!nitems) return;
-    const dim3 g(nitems < 8192u ? nitems : 8192u), b(256);
+    const dim3 g(nitems < 8191u ? nitems : 8191u), b(256);  // odd: fan-out slots spread over blocks
     hipStream_t s = (hipStream_t)stream;
     const K128 *sk2 = reinterpret_cast<const K128 *>(src_keys);
     K128 *dk2 = reinterpret_cast<K128 *>(dst_keys);

@@ -1039,7 +1039,9 @@ static okm_status do_count(okm_ctx *c) {
                                                        // gradients and line padding must still fit)
     bool weighted = false;
     for (auto &r : c->runs) weighted |= (r.counts != nullptr);
-    const uint32_t maxb = log2_floor(part_max_bins(weighted));  // bits one pass can split
+    uint32_t maxb = log2_floor(part_max_bins(weighted));  // bits one pass can split
+    if (const char *e = getenv("OKM_PART_MAXB"))                // tests: force small passes (fan-out, host rounds)
+        maxb = std::max(1, std::min((int)maxb, atoi(e)));
     c->hprof.mark("pre_count");
 
     // initial parts: the L1 bins, each a list of per-run segments
@@ -1095,6 +1097,31 @@ static okm_status do_count(okm_ctx *c) {
         }
         if (any) {
             c->info.l2_bits = *std::max_element(bits.begin(), bits.end());
+            // Fan-out: when the pass cannot bring some parts' children down to
+            // one item (the bits it can split are capped), every child gets
+            // 2^fan item slots and an oversized child is split once more in
+            // place on the device (k_fan_split) -- no host round.  Sized for
+            // twice the average child of the biggest part (canonical keys are
+            // not uniform inside a part).
+            FanOut fan;
+            {
+                static const int fan_env = [] {
+                    const char *e = getenv("OKM_FAN_BITS");
+                    return e ? atoi(e) : -1;
+                }();
+                uint32_t fb = 0;
+                for (uint32_t i = 0; i < parts.size(); ++i) {
+                    const uint64_t child = 2 * (parts[i].len >> bits[i]);
+                    if (!bits[i] || (parts[i].len >> bits[i]) <= target) continue;
+                    uint32_t f = 1;
+                    while (f < 3 && (child >> f) > target) ++f;
+                    fb = std::max(fb, f);
+                }
+                if (fan_env >= 0) fb = std::min<uint32_t>(fb, (uint32_t)fan_env);
+                fan.bits = fb;
+                fan.target = target;
+                fan.split_max = fan_split_max();
+            }
             c->hprof.mark("split.plan");
             uint64_t keys_in = 0;
             for (const Part &p : parts) keys_in += p.len;
@@ -1103,10 +1130,11 @@ static okm_status do_count(okm_ctx *c) {
             // (speculatively: the count kernels check make_items' flags), so
             // the first host sync of the round comes after the compaction.
             for (int attempt = 0;; ++attempt) {
-                unsigned long long *flags;  // [0] children too big, [1] 1: slot overflow | 2: 64-bit counts, [2] max
-                OKM_TRY(pool_get(c->pool, 3, &flags));
+                unsigned long long *flags;  // [0] children too big, [1] 1: slot overflow | 2: 64-bit counts, [2] max,
+                                            // [3] fan-out jobs
+                OKM_TRY(pool_get(c->pool, 4, &flags));
                 level_bufs.push_back(flags);
-                HIP_TRY(hipMemsetAsync(flags, 0, 3 * sizeof(unsigned long long), c->stream));
+                HIP_TRY(hipMemsetAsync(flags, 0, 4 * sizeof(unsigned long long), c->stream));
                 Level L;
                 OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L,
                                      try_sampled && !attempt ? flags + 1 : nullptr));
@@ -1115,18 +1143,37 @@ static okm_status do_count(okm_ctx *c) {
                     par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
                 DevParent *d_par;
                 OKM_TRY(pool_get(c->pool, par.size(), &d_par));
-                OKM_TRY(pool_get(c->pool, L.nout, &d_items));
-                OKM_TRY(pool_get(c->pool, L.nout, &d_segs));
+                const uint32_t nslots = L.nout << fan.bits;
+                OKM_TRY(pool_get(c->pool, nslots, &d_items));
+                OKM_TRY(pool_get(c->pool, nslots, &d_segs));
                 level_bufs.push_back(d_par);
+                if (fan.bits) {
+                    OKM_TRY(pool_get(c->pool, L.nout, &fan.jobs));
+                    level_bufs.push_back(fan.jobs);
+                }
                 OKM_TRY(h2d(c, d_par, par.data(), par.size() * sizeof(DevParent)));
                 launch_make_items(c->stream, L.d_offs, L.d_ends, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc,
-                                  d_items, d_segs, item_max, capbits, flags, c->kw);
+                                  d_items, d_segs, item_max, capbits, flags, c->kw, fan);
                 HIP_TRY(hipGetLastError());
+                if (fan.bits) {  // oversized children split into a second level array (same offsets)
+                    uint64_t *fk, *fc = nullptr;
+                    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &fk));
+                    level_bufs.push_back(fk);
+                    if (L.lc) {
+                        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &fc));
+                        level_bufs.push_back(fc);
+                    }
+                    c->timer.begin(c->stream);
+                    launch_fan_split(c->stream, fan.jobs, L.nout, flags, L.lk, L.lc, fk, fc, d_items, d_segs, item_max,
+                                     capbits, flags, c->wide);
+                    c->timer.end(c->stream, "fan_split", 0.0);
+                    HIP_TRY(hipGetLastError());
+                }
                 c->hprof.mark("split.round_launch");
-                c->info.work_items = L.nout;
+                c->info.work_items = nslots;
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
-                OKM_TRY(count_and_compact(c, d_items, d_segs, L.nout, L.padded, L.total, weighted, level_bufs, flags,
+                OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.padded, L.total, weighted, level_bufs, flags,
                                           hf, &aborted));
                 if (!aborted) {
                     c->info.max_partition = hf[2];

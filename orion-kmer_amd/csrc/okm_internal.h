@@ -46,12 +46,14 @@ struct DevChunk {
 };
 
 // One partition to count in LDS: segs[seg_begin, seg_begin + seg_count).
+constexpr uint32_t kItemEmpty = 1;
+
 struct DevItem {
     uint32_t seg_begin;
     uint32_t seg_count;
     uint64_t out_off;        // where its sorted distinct entries go (scratch)
     uint32_t rem_bits;       // key bits below the item's common prefix
-    uint32_t pad;
+    uint32_t pad;            // kItemEmpty: an empty fan-out slot (no segment read)
 };
 
 // Sampled L1 placement: bin b's claim cursor lives at cursor[b * OKM_L1_CUR_STRIDE]
@@ -140,16 +142,40 @@ struct DevParent {
     uint32_t rem;            // key bits below the children's common prefix
 };
 
+// Fan-out of a round's children (k_fan_split): a child larger than one item
+// (but <= split_max) is split in place by its next 1..bits key bits (the
+// fewest that bring it to <= target); every child owns 2^bits item slots in
+// key order, slots past its own sub-ranges are empty items.
+struct DevFanJob {
+    uint64_t off, len;
+    uint32_t item0, bits, rem, pad;
+};
+struct FanOut {
+    uint32_t bits = 0;          // 0: one item per child (no fan-out)
+    uint32_t pad = 0;
+    uint64_t target = 0;        // sub-range size aimed at
+    uint64_t split_max = 0;     // largest child one job takes (fan_split_max())
+    DevFanJob *jobs = nullptr;  // [nout]; job count in flags[3]
+};
+uint64_t fan_split_max();
+
 // One item (and one segment) per output bin of a split round, straight from
 // the device offsets (nout + 1 entries; bin b ends at ends[b], or at
 // offs[b + 1] when ends is null).  flags[0] += children that are still too
 // big for one item; flags[1] |= 2 when a child needs 64-bit counting;
-// flags[2] = max child length.  Count and compact kernels given `guard`
-// (= flags) return at once when guard[0] or guard[1] is set.
+// flags[2] = max child length; flags[3] = fan-out jobs.  Count and compact
+// kernels given `guard` (= flags) return at once when guard[0] or guard[1] is
+// set.  With fan.bits, item/segment slot i * 2^bits + j belongs to child i.
 void launch_make_items(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
                        const DevParent *parents, uint32_t nparents, const uint64_t *lk, const uint64_t *lc,
                        DevItem *items, DevSeg *segs, uint64_t item_max, uint32_t capbits,
-                       unsigned long long *flags, uint32_t kw);
+                       unsigned long long *flags, uint32_t kw, const FanOut &fan);
+// The fan-out jobs (flags[3] of them, <= max_jobs): keys of [off, off + len)
+// of sk/sc are split into the same range of dk/dc and their sub-items written;
+// oflags[0] += sub-ranges still too big, oflags[2] = max sub-range.
+void launch_fan_split(void *stream, const DevFanJob *jobs, uint32_t max_jobs, const unsigned long long *flags,
+                      const uint64_t *sk, const uint64_t *sc, uint64_t *dk, uint64_t *dc, DevItem *items,
+                      DevSeg *segs, uint64_t item_max, uint32_t capbits, unsigned long long *oflags, bool wide);
 
 // Sorted runs (okm_add_sorted_pairs_device).  out[b] = first index whose
 // (key >> shift) >= b, b = 0..nbins (out[nbins] = n).

@@ -467,3 +467,50 @@ def test_sampled_l1_placement_wide():
     ek, ec = oc.result(1)
     assert np.array_equal(gk.reshape(-1, 2), ek) and np.array_equal(gc, ec)
     assert stats["extract_sample"]["launches"] == 1 and "extract_hist" not in stats
+
+
+@pytest.mark.parametrize("k,wide", [(31, False), (21, False), (63, True), (45, True)])
+def test_fan_out_split(k, wide, monkeypatch):
+    # OKM_PART_MAXB caps a partition pass at 3 bits, so a 7 M-key batch leaves
+    # children of ~4-16 Ki keys: each child gets 2^f item slots and the
+    # oversized ones are split once more in place on the device (k_fan_split)
+    # instead of a host-planned second round (levels stays 1).  The weighted
+    # variant: the same table re-added as (key, count) pairs.
+    from oracle import OracleCounterWide
+    monkeypatch.setenv("OKM_PART_MAXB", "3")
+    batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=7, seed=k, sub_rate=0.01,
+                            n_rate=0.001)
+    gk, gc, stats, info = _count_device(batch, k, wide=wide)
+    oc = OracleCounterWide(k) if wide else OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    if wide:
+        gk = gk.reshape(-1, 2)
+    assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert "fan_split" in stats and info["levels"] == 1, (stats.keys(), info)
+    with okm.KmerCounter(k, wide=wide) as m:
+        m.set_timing(True)
+        m.add_pairs(gk, gc)
+        m.add_pairs(gk[::3], gc[::3])
+        mk, mc = m.result(1)
+        mstats = m.kernel_stats()
+    ec2 = ec.copy()
+    ec2[::3] *= 2
+    if wide:
+        mk = mk.reshape(-1, 2)
+    assert np.array_equal(mk, ek) and np.array_equal(mc, ec2)
+    assert "fan_split" in mstats
+
+
+def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
+    # a 2-bit pass cap leaves children too big for one fan-out job: the
+    # speculative count is abandoned and the host plans further rounds
+    monkeypatch.setenv("OKM_PART_MAXB", "1")
+    k = 31
+    batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=8, seed=3, sub_rate=0.01)
+    gk, gc, stats, info = _count_device(batch, k)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["levels"] >= 2

@@ -1,0 +1,26 @@
+#!/bin/bash
+# End-to-end CLI wall time on the C2 input (host parse + H2D + count + TSV
+# write), reported beside bench.py's device-resident number (SURVEY §8(d)
+# "End-to-end ... reported separately").  Inputs live in /tmp on the box.
+set -eo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+CLI=$ROOT/orion-kmer_amd/build/orion-kmer
+D=${TMPDIR:-/tmp}/okm_e2e
+mkdir -p "$D"
+python3 "$ROOT/tools/make_c2_fastq.py" "$D/c2.fastq"
+gzip -1 -c "$D/c2.fastq" > "$D/c2.fastq.gz"
+ls -la "$D"
+TIMEFORMAT="e2e %R s"
+run() {
+    echo "== $*"
+    time timeout -k 10 300 "$CLI" "$@"
+}
+cat "$D/c2.fastq" > /dev/null
+run count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv"
+run count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv"
+run count -k 31 -i "$D/c2.fastq" -o "$D/out2.tsv" -m 2
+run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out.tsv.gz"
+run -v count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv"
+wc -l "$D/out.tsv" "$D/out2.tsv"
+cmp "$D/out.tsv" <(zcat "$D/out.tsv.gz") && echo "gz output identical"
+rm -rf "$D"
