@@ -35,6 +35,9 @@ namespace okm {
 #ifndef OKM_COUNT_WPE
 #define OKM_COUNT_WPE 8  // waves per EU floor of the unweighted kernel: 4 blocks/CU (64 VGPRs)
 #endif
+#ifndef OKM_COUNT_PREFETCH  // full/dense kernel: load the next item's keys during this one
+#define OKM_COUNT_PREFETCH 1
+#endif
 #ifndef OKM_COUNT_PROF
 #define OKM_COUNT_PROF 0
 #endif
@@ -196,18 +199,6 @@ __device__ __forceinline__ void slice_sort(KT *sk, ull *sw, uint32_t a, uint32_t
     }
 }
 
-template <typename KT>
-__device__ __forceinline__ uint32_t slice_distinct(const KT *sk, uint32_t a, uint32_t n) {
-    uint32_t d = 0;
-    KT prev = KeyOps<KT>::empty();
-    for (uint32_t i = a; i < a + n; ++i) {
-        const KT x = sk[i];
-        d += KeyOps<KT>::eq(x, prev) ? 0u : 1u;
-        prev = x;
-    }
-    return d;
-}
-
 // Tag-mode LDS state between items: all tags empty, all counters zero.
 template <bool W>
 __device__ __forceinline__ void tag_reset(ull *lds) {
@@ -223,19 +214,17 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 // ---------------------------------------------------------------------------
 
 template <bool W, typename KT>
-__device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
-                                              ull *lds, uint32_t *wsum, uint64_t *__restrict__ out_keys_raw,
-                                              uint64_t *__restrict__ out_counts) {
+__device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
+                                              const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
+                                              uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts) {
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
     KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
-    KT kk[kPer];
-    ull ww[kPer];
-    load_item<W, KT>(it, segs, kk, ww);
     KT *sk = reinterpret_cast<KT *>(lds);
     ull *sw = reinterpret_cast<ull *>(sk + kCapI);
     uint32_t *hc = reinterpret_cast<uint32_t *>(sw + (W ? kCapI : 0));
+    uint16_t *first = reinterpret_cast<uint16_t *>(hc + kHomes / 2);  // [D + 1]: run starts in sk
     __syncthreads();  // the previous item's LDS state is dead
     hc[2 * t] = 0;
     hc[2 * t + 1] = 0;
@@ -260,6 +249,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
     hc[2 * t] = a | ((a + c0) << 16);
     hc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
     __syncthreads();
+    PMARK(11);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         if ((uint32_t)u >= nrows) break;
@@ -271,23 +261,52 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, const DevSeg *_
         }
     }
     __syncthreads();
+    PMARK(12);
+    // each thread's 4 homes are one slice of sk: sort it and flag the first
+    // key of every run (count.rs:33: a key's count = its run's length/weight);
+    // the flags of the dead home counters' bytes (hc) are then compacted into
+    // run starts by the whole block, so the emit below is coalesced
     slice_sort<W>(sk, sw, a, n);
-    const uint32_t d = slice_distinct(sk, a, n);
-    uint32_t D;
-    const uint32_t od = block_excl_scan32(d, wsum, &D);
-    uint64_t o = out_off + od;  // DashMap value = instances (count.rs:33)
-    uint32_t i = a;
-    while (i < a + n) {
-        const KT key = sk[i];
-        ull c = 0;
-        do {
-            c += W ? sw[i] : 1ull;
-            ++i;
-        } while (i < a + n && KeyOps<KT>::eq(sk[i], key));
-        out_keys[o] = key;
-        store_count<W>(out_counts, o, c);
-        ++o;
+    PMARK(13);
+    uint8_t *rf = reinterpret_cast<uint8_t *>(hc);  // [kCapI] run-start flags
+    {
+        KT prev = KeyOps<KT>::empty();
+        for (uint32_t i = a; i < a + n; ++i) {
+            const KT x = sk[i];
+            rf[i] = KeyOps<KT>::eq(x, prev) ? 0 : 1;
+            prev = x;
+        }
     }
+    __syncthreads();
+    uint32_t D;
+    {
+        constexpr int kPerT = kCapI / kCB;  // 8 positions per thread
+        static_assert(kPerT == 8, "two flag words per thread");
+        const uint32_t p0 = t * kPerT;
+        const uint32_t *rw = reinterpret_cast<const uint32_t *>(rf);
+        const uint64_t fw = (uint64_t)rw[2 * t] | ((uint64_t)rw[2 * t + 1] << 32);
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < kPerT; ++j) m |= ((fw >> (8 * j)) & 1u) && p0 + j < ntot ? 1u << j : 0u;
+        uint32_t q = block_excl_scan32((uint32_t)__builtin_popcount(m), wsum, &D);
+#pragma unroll
+        for (int j = 0; j < kPerT; ++j)
+            if (m & (1u << j)) first[q++] = (uint16_t)(p0 + j);
+        if (t == 0) first[D] = (uint16_t)ntot;  // ntot <= kCapI fits u16
+    }
+    __syncthreads();
+    PMARK(14);
+    for (uint32_t p = t; p < D; p += kCB) {
+        const uint32_t b = first[p], e = first[p + 1];
+        out_keys[out_off + p] = sk[b];
+        ull c = 0;
+        if (W)
+            for (uint32_t i = b; i < e; ++i) c += sw[i];
+        else
+            c = e - b;
+        store_count<W>(out_counts, out_off + p, c);
+    }
+    PMARK(15);
     return __builtin_amdgcn_readfirstlane(D);
 }
 
@@ -549,8 +568,10 @@ template <bool W>
 __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM_COUNT_WPE)))
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
-                   ull *__restrict__ ctl, uint32_t *__restrict__ defer, const ull *__restrict__ guard) {
+                   ull *__restrict__ ctl, uint32_t *__restrict__ defer, const ull *__restrict__ guard,
+                   const ull *__restrict__ d_nitems) {
     if (guard && (guard[0] | guard[1])) return;  // speculative launch whose items were not valid
+    if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     const uint32_t t = threadIdx.x;
@@ -589,23 +610,70 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
 // item (defer == nullptr: wide keys, which have no tag mode — LDS has no
 // 128-bit CAS): dense mode, or full mode (every instance counting-sorted).
 template <typename KT, bool W>
-__global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ items, uint32_t nitems,
+__global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeof(KT) > 8) ? 1 : 4))) void k_count_slow(const DevItem *__restrict__ items, uint32_t nitems,
                                                     const DevSeg *__restrict__ segs,
                                                     uint64_t *__restrict__ out_keys,
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                                                     ull *__restrict__ ctl, const uint32_t *__restrict__ defer,
-                                                    const ull *__restrict__ guard) {
+                                                    const ull *__restrict__ guard, const ull *__restrict__ d_nitems) {
     if (guard && (guard[0] | guard[1])) return;
-    constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2;
+    if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
+    constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2 + (kCapI + 16) * 2;
     constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
     constexpr int kBytes = kFull > kDense ? kFull : kDense;
     __shared__ __attribute__((aligned(16))) ull lds[kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     const uint32_t ndefer = defer ? *reinterpret_cast<volatile const unsigned int *>(ctl + 1) : nitems;
-    for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
-        const uint32_t item = defer ? defer[j] : j;
-        const DevItem it = items[item];
-        const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
+    if (OKM_COUNT_PROF && threadIdx.x == 0) g_prof_last = clock64();
+    // Unweighted: the next item's keys are loaded while this one is counted
+    // (the kernel is LDS-bound to 2 workgroups per CU, so the registers are
+    // free); weighted items load in place.
+    constexpr bool kPre = !W && OKM_COUNT_PREFETCH;
+    struct Next {
+        uint32_t item;
+        DevItem it;
+        uint64_t total;
+    };
+    auto fetch_meta = [&](uint32_t jj, Next &nx) {
+        nx.item = defer ? defer[jj] : jj;
+        nx.it = items[nx.item];
+        nx.total = nx.it.pad == kItemEmpty ? 0 : item_total(nx.it, segs);
+    };
+    auto is_full = [](const Next &nx) {
+        return nx.total != 0 && nx.it.rem_bits > (uint32_t)kDenseBits && nx.total <= (uint64_t)kCapI;
+    };
+    KT kn[kPer];
+    ull wn[kPer];
+    Next nx{};
+    uint32_t j = blockIdx.x;
+    if (kPre && j < ndefer) {
+        fetch_meta(j, nx);
+        if (is_full(nx)) load_item<W, KT>(nx.it, segs, kn, wn);
+    }
+    for (; j < ndefer; j += gridDim.x) {
+        Next cur;
+        KT kk[kPer];
+        ull ww[kPer];
+        if (kPre) {
+            cur = nx;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                kk[u] = kn[u];
+                ww[u] = 1;
+            }
+            const uint32_t jn = j + gridDim.x;
+            if (jn < ndefer) {
+                fetch_meta(jn, nx);
+                if (is_full(nx)) load_item<W, KT>(nx.it, segs, kn, wn);
+            }
+        } else {
+            fetch_meta(j, cur);
+            if (is_full(cur)) load_item<W, KT>(cur.it, segs, kk, ww);
+        }
+        PMARK(10);
+        const uint32_t item = cur.item;
+        const DevItem it = cur.it;
+        const uint64_t total = cur.total;
         uint32_t written = 0;
         if (total == 0) {  // an empty fan-out slot (block-uniform)
             if (threadIdx.x == 0) n_out[item] = 0;
@@ -614,7 +682,7 @@ __global__ __launch_bounds__(kCB) void k_count_slow(const DevItem *__restrict__ 
         if (it.rem_bits <= (uint32_t)kDenseBits) {
             written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum);
         } else if (total <= (uint64_t)kCapI) {
-            written = full_item<W, KT>(it, segs, (uint32_t)((total + kCB - 1) / kCB), lds, wsum, out_keys,
+            written = full_item<W, KT>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
                                        out_counts);
         } else if (threadIdx.x == 0) {
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
@@ -634,31 +702,31 @@ void count_prof_read(unsigned long long *out16) {
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
-                        const unsigned long long *guard) {
+                        const unsigned long long *guard, const unsigned long long *d_nitems) {
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
     if (wide) {  // every item through the full / dense modes
         const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems);
         else
             hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard);
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems);
         return;
     }
     const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
     const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
         hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer, guard);
+                           out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer, guard);
+                           out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems);
     }
 }
 

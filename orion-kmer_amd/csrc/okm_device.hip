@@ -420,8 +420,10 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
                                                        KT *__restrict__ dk,
                                                        uint64_t *__restrict__ dc,
                                                        const ull *__restrict__ guard,
-                                                       const ull *__restrict__ err) {
+                                                       const ull *__restrict__ err,
+                                                       const ull *__restrict__ d_nitems) {
     if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
+    if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
         for (uint64_t j = threadIdx.x; j < n; j += 256) {
@@ -435,7 +437,7 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts, uint64_t *dst_keys,
                           uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
-                          const unsigned long long *err) {
+                          const unsigned long long *err, const unsigned long long *d_nitems) {
     if (!nitems) return;
     const dim3 g(nitems < 8191u ? nitems : 8191u), b(256);  // odd: fan-out slots spread over blocks
     hipStream_t s = (hipStream_t)stream;
@@ -445,16 +447,36 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
     ull *dk1 = reinterpret_cast<ull *>(dst_keys);
     if (wide && narrow)
         hipLaunchKernelGGL((k_compact_items<K128, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk2, src_counts,
-                           dk2, dst_counts, guard, err);
+                           dk2, dst_counts, guard, err, d_nitems);
     else if (wide)
         hipLaunchKernelGGL((k_compact_items<K128, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk2,
-                           src_counts, dk2, dst_counts, guard, err);
+                           src_counts, dk2, dst_counts, guard, err, d_nitems);
     else if (narrow)
         hipLaunchKernelGGL((k_compact_items<ull, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk1, src_counts,
-                           dk1, dst_counts, guard, err);
+                           dk1, dst_counts, guard, err, d_nitems);
     else
         hipLaunchKernelGGL((k_compact_items<ull, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk1,
-                           src_counts, dk1, dst_counts, guard, err);
+                           src_counts, dk1, dst_counts, guard, err, d_nitems);
+}
+
+__global__ __launch_bounds__(256) void k_item_flags(const DevItem *__restrict__ items, uint32_t n,
+                                                    ull *__restrict__ flags) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i <= n) flags[i] = i < n && items[i].pad != kItemEmpty ? 1ull : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_item_scatter(const DevItem *__restrict__ items, uint32_t n,
+                                                      const ull *__restrict__ pos, DevItem *__restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n && pos[i + 1] != pos[i]) out[pos[i]] = items[i];
+}
+
+void launch_item_compact(void *stream, const DevItem *items, uint32_t nslots, DevItem *out, ull *flags, ull *pos,
+                         ull *scan_tmp) {
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_item_flags, dim3(nslots / 256 + 1), dim3(256), 0, s, items, nslots, flags);
+    launch_exclusive_scan(stream, flags, pos, (uint64_t)nslots + 1, scan_tmp);
+    if (nslots) hipLaunchKernelGGL(k_item_scatter, dim3((nslots + 255) / 256), dim3(256), 0, s, items, nslots, pos, out);
 }
 
 constexpr int kFilterBlock = 256;

@@ -787,7 +787,8 @@ static uint32_t log2_floor(uint64_t x) {
 static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems,
                                     uint64_t out_total, uint64_t in_total, bool weighted,
                                     std::vector<void *> &level_bufs, const unsigned long long *guard = nullptr,
-                                    unsigned long long *hguard = nullptr, bool *aborted = nullptr) {
+                                    unsigned long long *hguard = nullptr, bool *aborted = nullptr,
+                                    const unsigned long long *d_nitems = nullptr) {
     uint64_t *sk, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
@@ -802,10 +803,13 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             c->pool.put(p);
     };
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
+    // items past a device-side count (d_nitems) must scan as empty
+    HIP_TRY(hipMemsetAsync(d_nitems ? n_out : n_out + nitems, 0,
+                           (d_nitems ? nitems + 1 : 1) * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard);
+    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
+                       d_nitems);
     c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
@@ -822,7 +826,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     if (one_pass) {
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, !weighted, guard,
-                             c->flag);
+                             c->flag, d_nitems);
         c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
         HIP_TRY(hipGetLastError());
     }
@@ -861,7 +865,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts,
-                             c->wide, !weighted);
+                             c->wide, !weighted, nullptr, nullptr, d_nitems);
         c->timer.end(c->stream, "compact_items", (staged + dense) * (double)nd);
         HIP_TRY(hipGetLastError());
         OKM_TRY(sync(c));
@@ -1144,6 +1148,7 @@ static okm_status do_count(okm_ctx *c) {
                 DevParent *d_par;
                 OKM_TRY(pool_get(c->pool, par.size(), &d_par));
                 const uint32_t nslots = L.nout << fan.bits;
+                const unsigned long long *d_nitems = nullptr;  // fan-out: items kept, on the device
                 OKM_TRY(pool_get(c->pool, nslots, &d_items));
                 OKM_TRY(pool_get(c->pool, nslots, &d_segs));
                 level_bufs.push_back(d_par);
@@ -1168,13 +1173,25 @@ static okm_status do_count(okm_ctx *c) {
                                      capbits, flags, c->wide);
                     c->timer.end(c->stream, "fan_split", 0.0);
                     HIP_TRY(hipGetLastError());
+                    // drop the empty slots, so the count kernels deal real items only
+                    DevItem *dense_items;
+                    unsigned long long *iflags, *ipos, *itmp;
+                    OKM_TRY(pool_get(c->pool, nslots, &dense_items));
+                    OKM_TRY(pool_get(c->pool, (size_t)nslots + 1, &iflags));
+                    OKM_TRY(pool_get(c->pool, (size_t)nslots + 1, &ipos));
+                    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nslots + 1), &itmp));
+                    for (void *p : {(void *)d_items, (void *)iflags, (void *)ipos, (void *)itmp}) level_bufs.push_back(p);
+                    launch_item_compact(c->stream, d_items, nslots, dense_items, iflags, ipos, itmp);
+                    HIP_TRY(hipGetLastError());
+                    d_items = dense_items;
+                    d_nitems = ipos + nslots;
                 }
                 c->hprof.mark("split.round_launch");
                 c->info.work_items = nslots;
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.padded, L.total, weighted, level_bufs, flags,
-                                          hf, &aborted));
+                                          hf, &aborted, d_nitems));
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;

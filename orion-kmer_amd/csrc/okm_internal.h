@@ -133,7 +133,7 @@ uint32_t count_dense_bits();
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
-                        const unsigned long long *guard = nullptr);
+                        const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr);
 
 // A part that took part in a device-side split round: its children are the
 // output bins [out_base, out_base + nlocal) of the round.
@@ -158,6 +158,9 @@ struct FanOut {
     DevFanJob *jobs = nullptr;  // [nout]; job count in flags[3]
 };
 uint64_t fan_split_max();
+
+// d_nitems (count kernels, compaction): when given, the item count is
+// min(nitems, *d_nitems) -- a count known only on the device.
 
 // One item (and one segment) per output bin of a split round, straight from
 // the device offsets (nout + 1 entries; bin b ends at ends[b], or at
@@ -203,7 +206,13 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts,
                           uint64_t *dst_keys, uint64_t *dst_counts, bool wide, bool narrow,
-                          const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr);
+                          const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr,
+                          const unsigned long long *d_nitems = nullptr);
+// Drop the empty fan-out slots of items[0, nslots) (order kept) into out;
+// *d_nitems (= pos[nslots]) receives the number kept.  flags/pos: nslots + 1
+// words each, scan_tmp: scan_tmp_elems(nslots + 1).
+void launch_item_compact(void *stream, const DevItem *items, uint32_t nslots, DevItem *out,
+                         unsigned long long *flags, unsigned long long *pos, unsigned long long *scan_tmp);
 
 // Filter (count >= min) with order preserved; flags/scan in tmp.
 void launch_filter_count(void *stream, const uint64_t *counts, uint64_t n, uint64_t min_count,
