@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OKM_ABI_VERSION 1
+#define OKM_ABI_VERSION 2
 
 /* Byte that separates records in the device batch layout: any byte that is
  * not A/C/G/T/U (either case) kills every window containing it, so windows
@@ -251,6 +251,8 @@ typedef struct okm_engine_info {
     uint32_t work_items;     /* partitions counted in LDS */
     uint64_t max_partition;  /* largest partition (instances) */
     uint64_t device_bytes;   /* device memory held */
+    uint32_t groups;         /* key-range groups counted one after the other (0/1 = one) */
+    uint32_t reserved;
 } okm_engine_info;
 okm_status okm_engine_info_get(okm_ctx *ctx, okm_engine_info *info);
 

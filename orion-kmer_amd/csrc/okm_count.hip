@@ -36,7 +36,7 @@ namespace okm {
 #define OKM_COUNT_WPE 8  // waves per EU floor of the unweighted kernel: 4 blocks/CU (64 VGPRs)
 #endif
 #ifndef OKM_COUNT_PREFETCH  // full/dense kernel: load the next item's keys during this one
-#define OKM_COUNT_PREFETCH 1
+#define OKM_COUNT_PREFETCH 0  // measured slower on K128: the extra registers spill (k=63: 22.2 vs 17.2 ms)
 #endif
 #ifndef OKM_COUNT_PROF
 #define OKM_COUNT_PROF 0

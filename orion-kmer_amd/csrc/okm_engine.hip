@@ -99,6 +99,11 @@ struct DevPool {
         if (it == size_.end()) return;
         free_.emplace(it->second, p);
     }
+    size_t cached() const {
+        size_t b = 0;
+        for (auto &kv : free_) b += kv.first;
+        return b;
+    }
     void trim() {
         for (auto &kv : free_) {
             (void)hipFree(kv.second);
@@ -775,6 +780,13 @@ static uint32_t log2_floor(uint64_t x) {
     return r;
 }
 
+// A result table owned by the caller (key-range groups, do_count): entries
+// go to [off, off + distinct).
+struct ResDst {
+    uint64_t *keys, *counts;
+    uint64_t off;
+};
+
 // Count the items in LDS (okm_count.hip), then gather their sorted runs into
 // the dense result table.  The table is first sized by the instance bound
 // (in_total), so the distinct total is read back once, at the end; when that
@@ -788,7 +800,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     uint64_t out_total, uint64_t in_total, bool weighted,
                                     std::vector<void *> &level_bufs, const unsigned long long *guard = nullptr,
                                     unsigned long long *hguard = nullptr, bool *aborted = nullptr,
-                                    const unsigned long long *d_nitems = nullptr) {
+                                    const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr) {
     uint64_t *sk, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
@@ -817,12 +829,19 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     // one-pass: the result table sized by the instance bound
     const uint64_t bound = std::max<uint64_t>(in_total, 1);
     uint64_t *rk = nullptr, *rc = nullptr;
-    bool one_pass = c->pool.get(bound * 8 * c->kw, (void **)&rk) == OKM_OK;
-    if (one_pass && c->pool.get(bound * 8, (void **)&rc) != OKM_OK) {
-        c->pool.put(rk);
-        one_pass = false;
+    bool one_pass;
+    if (dst) {  // a key-range group: straight into the caller's table (sized by the instance bound)
+        rk = dst->keys + dst->off * c->kw;
+        rc = dst->counts + dst->off;
+        one_pass = true;
+    } else {
+        one_pass = c->pool.get(bound * 8 * c->kw, (void **)&rk) == OKM_OK;
+        if (one_pass && c->pool.get(bound * 8, (void **)&rc) != OKM_OK) {
+            c->pool.put(rk);
+            one_pass = false;
+        }
+        if (!one_pass) (void)hipGetLastError();  // the exact-size path below
     }
-    if (!one_pass) (void)hipGetLastError();  // the exact-size path below
     if (one_pass) {
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, !weighted, guard,
@@ -842,7 +861,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         *aborted = (hv[2] | hv[3]) != 0;
         if (*aborted) {
             release_own();
-            if (one_pass) {
+            if (one_pass && !dst) {
                 c->pool.put(rk);
                 c->pool.put(rc);
             }
@@ -857,7 +876,9 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         c->timer.stats[c->timer.id_of("count_items")].alg_bytes += staged * (double)nd;
         if (one_pass) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
     }
-    if (one_pass) {
+    if (dst) {
+        OKM_TRY(sync(c));  // the caller reuses this group's buffers for the next
+    } else if (one_pass) {
         c->res_keys = rk;
         c->res_counts = rc;
     } else {
@@ -1009,6 +1030,18 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
     return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
 }
 
+struct CountPlan {
+    uint32_t twok;
+    uint64_t item_max;
+    uint32_t capbits;
+    uint64_t target;
+    uint32_t maxb;
+};
+static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
+                              const CountPlan &cp, const ResDst *dst);
+static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
+                                const CountPlan &cp);
+
 static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
     invalidate_result(c);
@@ -1051,6 +1084,7 @@ static okm_status do_count(okm_ctx *c) {
     // initial parts: the L1 bins, each a list of per-run segments
     std::vector<DevSeg> segtab;
     std::vector<Part> parts;
+    const CountPlan cp{twok, item_max, capbits, target, maxb};
     for (uint32_t b = 0; b < c->nbins; ++b) {
         Part p{(uint32_t)segtab.size(), 0, 0, b, c->l1_bits};
         for (auto &r : c->runs) {
@@ -1072,7 +1106,15 @@ static okm_status do_count(okm_ctx *c) {
     c->info.l2_bits = 0;
     c->info.levels = 0;
     c->info.max_partition = 0;
+    return count_grouped(c, segtab, parts, weighted, cp);
+}
 
+// Count `parts` (key-range parts over segtab, in key order) into c->res_*, or
+// into *dst (then only c->n_res is set: this part's distinct keys).
+static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
+                              const CountPlan &cp, const ResDst *dst) {
+    const uint32_t twok = cp.twok, capbits = cp.capbits, maxb = cp.maxb;
+    const uint64_t item_max = cp.item_max, target = cp.target;
     auto plan = [&](uint32_t i) -> uint32_t {  // bits to split part i by (0: keep)
         const Part &p = parts[i];
         const uint32_t rem = twok - p.consumed;
@@ -1191,7 +1233,7 @@ static okm_status do_count(okm_ctx *c) {
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.padded, L.total, weighted, level_bufs, flags,
-                                          hf, &aborted, d_nitems));
+                                          hf, &aborted, d_nitems, dst));
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;
@@ -1257,7 +1299,116 @@ static okm_status do_count(okm_ctx *c) {
     OKM_TRY(h2d(c, d_segs, segtab.data(), segtab.size() * sizeof(DevSeg)));
     OKM_TRY(h2d(c, d_items, items.data(), nitems * sizeof(DevItem)));
     c->hprof.mark("items.build");
-    return count_and_compact(c, d_items, d_segs, nitems, out_total, in_total, weighted, level_bufs);
+    return count_and_compact(c, d_items, d_segs, nitems, out_total, in_total, weighted, level_bufs, nullptr, nullptr,
+                             nullptr, nullptr, dst);
+}
+
+// Memory-bounded counting.  The working set of a count (level array, fan-out
+// copy, per-item staging: ~4 key words + a count per instance) is bounded by
+// counting the L1 parts in key-range groups, one after the other; the result
+// is the groups' tables in order.  Either every group compacts straight into
+// one table sized by the instance bound (when it fits beside the runs), or
+// each group gets an exact table and the tables are joined at the end.
+// Needed from ~4 G instances on one GPU (e.g. BASELINE configs[3], k=63 over
+// 5.4 Gbases: 85 GB of L1 runs + 127 GB of result); OKM_GROUP_KEYS /
+// OKM_GROUP_MODE (A: bound table, B: exact tables) force it in tests.
+static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
+                                const CountPlan &cp) {
+    uint64_t total = 0;
+    for (const Part &p : parts) total += p.len;
+    const double ws_key = 8.0 * c->kw * 4 + 8.0;  // level + fan-out copy + staging keys (+ slack) + counts
+    const double res_key = 8.0 * c->kw + 8.0;     // result entry (instance bound)
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        free_b = 0;
+    }
+    const double avail = 0.9 * (double)(free_b + c->pool.cached());
+    uint64_t group_keys = total;
+    int mode = 0;  // 0: one group (no grouping)
+    const char *ge = getenv("OKM_GROUP_KEYS");
+    const char *gm = getenv("OKM_GROUP_MODE");
+    if (ge && atoll(ge) > 0) {
+        group_keys = (uint64_t)atoll(ge);
+        mode = (gm && gm[0] == 'B') ? 2 : 1;
+    } else if ((double)total * (ws_key + res_key) > avail) {
+        const double room_a = avail - (double)total * res_key;  // beside a bound-sized table
+        if (room_a >= (double)total * ws_key / 64.0) {
+            mode = 1;
+            group_keys = (uint64_t)(room_a / ws_key);
+        } else {
+            mode = 2;
+            group_keys = (uint64_t)(avail / 2.0 / ws_key);
+        }
+        group_keys = std::max<uint64_t>(group_keys, 1);
+    }
+    if (mode == 0 || group_keys >= total) return count_parts(c, segtab, parts, weighted, cp, nullptr);
+
+    ResDst d{nullptr, nullptr, 0};
+    if (mode == 1) {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &d.counts));
+    }
+    struct Tab {
+        uint64_t *keys, *counts, n;
+    };
+    std::vector<Tab> tabs;
+    okm_engine_info agg = c->info;
+    agg.work_items = 0;
+    agg.max_partition = 0;
+    uint32_t ngroups = 0;
+    for (size_t g0 = 0; g0 < parts.size();) {
+        size_t g1 = g0;
+        uint64_t keys = 0;
+        while (g1 < parts.size() && (g1 == g0 || keys + parts[g1].len <= group_keys)) keys += parts[g1++].len;
+        std::vector<Part> sub(parts.begin() + g0, parts.begin() + g1);
+        c->info.levels = 0;
+        c->info.l2_bits = 0;
+        OKM_TRY(count_parts(c, segtab, sub, weighted, cp, mode == 1 ? &d : nullptr));
+        agg.levels = std::max(agg.levels, c->info.levels);
+        agg.l2_bits = std::max(agg.l2_bits, c->info.l2_bits);
+        agg.work_items += c->info.work_items;
+        agg.max_partition = std::max(agg.max_partition, c->info.max_partition);
+        if (mode == 1) {
+            d.off += c->n_res;
+        } else {
+            tabs.push_back(Tab{c->res_keys, c->res_counts, c->n_res});
+            c->res_keys = c->res_counts = nullptr;
+        }
+        ++ngroups;
+        g0 = g1;
+    }
+    uint64_t nd = d.off;
+    if (mode == 1) {
+        c->res_keys = d.keys;
+        c->res_counts = d.counts;
+    } else {
+        nd = 0;
+        for (auto &t : tabs) nd += t.n;
+        c->pool.trim();  // the groups' working buffers make room for the joined table
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        uint64_t o = 0;
+        for (auto &t : tabs) {
+            if (t.n) {
+                HIP_TRY(hipMemcpyAsync(c->res_keys + o * c->kw, t.keys, t.n * 8 * c->kw, hipMemcpyDeviceToDevice,
+                                       c->stream));
+                HIP_TRY(hipMemcpyAsync(c->res_counts + o, t.counts, t.n * 8, hipMemcpyDeviceToDevice, c->stream));
+            }
+            o += t.n;
+        }
+        OKM_TRY(sync(c));
+        for (auto &t : tabs) {
+            c->pool.put(t.keys);
+            c->pool.put(t.counts);
+        }
+    }
+    agg.distinct = nd;
+    agg.groups = ngroups;
+    c->info = agg;
+    c->n_res = nd;
+    c->counted = true;
+    return OKM_OK;
 }
 
 static bool device_ok(int device, std::string *why) {

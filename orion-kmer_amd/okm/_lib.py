@@ -54,7 +54,8 @@ class KernelStat(Structure):
 class EngineInfo(Structure):
     _fields_ = [("kmers", c_uint64), ("distinct", c_uint64), ("l1_bits", c_uint32),
                 ("l2_bits", c_uint32), ("levels", c_uint32), ("work_items", c_uint32),
-                ("max_partition", c_uint64), ("device_bytes", c_uint64)]
+                ("max_partition", c_uint64), ("device_bytes", c_uint64), ("groups", c_uint32),
+                ("reserved", c_uint32)]
 
 
 class Key128(Structure):

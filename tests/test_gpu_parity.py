@@ -514,3 +514,37 @@ def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
     ek, ec = oc.result(1)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert info["levels"] >= 2
+
+
+@pytest.mark.parametrize("k,wide,mode,maxb", [(31, False, "A", None), (31, False, "B", None), (27, False, "A", "3"),
+                                              (63, True, "A", "3"), (45, True, "B", None)])
+def test_grouped_count(k, wide, mode, maxb, monkeypatch):
+    # memory-bounded counting: the L1 parts are counted in key-range groups
+    # (OKM_GROUP_KEYS forces ~1.5 M instances per group), compacted straight
+    # into one instance-bound table (A) or into exact per-group tables joined
+    # at the end (B); with OKM_PART_MAXB the groups also take the fan-out path
+    from oracle import OracleCounterWide
+    monkeypatch.setenv("OKM_GROUP_KEYS", "1500000")
+    monkeypatch.setenv("OKM_GROUP_MODE", mode)
+    if maxb:
+        monkeypatch.setenv("OKM_PART_MAXB", maxb)
+    batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=9, seed=k + 1, sub_rate=0.01,
+                            n_rate=0.001)
+    gk, gc, stats, info = _count_device(batch, k, wide=wide)
+    oc = OracleCounterWide(k) if wide else OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    if wide:
+        gk = gk.reshape(-1, 2)
+    assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["groups"] >= 4 and info["distinct"] == len(ec), info
+    if maxb:
+        assert "fan_split" in stats
+    with okm.KmerCounter(k, wide=wide) as m:  # min_count filter over a grouped table
+        m.add_records([r for r in batch.tobytes().split(b"\n") if r], normalized=True)
+        for mc in (1, 3):
+            fk, fc = m.result(mc)
+            xk, xc = oc.result(mc)
+            if wide:
+                fk = fk.reshape(-1, 2)
+            assert np.array_equal(fk, xk) and np.array_equal(fc, xc), mc

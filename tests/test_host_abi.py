@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     # and the ctypes prototypes cover the whole header
     assert set(syms) == set(_lib.PROTOTYPES), set(syms) ^ set(_lib.PROTOTYPES)
-    assert lib.okm_abi_version() == 1
+    assert lib.okm_abi_version() == 2
 
 
 def test_cli_links_only_the_c_abi():
