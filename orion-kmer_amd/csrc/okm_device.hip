@@ -136,13 +136,16 @@ void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t 
 }
 
 // Fan-out split of one oversized child per job: its keys (<= kFanBlock *
-// kFanPer, held in registers) are counting-sorted by the next `bits` key bits
-// into the same index range of `dk` (order inside a sub-range is free: items
-// are multisets), and each sub-range becomes the item slot item0 + j.  Ranks
-// come from wave ballots (no LDS atomics on the 2..8 counters).
+// kFanPer = 64 Ki) are counting-sorted by the next `bits` (<= 4) key bits into the
+// same index range of `dk` (order inside a sub-range is free: items are
+// multisets), and each sub-range becomes the item slot item0 + j.  Ranks come
+// from wave ballots (no LDS atomics on the few counters) and wait in LDS
+// between the two passes; the keys are read twice (the second time from L2:
+// a job is <= 1 MiB).
 constexpr int kFanBlock = 1024;
-constexpr int kFanPer = 16;
+constexpr int kFanPer = 64;
 constexpr int kFanWaves = kFanBlock / 64;
+constexpr int kFanBins = 16;  // <= 4 bits per job
 uint64_t fan_split_max() { return (uint64_t)kFanBlock * kFanPer; }
 
 template <typename KT, bool W>
@@ -152,41 +155,37 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
                                                          uint64_t *__restrict__ dc, DevItem *__restrict__ items,
                                                          DevSeg *__restrict__ segs, uint64_t item_max,
                                                          uint32_t capbits, ull *__restrict__ oflags) {
-    __shared__ uint32_t wtot[kFanWaves][8];
-    __shared__ uint32_t btot[8], bbase[8];
+    __shared__ uint16_t brs[kFanBlock * kFanPer];  // per key: bin << 12 | rank within (wave, bin) (<= 64 rows x 64 lanes)
+    __shared__ uint32_t wtot[kFanWaves][kFanBins];  // per (wave, bin): count, then start in the job's range
+    __shared__ uint32_t btot[kFanBins];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
     for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
         const DevFanJob jb = jobs[jx];
         const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
-        uint32_t br[kFanPer];  // bin << 16 | rank within (wave, bin); ~0 = none
-        uint32_t run[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform running counts per bin
-        const ull lt = (1ull << lane) - 1ull;
-        // pass 1: bins and ranks (keys are read again below, from L2: a job's
-        // range is <= 256 KiB, and keeping them in registers would spill)
         const uint32_t rows = (uint32_t)((jb.len + kFanBlock - 1) / kFanBlock);  // block-uniform
-#pragma unroll
-        for (int u = 0; u < kFanPer; ++u) {
-            br[u] = ~0u;
-            if ((uint32_t)u >= rows) continue;
+        const ull lt = (1ull << lane) - 1ull;
+        // pass 1: bins and ranks
+        uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
+        for (uint32_t u = 0; u < rows; ++u) {
             const uint64_t idx = (uint64_t)u * kFanBlock + t;
             const KT key = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
             const bool v = !KeyOps<KT>::is_empty(key);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(key, shift) & (nb - 1)) : 0u;
+            uint32_t br = 0;
 #pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) {
-                if (q >= nb) break;
-                const ull m = __ballot(v && b == q);
-                if (v && b == q) br[u] = (q << 16) | (run[q] + (uint32_t)__popcll(m & lt));
-                run[q] += (uint32_t)__popcll(m);
+            for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q) {
+                if (q < nb) {  // block-uniform
+                    const ull m = __ballot(v && b == q);
+                    if (v && b == q) br = (q << 12) | (run[q] + (uint32_t)__popcll(m & lt));
+                    run[q] += (uint32_t)__popcll(m);
+                }
             }
+            brs[u * kFanBlock + t] = (uint16_t)br;
         }
-        {
-            uint32_t mine = run[0];  // lane q publishes the wave's count of bin q (no dynamic register index)
 #pragma unroll
-            for (uint32_t z = 1; z < 8; ++z) mine = lane == z ? run[z] : mine;
-            if (lane < 8) wtot[wv][lane] = lane < nb ? mine : 0u;
-        }
+        for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
+            if (lane == 0) wtot[wv][q] = q < nb ? run[q] : 0u;
         __syncthreads();
         if (t < nb) {
             uint32_t s = 0;
@@ -194,21 +193,26 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
             btot[t] = s;
         }
         __syncthreads();
-        if (t < nb) {
+        if (t < nb) {  // thread q: bin q's item, and every wave's start in bin q
             uint32_t a = 0;
             for (uint32_t q = 0; q < t; ++q) a += btot[q];
-            bbase[t] = a;
             const ull o = jb.off + a, len = btot[t];
-            DevSeg s;
-            s.keys = reinterpret_cast<const uint64_t *>(dk + o);
-            s.counts = W ? dc + o : nullptr;
-            s.len = len;
-            s.key_base = 0;
-            s.out_base = 0;
-            s.shift = kSingleBin;
-            s.nlocal = 1;
-            s.pad = 0;
-            segs[jb.item0 + t] = s;
+            uint32_t w0 = a;
+            for (int w = 0; w < kFanWaves; ++w) {
+                const uint32_t c = wtot[w][t];
+                wtot[w][t] = w0;
+                w0 += c;
+            }
+            DevSeg sg;
+            sg.keys = reinterpret_cast<const uint64_t *>(dk + o);
+            sg.counts = W ? dc + o : nullptr;
+            sg.len = len;
+            sg.key_base = 0;
+            sg.out_base = 0;
+            sg.shift = kSingleBin;
+            sg.nlocal = 1;
+            sg.pad = 0;
+            segs[jb.item0 + t] = sg;
             DevItem it;
             it.seg_begin = jb.item0 + t;
             it.seg_count = 1;
@@ -219,28 +223,19 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
             if (len > item_max && it.rem_bits > capbits) atomicAdd(&oflags[0], 1ull);
             atomicMax(&oflags[2], len);
         }
-        // this wave's start in each bin: the bin's base + the earlier waves' counts
         __syncthreads();
-        uint32_t wb[8];
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
-            uint32_t a = q < nb ? bbase[q] : 0u;
-            for (uint32_t w = 0; w < wv; ++w) a += q < nb ? wtot[w][q] : 0u;
-            wb[q] = a;
-        }
-#pragma unroll
-        for (int u = 0; u < kFanPer; ++u) {
-            if (br[u] == ~0u) continue;
+        // pass 2: every key to its place (keys read again, from L2)
+        for (uint32_t u = 0; u < rows; ++u) {
             const uint64_t idx = (uint64_t)u * kFanBlock + t;
-            const uint32_t q = br[u] >> 16;
-            uint32_t base = wb[0];
-#pragma unroll
-            for (uint32_t z = 1; z < 8; ++z) base = q == z ? wb[z] : base;
-            const ull o = jb.off + base + (br[u] & 0xFFFFu);
-            dk[o] = sk[jb.off + idx];
+            if (idx >= jb.len) continue;
+            const KT key = sk[jb.off + idx];
+            if (KeyOps<KT>::is_empty(key)) continue;
+            const uint32_t br = brs[u * kFanBlock + t];
+            const ull o = jb.off + wtot[wv][br >> 12] + (br & 0xFFFu);
+            dk[o] = key;
             if (W) dc[o] = sc ? sc[jb.off + idx] : 1ull;
         }
-        __syncthreads();  // wtot / bbase reuse by the next job
+        __syncthreads();  // brs / wtot reuse by the next job
     }
 }
 

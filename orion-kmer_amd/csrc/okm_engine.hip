@@ -1160,7 +1160,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                     const uint64_t child = 2 * (parts[i].len >> bits[i]);
                     if (!bits[i] || (parts[i].len >> bits[i]) <= target) continue;
                     uint32_t f = 1;
-                    while (f < 3 && (child >> f) > target) ++f;
+                    while (f < 4 && (child >> f) > target) ++f;
                     fb = std::max(fb, f);
                 }
                 if (fan_env >= 0) fb = std::min<uint32_t>(fb, (uint32_t)fan_env);

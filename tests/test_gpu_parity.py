@@ -503,11 +503,12 @@ def test_fan_out_split(k, wide, monkeypatch):
 
 
 def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
-    # a 2-bit pass cap leaves children too big for one fan-out job: the
-    # speculative count is abandoned and the host plans further rounds
+    # a 1-bit pass cap leaves children (~70 Ki keys) too big for one fan-out
+    # job (<= 64 Ki): the speculative count is abandoned and the host plans
+    # further rounds
     monkeypatch.setenv("OKM_PART_MAXB", "1")
     k = 31
-    batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=8, seed=3, sub_rate=0.01)
+    batch = okm.synth_reads(300_000, 150, genome_len=3_000_000, genome_seed=8, seed=3, sub_rate=0.01)
     gk, gc, stats, info = _count_device(batch, k)
     oc = OracleCounter(k)
     oc.add_separated(batch)
