@@ -148,10 +148,8 @@ __device__ __forceinline__ uint32_t half_shift(uint32_t h) { return (h & 1u) << 
 __device__ __forceinline__ uint32_t half_of(uint32_t word, uint32_t h) { return (word >> half_shift(h)) & 0xFFFFu; }
 
 // Instances of an item (scalar loop over its segments: block-uniform).
-__device__ __forceinline__ uint64_t item_total(const DevItem &it, const DevSeg *__restrict__ segs) {
-    uint64_t total = 0;
-    for (uint32_t sg = 0; sg < it.seg_count; ++sg) total += segs[it.seg_begin + sg].len;
-    return total;
+__device__ __forceinline__ uint64_t item_total(const DevItem &it, const DevSeg *__restrict__) {
+    return it.total;
 }
 
 // Load a tag/full-mode item's instances into registers (flat index over its
@@ -164,6 +162,19 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
     for (int u = 0; u < kPer; ++u) {
         kk[u] = KeyOps<KT>::empty();
         ww[u] = 1;
+    }
+    if (it.seg_count == 1) {  // one segment: straight from the item (no dependent segment load)
+        const uint32_t len = (uint32_t)it.total;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            if ((uint32_t)u * kCB >= len) break;  // block-uniform
+            const uint32_t f = (uint32_t)u * kCB + t;
+            if (f < len) {
+                kk[u] = reinterpret_cast<const KT *>(it.keys0)[f];
+                if (W && it.counts0) ww[u] = it.counts0[f];
+            }
+        }
+        return;
     }
     uint32_t sbase = 0;
     for (uint32_t sg = 0; sg < it.seg_count; ++sg) {

@@ -117,6 +117,9 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
         it.out_off = o;  // distinct <= instances: the bin's own range is a safe output slot
         it.rem_bits = rem;
         it.pad = j == 0 ? 0u : kItemEmpty;
+        it.total = s.len;
+        it.keys0 = s.keys;
+        it.counts0 = s.counts;
         items[(uint64_t)i * F + j] = it;
     }
     if (b) {
@@ -219,6 +222,9 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
             it.out_off = o;
             it.rem_bits = jb.rem - jb.bits;
             it.pad = len ? 0u : kItemEmpty;
+            it.total = len;
+            it.keys0 = sg.keys;
+            it.counts0 = sg.counts;
             items[jb.item0 + t] = it;
             if (len > item_max && it.rem_bits > capbits) atomicAdd(&oflags[0], 1ull);
             atomicMax(&oflags[2], len);
@@ -371,6 +377,9 @@ __global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t
     it.out_off = 0;  // set from the scan of itemtot (k_set_out_off)
     it.rem_bits = shift;
     it.pad = 0;
+    it.total = tot;
+    it.keys0 = segs[(uint64_t)i * nruns].keys;
+    it.counts0 = segs[(uint64_t)i * nruns].counts;
     items[i] = it;
     itemtot[i] = tot;
     if (tot > item_max && shift > capbits) atomicAdd(&flags[0], 1ull);

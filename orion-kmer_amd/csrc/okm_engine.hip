@@ -1280,7 +1280,8 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
         // distinct <= instances, and <= 2^remaining-bits
         const uint32_t rem = twok - parts[i].consumed;
         const uint64_t bound = rem >= 63 ? parts[i].len : std::min<uint64_t>(parts[i].len, 1ull << rem);
-        items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total, rem, 0};
+        const DevSeg &s0 = segtab[parts[i].seg_begin];
+        items[i] = DevItem{parts[i].seg_begin, parts[i].seg_count, out_total, rem, 0, parts[i].len, s0.keys, s0.counts};
         out_total += bound;
         in_total += parts[i].len;
         c->info.max_partition = std::max(c->info.max_partition, parts[i].len);

@@ -54,6 +54,9 @@ struct DevItem {
     uint64_t out_off;        // where its sorted distinct entries go (scratch)
     uint32_t rem_bits;       // key bits below the item's common prefix
     uint32_t pad;            // kItemEmpty: an empty fan-out slot (no segment read)
+    uint64_t total;          // instances over all its segments
+    const uint64_t *keys0;   // seg_count == 1: its segment's keys / counts (no
+    const uint64_t *counts0; //   dependent segment load in the count kernels)
 };
 
 // Sampled L1 placement: bin b's claim cursor lives at cursor[b * OKM_L1_CUR_STRIDE]
