@@ -169,6 +169,9 @@ okm_status okm_result_device(okm_ctx *ctx, const uint64_t **d_keys, const uint64
  * device (compare.rs:58 HashSet::intersection().count()). */
 okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint64_t *b,
                                      uint64_t nb, int device, uint64_t *out);
+/* The same over device-resident arrays (e.g. two okm_result_device tables). */
+okm_status okm_set_intersection_size_device(const uint64_t *d_a, uint64_t na, const uint64_t *d_b,
+                                            uint64_t nb, int device, uint64_t *out);
 
 /* ------------------------------------------------------------------------
  * Device k-mer sets — the read-only callers of the counting path.

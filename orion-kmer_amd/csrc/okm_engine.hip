@@ -1822,6 +1822,37 @@ okm_status okm_set_intersection_size(const uint64_t *a, uint64_t na, const uint6
     return status;
 }
 
+okm_status okm_set_intersection_size_device(const uint64_t *d_a, uint64_t na, const uint64_t *d_b, uint64_t nb,
+                                            int device, uint64_t *out) {
+    if (!out) return fail(OKM_E_ARG, "null out");
+    *out = 0;
+    if (na == 0 || nb == 0) return OKM_OK;
+    if (!d_a || !d_b) return fail(OKM_E_ARG, "null input");
+    std::string why;
+    if (!device_ok(device, &why)) return fail(OKM_E_DEVICE, why);
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long *dout = nullptr;
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    okm_status status = OKM_OK;
+    const bool swap = na > nb;  // probe the smaller set into the larger (compare.rs:58)
+    unsigned long long h = 0;
+    if (hipMalloc(&dout, 8) != hipSuccess) {
+        status = fail(OKM_E_NOMEM, "okm_set_intersection_size_device: device allocation");
+    } else if (hipMemsetAsync(dout, 0, 8, st) != hipSuccess) {
+        status = fail(OKM_E_DEVICE, "okm_set_intersection_size_device: memset");
+    } else {
+        launch_intersect_count(st, swap ? d_b : d_a, swap ? nb : na, swap ? d_a : d_b, swap ? na : nb, dout, false);
+        if (hipMemcpyAsync(&h, dout, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+            status = fail(OKM_E_DEVICE, "okm_set_intersection_size_device: kernel");
+    }
+    if (status == OKM_OK) *out = h;
+    (void)hipGetLastError();
+    if (dout) (void)hipFree(dout);
+    (void)hipStreamDestroy(st);
+    return status;
+}
+
 okm_status okm_synchronize(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));

@@ -360,6 +360,14 @@ def set_intersection_size(a: np.ndarray, b: np.ndarray, device: int = 0) -> int:
     return out.value
 
 
+def set_intersection_size_device(d_a: int, na: int, d_b: int, nb: int, device: int = 0) -> int:
+    """|A ∩ B| of two sorted unique u64 arrays in device memory (compare.rs:58)."""
+    out = c_uint64()
+    check(lib().okm_set_intersection_size_device(c_void_p(d_a), na, c_void_p(d_b), nb, device, byref(out)),
+          "okm_set_intersection_size_device")
+    return out.value
+
+
 # ---------------------------------------------------------------------------
 # KmerDbV2 (db_types.rs:7-14)
 # ---------------------------------------------------------------------------

@@ -89,6 +89,7 @@ PROTOTYPES = {
     "okm_free_result": (None, [c_void_p]),
     "okm_result_device": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), _P64]),
     "okm_set_intersection_size": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_int, _P64]),
+    "okm_set_intersection_size_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_int, _P64]),
     "okm_synchronize": (c_int, [c_void_p]),
     "okm_set_timing": (c_int, [c_void_p, c_int]),
     "okm_kernel_stats": (c_int, [c_void_p, POINTER(KernelStat), c_int, POINTER(c_int)]),

@@ -13,6 +13,9 @@ input, warmup then timed steps bracketed by device syncs).
                      ONT-like lognormal reads (median 2,891 bp, sigma 1.085,
                      clipped 200..100k, 5 % substitutions); --gbases sets the
                      size (configs[3] is ~5.36 Gbases).
+  --workload c5      BASELINE configs[4] shape: build.rs per-sample sets of 64
+                     WGS-shaped synthetic samples (tools/c5_runs.json) into two
+                     databases, then compare.rs (unions, |A ∩ B|, Jaccard).
   --workload classify classify.rs:215-308 — probe a 32-reference database
                      (the genome split in 32 slices, ~100 M keys) against the
                      counted table of the batch (okm_classifier_probe_db).
@@ -195,6 +198,135 @@ def wl_wide(args):
             "kernels": kern, "engine": info}
 
 
+def c5_samples(cap_bases: float):
+    """64 synthetic samples shaped by 64 WGS runs of
+    data_metagenome.json.gz (tools/c5_runs.json: mean read length, base count
+    capped at cap_bases), each drawn from 3 of a pool of 48 seeded genomes
+    (2-8 Mbp); samples 0-31 (DB1) use genomes 0-35, samples 32-63 (DB2)
+    genomes 12-47, so the two halves share half of their genomes."""
+    runs = json.load(open(os.path.join(ROOT, "tools", "c5_runs.json")))["runs"]
+    glen = [2_000_000 + g * 6_000_000 // 47 for g in range(48)]
+    out = []
+    for s_, r in enumerate(runs):
+        rng = np.random.default_rng(5_000 + s_)
+        lo = 0 if s_ < 32 else 12
+        gs = rng.choice(np.arange(lo, lo + 36), size=3, replace=False)
+        L = int(min(max(r["mean_read_len"], 100), 30_000))
+        bases = int(min(r["base_count"], cap_bases))
+        parts = []
+        for j, g in enumerate(gs):
+            nr = max(1, bases // 3 // L)
+            parts.append(okm.synth_reads(nr, L, genome_len=glen[g], genome_seed=9_000 + int(g),
+                                         seed=s_ * 16 + j, sub_rate=0.001, n_rate=0.0001))
+        out.append(np.concatenate(parts))
+    return out
+
+
+def wl_c5(args):
+    """build.rs:46-116 (one k-mer set per sample file) for DB1 and DB2, then
+    compare.rs:51-66 (union of each DB's references, |A ∩ B|, Jaccard), all on
+    the device with the samples resident."""
+    k = 31
+    t = time.time()
+    samples = c5_samples(args.c5_cap)
+    bases = sum(int(len(b)) - int((b == 10).sum()) for b in samples)
+    log(f"C5: 64 samples, {bases / 1e9:.2f} Gbases ({time.time() - t:.1f}s)")
+    dev = []
+    for b in samples:
+        d = okm.DeviceBuffer(len(b))
+        d.upload(b)
+        dev.append((d, len(b)))
+    sample_ctx = okm.KmerCounter(k, "set")
+    unions = [okm.KmerCounter(k, "set"), okm.KmerCounter(k, "set")]
+    cap = [0]
+    store = [None]
+
+    def step():
+        # build: each sample's set, copied into the DB's reference store
+        sizes = []
+        off = 0
+        for i, (d, n) in enumerate(dev):
+            sample_ctx.reset()
+            sample_ctx.add_device_batch(d.address, n)
+            m = sample_ctx.count()
+            if store[0] is None or off + m > cap[0]:
+                raise RuntimeError("reference store too small")
+            sample_ctx.fetch_into_device(store[0].address + 8 * off, 0, m)
+            sizes.append((off, m))
+            off += m
+        # compare: A = union of DB1's references, B = union of DB2's
+        res = []
+        for h in (0, 1):
+            u = unions[h]
+            u.reset()
+            for o, m in sizes[32 * h:32 * h + 32]:
+                u.add_sorted_pairs_device(store[0].address + 8 * o, 0, m)
+            na = u.count()
+            res.append(u.result_device()[0:1] + (na,))
+        inter = okm.set_intersection_size_device(res[0][0], res[0][1], res[1][0], res[1][1])
+        return sizes, res, inter
+
+    # size the reference store once (sum of the sample set sizes)
+    tot = 0
+    for d, n in dev:
+        sample_ctx.reset()
+        sample_ctx.add_device_batch(d.address, n)
+        tot += sample_ctx.count()
+    cap[0] = tot
+    store[0] = okm.DeviceBuffer(8 * tot)
+    dt = timed(step, args.steps, args.warmup)
+    sizes, res, inter = step()
+    na, nb = res[0][1], res[1][1]
+    union = na + nb - inter
+    jac = inter / union if union else 0.0
+    # consistency on the host (bounded): the union of two references per DB
+    # and their intersection, device vs numpy on the downloaded sets
+    sub = []
+    for h in (0, 1):
+        parts = []
+        for o, m in sizes[32 * h:32 * h + 2]:
+            x = np.empty(m, np.uint64)
+            okm.lib().okm_memcpy_d2h(x.ctypes.data, okm.c_void_p(store[0].address + 8 * o), 8 * m)
+            parts.append(x)
+        with okm.KmerCounter(k, "set") as u:
+            for x in parts:
+                u.add_pairs(x)
+            gu, _ = u.result(1)
+        hu = np.union1d(parts[0], parts[1])
+        assert np.array_equal(gu, hu), "device union != host union"
+        sub.append(hu)
+    assert okm.set_intersection_size(sub[0], sub[1]) == len(np.intersect1d(sub[0], sub[1], assume_unique=True))
+    # CPU baseline + parity spot check: the C restatement's set of a sample prefix
+    import oracle
+    sb = samples[0][:min(len(samples[0]), 8_000_000)]
+    sb = sb[:int(np.flatnonzero(sb == 10)[-1]) + 1]
+    tc = time.perf_counter()
+    oc = oracle.OracleCounter(k)
+    oc.add_separated(sb)
+    ek, _ = oc.result(1)
+    tcpu = time.perf_counter() - tc
+    with okm.KmerCounter(k, "set") as c1:
+        c1.add_records([r for r in sb.tobytes().split(b"\n") if r], normalized=True)
+        gk, _ = c1.result(1)
+    assert np.array_equal(gk, ek), "engine set != oracle set on the CPU sample"
+    cb = int(len(sb) - (sb == 10).sum())
+    return {"metric": "bases/sec built into per-sample k-mer sets + compared (k=31, build.rs + compare.rs) "
+                      "on one MI355X",
+            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u64",
+            "data": "synthetic (64 samples shaped by tools/c5_runs.json, device-resident)",
+            "config": {"workload": f"BASELINE configs[4] shape on one GPU: 64 WGS-shaped samples (reads from 3 of 48 "
+                                   f"seeded 2-8 Mbp genomes, <= {args.c5_cap / 1e6:.0f} Mbases each), DB1 = "
+                                   f"samples 0-31, DB2 = 32-63",
+                       "k": k, "bases": bases, "set_sizes_total": int(tot),
+                       "db1_total_unique_kmers_across_references": int(na),
+                       "db2_total_unique_kmers_across_references": int(nb), "intersection_size": int(inter),
+                       "union_size": int(union), "jaccard_index": jac},
+            "cpu_baseline": {"value": round(cb / tcpu, 1), "unit": "bases/s", "cores": 1, "kind": "port",
+                             "sample": f"first {cb} bases of sample 0, oracle set build (O(k) encode per window, "
+                                       f"1 thread), {tcpu:.1f} s; engine set identical"}}
+
+
 def wl_classify(args):
     k = 31
     batch = c2_batch()
@@ -225,13 +357,15 @@ def wl_classify(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["query", "build", "wide", "classify"], required=True)
+    ap.add_argument("--workload", choices=["query", "build", "wide", "classify", "c5"], required=True)
+    ap.add_argument("--c5-cap", type=float, default=256e6, help="c5: base cap per sample (SURVEY: 256 Mbases)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gbases", type=float, default=1.0)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     args = ap.parse_args()
-    out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify}[args.workload](args)
+    out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify,
+           "c5": wl_c5}[args.workload](args)
     print(json.dumps(out), flush=True)
 
 
