@@ -313,6 +313,97 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
     }
 }
 
+// Single sweep (OKM_WIDE_SWEEP1, default): the 16 keys of a thread and their
+// within-bin ranks (returned by the histogram atomic) stay in registers, as
+// in k_extract_scatter, so each window is extracted once and the second LDS
+// atomic pass of the two-sweep kernel above is gone; the next tile's bytes
+// are loaded while this tile is staged and written.
+#ifndef OKM_WIDE_SWEEP1
+#define OKM_WIDE_SWEEP1 1
+#endif
+__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const uint8_t *__restrict__ seq,
+                                                                         ExtractGeom g,
+                                                                         const uint32_t *__restrict__ HC,
+                                                                         ull *__restrict__ cursor,
+                                                                         K128 *__restrict__ out,
+                                                                         const ull *__restrict__ cap_end,
+                                                                         ull *__restrict__ ovf) {
+    __shared__ K128 stage[kTileW + 64];  // + one dummy slot per lane for invalid windows
+    __shared__ ull gcur[kMaxL1Bins];
+    __shared__ uint32_t hist[kMaxL1Bins + 1];
+    __shared__ uint32_t lofs[kMaxL1Bins];
+    __shared__ uint32_t lcur[kMaxL1Bins];
+    __shared__ ull wsum[kExtractBlock / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t nb = g.nbins;
+    if (t < nb && HC) {
+        const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
+        gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
+    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
+    const uint32_t shift = g.shift;
+    constexpr int NP = WinWords<kSegW, 64>::kLoad / 16;
+    WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead
+    if (beg + (uint64_t)t * kSegW < end) load_windows<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
+    const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
+    for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
+        if (t <= nb) hist[t] = 0;
+        __syncthreads();
+        const uint64_t w0 = t0 + (uint64_t)t * kSegW;
+        const bool live = w0 < end;
+        uint32_t tile_n;
+        {
+            K128 kk[kSegW];
+            uint32_t rk[kSegW];  // bin << 16 | rank; invalid: nb << 16
+#pragma unroll
+            for (int j = 0; j < kSegW; ++j) rk[j] = nb << 16;
+            if (live) {
+                Codes<NP> c;
+                make_codes<NP, false>(ww.w, c);
+#pragma unroll
+                for (int j = 0; j < kSegW; ++j) {
+                    bool valid;
+                    const K128 key = window_key128(c, j, g.k, &valid);
+                    const uint32_t b = valid ? bin_of_wide(key, shift) : nb;
+                    kk[j] = key;
+                    rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
+                }
+            }
+            if (w0 + kTileW < end) load_windows<kSegW, 64>(seq, g.n, w0 + kTileW, ww);  // next tile, in flight
+            __syncthreads();
+            tile_n = tile_offsets<kExtractBlock>(t, nb, hist, lofs, lcur, wsum);
+            uint32_t ch = 0;
+            ull cp = 0;
+            if (!HC && t < nb) {
+                ch = hist[t];
+                if (ch) cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kSegW; ++j) {
+                const uint32_t b = rk[j] >> 16;
+                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTileW + (t & 63u);
+                stage[dst] = kk[j];
+            }
+            if (!HC && t < nb) {
+                const bool fits = ch && cp + ch <= capb;
+                if (ch && !fits) atomicOr(ovf, 1ull);
+                gcur[t] = fits ? cp : ~0ull;
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
+            const K128 key = stage[j];
+            const uint32_t b = bin_of_wide(key, shift);
+            const ull gb = gcur[b];
+            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
+        }
+        __syncthreads();
+        if (HC && t < nb) gcur[t] += hist[t];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fill_line_tails_wide(const ull *__restrict__ end, uint32_t nbins,
                                                               K128 *__restrict__ keys, const ull *__restrict__ cap) {
     const uint32_t b = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
@@ -349,8 +440,12 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
                             const unsigned long long *cap_end, unsigned long long *ovf) {
     hipStream_t s = (hipStream_t)stream;
     if (g.k > 32) {
-        hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC, cursor,
-                           reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
+        if (OKM_WIDE_SWEEP1)
+            hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC,
+                               cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
+        else
+            hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC,
+                               cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
         return;
     }
     switch (g.k) {
