@@ -25,7 +25,7 @@ so no final merge is needed.  The same code runs over gloo with CPU tensors
 
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -34,6 +34,15 @@ import torch.distributed as dist
 HIST_BITS = 16
 
 MergeFn = Callable[[torch.Tensor, torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]
+
+
+class DeviceView:
+    """__cuda_array_interface__ of an engine-owned int64 device array, so
+    torch.as_tensor(DeviceView(ptr, n), device="cuda") wraps it without a copy."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False),
+                                         "version": 3, "strides": None}
 
 
 def key_bins(keys: torch.Tensor, k: int, bits: int) -> torch.Tensor:
@@ -84,16 +93,30 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, k: int,
     return rk, rc, bounds
 
 
-def exchange_runs(keys: torch.Tensor, counts: torch.Tensor, k: int,
-                  group: Optional[dist.ProcessGroup] = None):
+def shared_bounds(tables: Sequence[torch.Tensor], k: int,
+                  group: Optional[dist.ProcessGroup] = None) -> List[int]:
+    """Owner bin bounds balanced over the sum of several sorted tables (one
+    all_reduce): tables exchanged with the same bounds land on the same owner
+    key by key, so per-owner results combine by a plain sum (C5's |A ∩ B|)."""
+    world = dist.get_world_size(group)
+    hist = local_histogram(tables[0], k)
+    for t in tables[1:]:
+        hist += local_histogram(t, k)
+    dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    return owner_ranges(hist.cpu().numpy(), world)
+
+
+def exchange_runs(keys: torch.Tensor, counts: Optional[torch.Tensor], k: int,
+                  group: Optional[dist.ProcessGroup] = None, bounds: Optional[List[int]] = None):
     """exchange(), also returning the number of pairs received from each rank:
     rank r's run is rk[sum(sizes[:r]) : sum(sizes[:r+1])], sorted by key
-    (okm_add_sorted_pairs_device takes each run without copying)."""
+    (okm_add_sorted_pairs_device takes each run without copying).  counts may
+    be None (sets: rc is then None); bounds default to this table's own
+    balanced ranges (shared_bounds() for several tables)."""
     world = dist.get_world_size(group)
     dev = keys.device
-    hist = local_histogram(keys, k)
-    dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
-    bounds = owner_ranges(hist.cpu().numpy(), world)
+    if bounds is None:
+        bounds = shared_bounds([keys], k, group)
     bits = hist_bits(k)
     shift = 2 * k - bits
     # key boundaries of the owners' ranges (first key of each range)
@@ -114,10 +137,38 @@ def exchange_runs(keys: torch.Tensor, counts: torch.Tensor, k: int,
     ss = send_sizes.cpu().tolist()
     rs = recv_sizes.cpu().tolist()
     rk = torch.empty(sum(rs), dtype=torch.int64, device=dev)
-    rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
     dist.all_to_all_single(rk, keys.contiguous(), rs, ss, group=group)
-    dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
+    rc = None
+    if counts is not None:
+        rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
     return rk, rc, bounds, rs
+
+
+UnionFn = Callable[[torch.Tensor, List[int]], Tuple[int, object]]
+IntersectFn = Callable[[object, int, object, int], int]
+
+
+def distributed_compare(a_keys: torch.Tensor, b_keys: torch.Tensor, k: int, union: UnionFn,
+                        intersect: IntersectFn,
+                        group: Optional[dist.ProcessGroup] = None) -> Tuple[int, int, int]:
+    """compare.rs:51-66 over ranks (SURVEY.md §8(e) "C5"): a_keys / b_keys are
+    this rank's union of its share of DB1's / DB2's references (sorted unique
+    keys).  Both go to value-range owners under ONE set of bounds, each owner
+    unions its received runs (union(received, run sizes) -> (size, handle))
+    and intersects its two owned ranges; the three sizes are summed with one
+    all_reduce.  Returns (|A|, |B|, |A ∩ B|) of the global unions."""
+    bounds = shared_bounds([a_keys, b_keys], k, group)
+    ra, _, _, rsa = exchange_runs(a_keys, None, k, group, bounds)
+    na, ha = union(ra, rsa)
+    rb, _, _, rsb = exchange_runs(b_keys, None, k, group, bounds)
+    nb, hb = union(rb, rsb)
+    inter = intersect(ha, na, hb, nb)
+    dev = a_keys.device
+    tot = torch.tensor([na, nb, inter], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    na_g, nb_g, i_g = (int(x) for x in tot.cpu().tolist())
+    return na_g, nb_g, i_g
 
 
 def distributed_merge(keys: torch.Tensor, counts: torch.Tensor, k: int, merge: MergeFn,

@@ -108,3 +108,79 @@ def test_owner_ranges_balance_and_cover():
     h[7] = 100
     b = okm_dist.owner_ranges(h, 4)
     assert b[0] == 0 and b[-1] == 64 and sorted(b) == b
+
+
+# ---------------------------------------------------------------------------
+# C5 over ranks: compare.rs:51-66 with the references sharded by sample
+# ---------------------------------------------------------------------------
+
+def _c5_samples(n=8, n_reads=600, read_len=120):
+    """Small WGS-like samples: DB1 = samples [0, n/2), DB2 = [n/2, n); each
+    sample draws reads from 2 of 6 seeded genomes, the halves share some."""
+    out = []
+    for s in range(n):
+        rng = np.random.default_rng(100 + s)
+        lo = 0 if s < n // 2 else 2
+        gs = rng.choice(np.arange(lo, lo + 4), size=2, replace=False)
+        out.append(np.concatenate([okm.synth_reads(n_reads, read_len, genome_len=30_000, genome_seed=700 + int(g),
+                                                   seed=s * 8 + j, sub_rate=0.002, n_rate=0.001)
+                                   for j, g in enumerate(gs)]))
+    return out
+
+
+def _oracle_set(batch, k):
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    return oc.result(1)[0]
+
+
+def _c5_worker(rank, world, port, k, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        samples = _c5_samples()
+        half = len(samples) // 2
+        mine = range(rank, len(samples), world)  # samples dealt round-robin
+        local = {0: [], 1: []}
+        for s in mine:
+            local[0 if s < half else 1].append(_oracle_set(samples[s], k))
+
+        def local_union(sets):
+            u = np.unique(np.concatenate(sets)) if sets else np.zeros(0, np.uint64)
+            return torch.from_numpy(u.view(np.int64).copy())
+
+        def union(rk, sizes):
+            # every received run is sorted and unique (a rank's own union)
+            off, runs = 0, []
+            for sz in sizes:
+                run = rk[off:off + sz].numpy().view(np.uint64)
+                assert np.all(run[1:] > run[:-1])
+                runs.append(run)
+                off += sz
+            u = np.unique(np.concatenate(runs)) if runs else np.zeros(0, np.uint64)
+            return len(u), u
+
+        def intersect(ha, na, hb, nb):
+            return len(np.intersect1d(ha, hb, assume_unique=True))
+
+        na, nb, inter = okm_dist.distributed_compare(local_union(local[0]), local_union(local[1]), k, union,
+                                                     intersect)
+        if rank == 0:
+            np.savez(out_path, res=np.array([na, nb, inter], np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 31), (3, 32)])
+def test_distributed_compare_equals_single_process(world, k, tmp_path):
+    out = os.path.join(str(tmp_path), f"c5_{world}_{k}.npz")
+    mp.spawn(_c5_worker, args=(world, _free_port(), k, out), nprocs=world, join=True)
+    na, nb, inter = (int(x) for x in np.load(out)["res"])
+    samples = _c5_samples()
+    half = len(samples) // 2
+    a = np.unique(np.concatenate([_oracle_set(s, k) for s in samples[:half]]))
+    b = np.unique(np.concatenate([_oracle_set(s, k) for s in samples[half:]]))
+    ei = len(np.intersect1d(a, b, assume_unique=True))
+    assert (na, nb, inter) == (len(a), len(b), ei)
+    assert 0 < ei < min(len(a), len(b))  # the halves share genomes, not all of them

@@ -16,6 +16,8 @@ input, warmup then timed steps bracketed by device syncs).
   --workload c5      BASELINE configs[4] shape: build.rs per-sample sets of 64
                      WGS-shaped synthetic samples (tools/c5_runs.json) into two
                      databases, then compare.rs (unions, |A ∩ B|, Jaccard).
+                     Under torchrun (WORLD_SIZE > 1) the samples shard over the
+                     ranks and the unions are owner-partitioned (wl_c5_dist).
   --workload classify classify.rs:215-308 — probe a 32-reference database
                      (the genome split in 32 slices, ~100 M keys) against the
                      counted table of the batch (okm_classifier_probe_db).
@@ -198,7 +200,7 @@ def wl_wide(args):
             "kernels": kern, "engine": info}
 
 
-def c5_samples(cap_bases: float):
+def c5_samples(cap_bases: float, which=None):
     """64 synthetic samples shaped by 64 WGS runs of
     data_metagenome.json.gz (tools/c5_runs.json: mean read length, base count
     capped at cap_bases), each drawn from 3 of a pool of 48 seeded genomes
@@ -208,6 +210,8 @@ def c5_samples(cap_bases: float):
     glen = [2_000_000 + g * 6_000_000 // 47 for g in range(48)]
     out = []
     for s_, r in enumerate(runs):
+        if which is not None and s_ not in which:
+            continue
         rng = np.random.default_rng(5_000 + s_)
         lo = 0 if s_ < 32 else 12
         gs = rng.choice(np.arange(lo, lo + 36), size=3, replace=False)
@@ -327,6 +331,136 @@ def wl_c5(args):
                                        f"1 thread), {tcpu:.1f} s; engine set identical"}}
 
 
+def wl_c5_dist(args):
+    """C5 over WORLD_SIZE ranks, one GPU each (SURVEY.md §8(e) "C5"): the 64
+    samples are dealt round-robin (sample s -> rank s mod N), every rank builds
+    its samples' sets (build.rs:46-116) and unions its share of each DB's
+    references; okm.dist.distributed_compare then moves both unions to
+    value-range owners under one set of bounds, each owner unions and
+    intersects its ranges on its GPU and one all_reduce sums |A|, |B|, |A ∩ B|
+    (compare.rs:51-66).  Strong scaling: the 64-sample workload is fixed."""
+    import torch
+    import torch.distributed as tdist
+    from okm import dist as okm_dist
+    k = 31
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    else:
+        tdist.init_process_group(backend)
+    mine = list(range(rank, 64, world))
+    t = time.time()
+    samples = dict(zip(mine, c5_samples(args.c5_cap, set(mine))))
+    my_bases = sum(int(len(b)) - int((b == 10).sum()) for b in samples.values())
+    log(f"[rank {rank}] C5: {len(mine)} samples, {my_bases / 1e9:.2f} Gbases ({time.time() - t:.1f}s)")
+    dev = {}
+    for s_, b in samples.items():
+        d = okm.DeviceBuffer(len(b), device)
+        d.upload(b)
+        dev[s_] = (d, len(b))
+    sample_ctx = okm.KmerCounter(k, "set", device)
+    locals_ = [okm.KmerCounter(k, "set", device), okm.KmerCounter(k, "set", device)]
+    owners = [okm.KmerCounter(k, "set", device), okm.KmerCounter(k, "set", device)]
+    tot = 0
+    for d, n in dev.values():
+        sample_ctx.reset()
+        sample_ctx.add_device_batch(d.address, n)
+        tot += sample_ctx.count()
+    store = okm.DeviceBuffer(max(8, 8 * tot), device)
+
+    def as_tensor(ptr, n):
+        if n == 0:
+            return torch.empty(0, dtype=torch.int64, device="cuda")
+        t_ = torch.as_tensor(okm_dist.DeviceView(ptr, n), device="cuda")
+        return t_ if backend == "nccl" else t_.cpu()
+
+    def step():
+        sizes = {}
+        off = 0
+        for s_, (d, n) in dev.items():
+            sample_ctx.reset()
+            sample_ctx.add_device_batch(d.address, n)
+            m = sample_ctx.count()
+            sample_ctx.fetch_into_device(store.address + 8 * off, 0, m)
+            sizes[s_] = (off, m)
+            off += m
+        tabs = []
+        for h in (0, 1):
+            u = locals_[h]
+            u.reset()
+            for s_, (o, m) in sizes.items():
+                if (s_ < 32) == (h == 0) and m:
+                    u.add_sorted_pairs_device(store.address + 8 * o, 0, m)
+            n = u.count()
+            tabs.append(as_tensor(u.result_device()[0], n))
+        torch.cuda.synchronize()
+        which = [0]
+
+        def union(rk, rs):
+            o_ = owners[which[0]]
+            which[0] += 1
+            if backend != "nccl":
+                rk = rk.cuda()
+            o_.reset()
+            pos = 0
+            for sz in rs:
+                if sz:
+                    o_.add_sorted_pairs_device(rk.data_ptr() + 8 * pos, 0, sz)
+                pos += sz
+            n = o_.count()
+            keep.append(rk)  # borrowed until count(); kept alive for the step
+            return n, o_.result_device()[0]
+
+        def intersect(ha, na, hb, nb):
+            return okm.set_intersection_size_device(ha, na, hb, nb, device) if na and nb else 0
+
+        keep = []
+        return okm_dist.distributed_compare(tabs[0], tabs[1], k, union, intersect)
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        tdist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier_sync()
+    dt = (time.perf_counter() - t0) / args.steps
+    tt = torch.tensor([dt, float(my_bases), float(tot)], dtype=torch.float64,
+                      device="cuda" if backend == "nccl" else "cpu")
+    mx = tt.clone()
+    tdist.all_reduce(mx, op=tdist.ReduceOp.MAX)
+    tdist.all_reduce(tt, op=tdist.ReduceOp.SUM)
+    dt = float(mx[0])
+    bases, set_total = int(tt[1]), int(tt[2])
+    na, nb, inter = res
+    union_ = na + nb - inter
+    tdist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {"metric": f"bases/sec built into per-sample k-mer sets + compared (k=31, build.rs + compare.rs) "
+                      f"on {world} MI355X",
+            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "dtype": "u64",
+            "data": "synthetic (64 samples shaped by tools/c5_runs.json, device-resident)",
+            "config": {"workload": f"BASELINE configs[4] shape over {world} ranks: 64 WGS-shaped samples "
+                                   f"(<= {args.c5_cap / 1e6:.0f} Mbases each) dealt round-robin, DB1 = samples "
+                                   f"0-31, DB2 = 32-63, unions owner-partitioned ({backend})",
+                       "k": k, "bases": bases, "set_sizes_total": set_total,
+                       "db1_total_unique_kmers_across_references": na,
+                       "db2_total_unique_kmers_across_references": nb, "intersection_size": inter,
+                       "union_size": union_, "jaccard_index": inter / union_ if union_ else 0.0}}
+
+
 def wl_classify(args):
     k = 31
     batch = c2_batch()
@@ -364,9 +498,11 @@ def main():
     ap.add_argument("--gbases", type=float, default=1.0)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     args = ap.parse_args()
+    c5 = wl_c5_dist if int(os.environ.get("WORLD_SIZE", "1")) > 1 else wl_c5
     out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify,
-           "c5": wl_c5}[args.workload](args)
-    print(json.dumps(out), flush=True)
+           "c5": c5}[args.workload](args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
