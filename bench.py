@@ -92,7 +92,10 @@ def main():
     # nccl (= RCCL over xGMI) is the product path; OKM_BENCH_BACKEND=gloo rehearses
     # the same exchange through host memory (RCCL refuses two ranks on one GPU)
     backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
-    if world > 1:
+    # OKM_BENCH_EXCHANGE=1 runs the N>1 exchange + merge path at world size 1
+    # too (torchrun --nproc-per-node 1): its cost on one GPU, RCCL self-send
+    dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -110,8 +113,8 @@ def main():
         f"({time.time() - t0:.1f}s)")
 
     ctr = okm.KmerCounter(K, "count", device)
-    merger = okm.KmerCounter(K, "count", device) if world > 1 else None
-    if world > 1:
+    merger = okm.KmerCounter(K, "count", device) if dist_on else None
+    if dist_on:
         from okm import dist as okm_dist
 
     class _DevView:  # zero-copy int64 view of an engine-owned device array
@@ -138,12 +141,15 @@ def main():
             ctr.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
         return keys, counts
 
+    xt = [0.0, 0.0]  # exchange, merge wall time (N>1 path)
+
     def step():
         ctr.reset()
         ctr.add_device_batch(dbuf.address, len(batch))
         n = ctr.count()
-        if world == 1:
+        if not dist_on:
             return n
+        t_x = time.perf_counter()
         keys, counts = table_tensors(n)
         if backend == "nccl":
             rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
@@ -151,6 +157,8 @@ def main():
             rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
             rk, rc = rk.cuda(), rc.cuda()
         torch.cuda.synchronize()
+        t_m = time.perf_counter()
+        xt[0] += t_m - t_x
         # each rank's slice is sorted: the owner counts them in place (no copy,
         # no partition pass; okm_add_sorted_pairs_device)
         merger.reset()
@@ -159,12 +167,14 @@ def main():
             if sz:
                 merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
             off += sz
-        return merger.count()
+        n_m = merger.count()
+        xt[1] += time.perf_counter() - t_m
+        return n_m
 
     def barrier_sync():
         torch.cuda.synchronize()
         ctr.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -172,13 +182,14 @@ def main():
         step()
     ctr.set_timing(not args.no_timing)
     barrier_sync()
+    xt[0] = xt[1] = 0.0
     t_start = time.perf_counter()
     n_owned = 0
     for _ in range(args.steps):
         n_owned = step()
     barrier_sync()
     dt = time.perf_counter() - t_start
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -203,7 +214,7 @@ def main():
                          f"count.rs is single-threaded), {tcpu:.1f} s incl. filter+sort"}
 
     if rank != 0:
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
 
@@ -267,10 +278,12 @@ def main():
         "kernels": kernels,
         "engine": info,
     }
-    if world > 1:
+    if dist_on:
         out["config"]["owned_distinct_rank0"] = int(n_owned)
+        out["exchange_ms_per_step_rank0"] = {"exchange": round(xt[0] / args.steps * 1e3, 3),
+                                             "merge": round(xt[1] / args.steps * 1e3, 3)}
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     dbuf.free()
 
