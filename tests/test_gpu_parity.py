@@ -313,6 +313,26 @@ def test_unique_keys_full_mode(k):
     assert np.array_equal(mk, ek2) and np.array_equal(mc, ec2)
 
 
+def test_deferred_items_mid_table():
+    # covered reads everywhere + a burst of unique k-mers that all start with
+    # CCCCCCC (canonical keys in one mid-table key range): the items of that
+    # range overflow the tag mode and are deferred to k_count_slow while the
+    # items on both sides are tag-counted; one dense table in key order
+    k = 31
+    cov = okm.synth_reads(60_000, 150, genome_len=400_000, genome_seed=3, seed=31, sub_rate=0.002)
+    rng = np.random.default_rng(7)
+    tails = rng.integers(0, 4, size=(40_000, 24))
+    burst = [b"CCCCCCC" + bytes(b"ACGT"[x] for x in row) for row in tails]
+    recs = [r for r in cov.tobytes().split(b"\n") if r] + burst
+    oc = OracleCounter(k)
+    oc.add_records(recs)
+    ek, ec = oc.result(1)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records(recs)
+        gk, gc = ctr.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
 def test_empty_inputs():
     with okm.KmerCounter(21) as ctr:
         ctr.add_records([])
