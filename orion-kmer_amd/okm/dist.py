@@ -114,12 +114,15 @@ def shared_bounds(tables: Sequence[torch.Tensor], k: int,
 
 
 def exchange_runs(keys: torch.Tensor, counts: Optional[torch.Tensor], k: int,
-                  group: Optional[dist.ProcessGroup] = None, bounds: Optional[List[int]] = None):
+                  group: Optional[dist.ProcessGroup] = None, bounds: Optional[List[int]] = None,
+                  narrow_counts: bool = True):
     """exchange(), also returning the number of pairs received from each rank:
     rank r's run is rk[sum(sizes[:r]) : sum(sizes[:r+1])], sorted by key
     (okm_add_sorted_pairs_device takes each run without copying).  counts may
     be None (sets: rc is then None); bounds default to this table's own
-    balanced ranges (shared_bounds() for several tables)."""
+    balanced ranges (shared_bounds() for several tables); narrow_counts sends
+    counts as bytes with escapes (_send_counts_u8), the received rc is int64
+    either way."""
     world = dist.get_world_size(group)
     dev = keys.device
     if bounds is None:
@@ -147,9 +150,45 @@ def exchange_runs(keys: torch.Tensor, counts: Optional[torch.Tensor], k: int,
     dist.all_to_all_single(rk, keys.contiguous(), rs, ss, group=group)
     rc = None
     if counts is not None:
-        rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
+        if narrow_counts:
+            rc = _send_counts_u8(counts.contiguous(), edges, ss, rs, group)
+        else:
+            rc = torch.empty(sum(rs), dtype=torch.int64, device=dev)
+            dist.all_to_all_single(rc, counts.contiguous(), rs, ss, group=group)
     return rk, rc, bounds, rs
+
+
+COUNT_ESCAPE = 255
+
+
+def _send_counts_u8(counts: torch.Tensor, edges: torch.Tensor, ss: List[int], rs: List[int],
+                    group: Optional[dist.ProcessGroup]) -> torch.Tensor:
+    """Counts over the wire as one byte each (a count >= 255 travels as 255 plus
+    an escape entry: its position in the destination's run and its full
+    value).  Tables of covered reads hold mostly small counts, so a pair costs
+    9 bytes instead of 16 on the link; xGMI is point-to-point (one link per GPU
+    pair), so at 2 and 4 ranks these bytes bound the exchange."""
+    world = len(ss)
+    dev = counts.device
+    r8 = torch.empty(sum(rs), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(r8, torch.clamp(counts, max=COUNT_ESCAPE).to(torch.uint8), rs, ss, group=group)
+    esc = torch.nonzero(counts >= COUNT_ESCAPE).flatten()  # ascending positions
+    esend = (torch.searchsorted(esc, edges[1:]) - torch.searchsorted(esc, edges[:-1])).to(torch.int64)
+    erecv = torch.empty_like(esend)
+    dist.all_to_all_single(erecv, esend, group=group)
+    es, er = esend.cpu().tolist(), erecv.cpu().tolist()
+    ranks = torch.arange(world, dtype=torch.int64, device=dev)
+    rel = esc - edges[:-1][torch.repeat_interleave(ranks, esend)]  # position within its destination run
+    rrel = torch.empty(sum(er), dtype=torch.int64, device=dev)
+    rval = torch.empty(sum(er), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rrel, rel, er, es, group=group)
+    dist.all_to_all_single(rval, counts[esc], er, es, group=group)
+    rc = r8.to(torch.int64)
+    if sum(er):
+        run0 = torch.tensor(np.concatenate([[0], np.cumsum(rs[:-1], dtype=np.int64)]), dtype=torch.int64,
+                            device=dev)
+        rc[run0[torch.repeat_interleave(ranks, erecv)] + rrel] = rval
+    return rc
 
 
 UnionFn = Callable[[torch.Tensor, List[int]], Tuple[int, object]]

@@ -31,8 +31,13 @@ def _free_port() -> int:
 
 
 def _reads(n_reads: int, read_len: int, seed: int) -> np.ndarray:
-    return okm.synth_reads(n_reads, read_len, genome_len=200_000, genome_seed=seed, seed=seed + 1,
-                           sub_rate=0.01, n_rate=0.001)
+    b = okm.synth_reads(n_reads, read_len, genome_len=200_000, genome_seed=seed, seed=seed + 1,
+                        sub_rate=0.01, n_rate=0.001)
+    if seed % 2:  # odd seeds: every 50th read a poly-A / ACGT repeat, so counts pass the 255 escape
+        recs = b.reshape(n_reads, read_len + 1)
+        recs[::50, :read_len] = np.frombuffer(b"A" * read_len, np.uint8)
+        recs[25::100, :read_len] = np.frombuffer((b"ACGT" * read_len)[:read_len], np.uint8)
+    return b
 
 
 def _oracle_merge(k):
@@ -45,7 +50,7 @@ def _oracle_merge(k):
     return merge
 
 
-def _worker(rank, world, port, k, n_reads, read_len, seed, empty_rank, out_path):
+def _worker(rank, world, port, k, n_reads, read_len, seed, empty_rank, out_path, narrow=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,7 +64,8 @@ def _worker(rank, world, port, k, n_reads, read_len, seed, empty_rank, out_path)
         lk, lc = oc.result(1)
         keys = torch.from_numpy(lk.view(np.int64).copy())
         counts = torch.from_numpy(lc.view(np.int64).copy())
-        mk, mc = okm_dist.distributed_merge(keys, counts, k, _oracle_merge(k))
+        rk, rc, _, _ = okm_dist.exchange_runs(keys, counts, k, narrow_counts=narrow)
+        mk, mc = _oracle_merge(k)(rk, rc)
         # owned ranges are sorted and disjoint, in rank order
         gk, gc = okm_dist.gather_global(mk, mc)
         if rank == 0:
@@ -68,9 +74,9 @@ def _worker(rank, world, port, k, n_reads, read_len, seed, empty_rank, out_path)
         dist.destroy_process_group()
 
 
-def _run(world, k, n_reads=6_000, read_len=150, seed=11, empty_rank=-1, tmp_path=None):
+def _run(world, k, n_reads=6_000, read_len=150, seed=11, empty_rank=-1, tmp_path=None, narrow=True):
     out = os.path.join(str(tmp_path), f"merged_{world}_{k}.npz")
-    mp.spawn(_worker, args=(world, _free_port(), k, n_reads, read_len, seed, empty_rank, out),
+    mp.spawn(_worker, args=(world, _free_port(), k, n_reads, read_len, seed, empty_rank, out, narrow),
              nprocs=world, join=True)
     got = np.load(out)
     batch = _reads(n_reads, read_len, seed)
@@ -86,6 +92,15 @@ def _run(world, k, n_reads=6_000, read_len=150, seed=11, empty_rank=-1, tmp_path
 @pytest.mark.parametrize("world,k", [(2, 31), (2, 32), (3, 21)])
 def test_owner_partitioned_merge_equals_single_table(world, k, tmp_path):
     gk, gc, ek, ec = _run(world, k, tmp_path=tmp_path)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+@pytest.mark.parametrize("narrow", [True, False])
+def test_merge_counts_past_the_byte_escape(narrow, tmp_path):
+    # seed 11 is odd: poly-A and ACGT-repeat reads give counts in the
+    # thousands, which travel as escapes when counts go as bytes
+    gk, gc, ek, ec = _run(3, 31, seed=11, tmp_path=tmp_path, narrow=narrow)
+    assert (ec >= 255).sum() >= 2
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
 
 
