@@ -13,8 +13,16 @@ random genome (0.1 % substitutions, 0.01 % N).  With
 --gpus N every rank counts its own 3,355,443 reads of the same genome (weak
 scaling) and the tables are merged.
 
+Batches in flight (--streams, default 2): at N=1 two engine contexts, each
+with its own HIP stream and table, count whole batches concurrently from two
+host threads (one batch's host syncs and latency-bound count phase overlap the
+other's streaming kernels); at N>1 one thread counts into two contexts in turn
+while the exchange + merge of the previous batch runs (RCCL on its own stream).
+Every step still counts one full batch into its own sorted table.
+
 Prints ONE JSON line on rank 0 (the driver's contract), including `roofline`
-for the dominant kernel (HIP events on the engine's own stream) and
+for the dominant kernel (HIP events on the engine's own stream, from a
+single-stream pass of the same K steps after the timed region) and
 `cpu_baseline` (the oracle, oracle/okm_oracle.c, on a bounded sample, rank 0
 at N=1 only).
 """
@@ -76,6 +84,8 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=300_000,
                     help="reads in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
     return ap.parse_args()
 
 
@@ -112,51 +122,58 @@ def main():
     log(f"[rank {rank}] synthetic batch: {args.reads} reads, {bases} bases, {len(batch)} bytes "
         f"({time.time() - t0:.1f}s)")
 
-    ctr = okm.KmerCounter(K, "count", device)
+    # Batches in flight: at N=1, S contexts (each its own HIP stream and result
+    # table) driven by S host threads count whole batches concurrently, so one
+    # batch's host syncs and latency-bound phases overlap another's streaming
+    # kernels.  At N>1 one thread counts into two contexts in turn while this
+    # thread exchanges and merges the previous batch's table (RCCL on its own
+    # stream): the xGMI exchange overlaps the next count.
+    S = max(1, args.streams)
+    ctrs = [okm.KmerCounter(K, "count", device) for _ in range(2 if dist_on else S)]
+    ctr = ctrs[0]
     merger = okm.KmerCounter(K, "count", device) if dist_on else None
+    xs = torch.cuda.Stream() if dist_on and backend == "nccl" else None
     if dist_on:
         from okm import dist as okm_dist
 
-    class _DevView:  # zero-copy int64 view of an engine-owned device array
-        def __init__(self, ptr, n):
-            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False),
-                                             "version": 3, "strides": None}
-
     zero_copy = [True]
 
-    def table_tensors(n):
+    def table_tensors(c, n):
         """The counted table as int64 device tensors: views of the engine's
         result arrays when torch takes __cuda_array_interface__, else a copy."""
         if zero_copy[0] and n:
-            kp, cp, _ = ctr.result_device()
+            kp, cp, _ = c.result_device()
             try:
-                return (torch.as_tensor(_DevView(kp, n), device="cuda"),
-                        torch.as_tensor(_DevView(cp, n), device="cuda"))
+                return (torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda"),
+                        torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda"))
             except Exception as e:  # pragma: no cover - torch build without the protocol
                 log(f"note: no zero-copy device views ({e}); copying the table")
                 zero_copy[0] = False
         keys = torch.empty(n, dtype=torch.int64, device="cuda")
         counts = torch.empty(n, dtype=torch.int64, device="cuda")
         if n:
-            ctr.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
+            c.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
         return keys, counts
+
+    def count_batch(c):
+        c.reset()
+        c.add_device_batch(dbuf.address, len(batch))
+        return c.count()
 
     xt = [0.0, 0.0]  # exchange, merge wall time (N>1 path)
 
-    def step():
-        ctr.reset()
-        ctr.add_device_batch(dbuf.address, len(batch))
-        n = ctr.count()
-        if not dist_on:
-            return n
+    def exchange_merge(c, n, release):
         t_x = time.perf_counter()
-        keys, counts = table_tensors(n)
+        keys, counts = table_tensors(c, n)
         if backend == "nccl":
-            rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
+            with torch.cuda.stream(xs):
+                rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
+                xs.synchronize()
         else:
             rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
             rk, rc = rk.cuda(), rc.cuda()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+        release()  # the table has been copied out: its context may count the next batch
         t_m = time.perf_counter()
         xt[0] += t_m - t_x
         # each rank's slice is sorted: the owner counts them in place (no copy,
@@ -171,29 +188,95 @@ def main():
         xt[1] += time.perf_counter() - t_m
         return n_m
 
+    def run_steps(nsteps):
+        """nsteps batches through the path; returns the distinct count (N=1)
+        or this rank's owned distinct count of the last merge (N>1)."""
+        import threading
+        if not dist_on:
+            if S == 1:
+                n = 0
+                for _ in range(nsteps):
+                    n = count_batch(ctr)
+                return n
+            nxt, lock, res, err = [0], threading.Lock(), [], []
+
+            def worker(c):
+                try:
+                    while True:
+                        with lock:
+                            if nxt[0] >= nsteps:
+                                return
+                            nxt[0] += 1
+                        res.append(count_batch(c))
+                except BaseException as e:  # surfaced below
+                    err.append(e)
+
+            th = [threading.Thread(target=worker, args=(c,), daemon=True) for c in ctrs]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            if err:
+                raise err[0]
+            return res[-1]
+        import queue
+        free = [threading.Semaphore(1), threading.Semaphore(1)]
+        q = queue.Queue()
+        err = []
+
+        def producer():
+            try:
+                for i in range(nsteps):
+                    j = i % 2
+                    free[j].acquire()
+                    q.put((j, count_batch(ctrs[j])))
+            except BaseException as e:
+                err.append(e)
+                q.put(None)
+
+        th = threading.Thread(target=producer, daemon=True)
+        th.start()
+        n_owned = 0
+        for _ in range(nsteps):
+            item = q.get()
+            if item is None:
+                raise err[0]
+            j, n = item
+            n_owned = exchange_merge(ctrs[j], n, free[j].release)
+        th.join()
+        return n_owned
+
     def barrier_sync():
         torch.cuda.synchronize()
-        ctr.synchronize()
+        for c in ctrs:
+            c.synchronize()
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    ctr.set_timing(not args.no_timing)
+    for c in ctrs:  # every context warmed (pool sized) before the timed region
+        count_batch(c)
+    run_steps(args.warmup)
     barrier_sync()
     xt[0] = xt[1] = 0.0
     t_start = time.perf_counter()
-    n_owned = 0
-    for _ in range(args.steps):
-        n_owned = step()
+    n_owned = run_steps(args.steps)
     barrier_sync()
     dt = time.perf_counter() - t_start
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    stats = ctr.kernel_stats() if not args.no_timing else {}
+    # per-kernel HIP-event timing: a separate single-stream pass of the same K
+    # steps (kernels of the timed region overlap across streams, so their
+    # durations there would not be any one kernel's)
+    stats = {}
+    if not args.no_timing:
+        ctr.set_timing(True)
+        for _ in range(args.steps):
+            count_batch(ctr)
+        stats = ctr.kernel_stats()
+        ctr.set_timing(False)
     info = ctr.engine_info()
 
     # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) -------
@@ -240,7 +323,9 @@ def main():
                 "traffic": round(tk["traffic_bytes"]) if tk else None,
                 "traffic_unit": "bytes per launch (HBM, rocprofv3 PMC)",
                 "traffic_source": tsrc if tk else None,
-                "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"]}
+                "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"],
+                "measured": "HIP events on the engine stream, single-stream pass of the same K steps after the "
+                            "timed region"}
         if tk:
             roof["traffic_GBs"] = round(tk["traffic_bytes"] / (dk["avg_ms"] * 1e-3) / 1e9, 1)
         tot_ms = sum(s["total_ms"] for s in stats.values())
@@ -268,7 +353,8 @@ def main():
                                "per GPU + RCCL owner-partitioned table merge",
                    "k": K, "reads_per_gpu": args.reads, "read_len": READ_LEN, "genome_bp": GENOME_BP,
                    "distinct_kmers": int(info["distinct"]) if world == 1 else None,
-                   "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}"},
+                   "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}",
+                   "batches_in_flight": 2 if dist_on else S},
         "roofline": roof,
         "cpu_baseline": cpu,
         "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,
