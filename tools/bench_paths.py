@@ -242,44 +242,74 @@ def wl_c5(args):
         d = okm.DeviceBuffer(len(b))
         d.upload(b)
         dev.append((d, len(b)))
-    sample_ctx = okm.KmerCounter(k, "set")
+    # two contexts (own HIP stream each) build alternate samples from two host
+    # threads, and the two unions run concurrently the same way
+    import threading
+    sample_ctxs = [okm.KmerCounter(k, "set"), okm.KmerCounter(k, "set")]
     unions = [okm.KmerCounter(k, "set"), okm.KmerCounter(k, "set")]
-    cap = [0]
-    store = [None]
+    # per-sample set sizes (deterministic) fix each sample's slice of the store
+    offs = []
+    tot = 0
+    sample_ctx = sample_ctxs[0]
+    for d, n in dev:
+        sample_ctx.reset()
+        sample_ctx.add_device_batch(d.address, n)
+        m = sample_ctx.count()
+        offs.append((tot, m))
+        tot += m
+    store = [okm.DeviceBuffer(8 * tot)]
+
+    def par(fn, items):
+        """items[0::2] on one host thread, items[1::2] on another."""
+        err = []
+
+        def run(part):
+            try:
+                for x in part:
+                    fn(*x)
+            except BaseException as e:
+                err.append(e)
+
+        th = [threading.Thread(target=run, args=(items[i::2],), daemon=True) for i in range(2)]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        if err:
+            raise err[0]
 
     def step():
-        # build: each sample's set, copied into the DB's reference store
-        sizes = []
-        off = 0
-        for i, (d, n) in enumerate(dev):
-            sample_ctx.reset()
-            sample_ctx.add_device_batch(d.address, n)
-            m = sample_ctx.count()
-            if store[0] is None or off + m > cap[0]:
-                raise RuntimeError("reference store too small")
-            sample_ctx.fetch_into_device(store[0].address + 8 * off, 0, m)
-            sizes.append((off, m))
-            off += m
+        # build: each sample's set, copied into its slice of the reference store
+        got = [0] * len(dev)
+
+        def build(i, c):
+            d, n = dev[i]
+            c.reset()
+            c.add_device_batch(d.address, n)
+            m = c.count()
+            if m != offs[i][1]:
+                raise RuntimeError("sample set size changed between steps")
+            c.fetch_into_device(store[0].address + 8 * offs[i][0], 0, m)
+            got[i] = m
+
+        # sample i on context i % 2: thread j (items j::2) owns context j
+        par(build, [(i, sample_ctxs[i % 2]) for i in range(len(dev))])
+        sizes = [(o, m) for (o, _), m in zip(offs, got)]
         # compare: A = union of DB1's references, B = union of DB2's
-        res = []
-        for h in (0, 1):
+        res = [None, None]
+
+        def union(h):
             u = unions[h]
             u.reset()
             for o, m in sizes[32 * h:32 * h + 32]:
                 u.add_sorted_pairs_device(store[0].address + 8 * o, 0, m)
             na = u.count()
-            res.append(u.result_device()[0:1] + (na,))
+            res[h] = u.result_device()[0:1] + (na,)
+
+        par(union, [(0,), (1,)])
         inter = okm.set_intersection_size_device(res[0][0], res[0][1], res[1][0], res[1][1])
         return sizes, res, inter
 
-    # size the reference store once (sum of the sample set sizes)
-    tot = 0
-    for d, n in dev:
-        sample_ctx.reset()
-        sample_ctx.add_device_batch(d.address, n)
-        tot += sample_ctx.count()
-    cap[0] = tot
-    store[0] = okm.DeviceBuffer(8 * tot)
     dt = timed(step, args.steps, args.warmup)
     sizes, res, inter = step()
     na, nb = res[0][1], res[1][1]
