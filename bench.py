@@ -219,32 +219,9 @@ def main():
             if err:
                 raise err[0]
             return res[-1]
-        import queue
-        free = [threading.Semaphore(1), threading.Semaphore(1)]
-        q = queue.Queue()
-        err = []
-
-        def producer():
-            try:
-                for i in range(nsteps):
-                    j = i % 2
-                    free[j].acquire()
-                    q.put((j, count_batch(ctrs[j])))
-            except BaseException as e:
-                err.append(e)
-                q.put(None)
-
-        th = threading.Thread(target=producer, daemon=True)
-        th.start()
-        n_owned = 0
-        for _ in range(nsteps):
-            item = q.get()
-            if item is None:
-                raise err[0]
-            j, n = item
-            n_owned = exchange_merge(ctrs[j], n, free[j].release)
-        th.join()
-        return n_owned
+        res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
+                                     lambda i, j, n, release: exchange_merge(ctrs[j], n, release))
+        return res[-1] if res else 0
 
     def barrier_sync():
         torch.cuda.synchronize()

@@ -244,3 +244,47 @@ def gather_global(keys: torch.Tensor, counts: torch.Tensor,
     ok = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gk, ns)]).view(np.uint64)
     oc = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gc, ns)]).view(np.uint64)
     return ok, oc
+
+
+def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
+                  consume: Callable[[int, int, object, Callable[[], None]], object]) -> List[object]:
+    """Double-buffered N>1 step loop (bench.py): a worker thread counts batch i
+    into table buffer i % 2 (count_into(i, j) -> handle) while this thread
+    consumes the previous one (consume(i, j, handle, release) -> result), so
+    the exchange of batch i overlaps the count of batch i + 1.  consume calls
+    release() once the table has been copied out (the buffer may then count
+    batch i + 2).  Only this thread issues collectives, so every rank issues
+    them in the same order.  An exception in the worker is re-raised here."""
+    import queue
+    import threading
+    free = [threading.Semaphore(1), threading.Semaphore(1)]
+    q: "queue.Queue" = queue.Queue()
+    err: List[BaseException] = []
+    stop = threading.Event()
+
+    def producer():
+        try:
+            for i in range(nsteps):
+                j = i % 2
+                while not free[j].acquire(timeout=0.1):
+                    if stop.is_set():
+                        return
+                q.put((i, j, count_into(i, j)))
+        except BaseException as e:  # surfaced on the consuming thread
+            err.append(e)
+            q.put(None)
+
+    th = threading.Thread(target=producer, daemon=True)
+    th.start()
+    out = []
+    try:
+        for _ in range(nsteps):
+            item = q.get()
+            if item is None:
+                raise err[0]
+            i, j, h = item
+            out.append(consume(i, j, h, free[j].release))
+    finally:
+        stop.set()
+        th.join()
+    return out

@@ -199,3 +199,65 @@ def test_distributed_compare_equals_single_process(world, k, tmp_path):
     ei = len(np.intersect1d(a, b, assume_unique=True))
     assert (na, nb, inter) == (len(a), len(b), ei)
     assert 0 < ei < min(len(a), len(b))  # the halves share genomes, not all of them
+
+
+# ---------------------------------------------------------------------------
+# bench.py's N>1 loop: double-buffered count / exchange+merge pipeline
+# ---------------------------------------------------------------------------
+
+def _pipe_worker(rank, world, port, k, nsteps, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bufs = [None, None]
+        busy = [False, False]
+
+        def count_into(i, j):
+            assert not busy[j], "a table buffer was recounted before its exchange released it"
+            busy[j] = True
+            recs = _reads(3_000, 150, seed=20 + i).reshape(3_000, 151)
+            oc = OracleCounter(k)
+            oc.add_separated(np.ascontiguousarray(np.array_split(recs, world)[rank]).reshape(-1))
+            lk, lc = oc.result(1)
+            bufs[j] = (torch.from_numpy(lk.view(np.int64).copy()), torch.from_numpy(lc.view(np.int64).copy()))
+            return len(lk)
+
+        def consume(i, j, n, release):
+            keys, counts = bufs[j]
+            assert keys.numel() == n
+            rk, rc, _, _ = okm_dist.exchange_runs(keys, counts, k)
+            busy[j] = False
+            release()
+            mk, mc = _oracle_merge(k)(rk, rc)
+            return okm_dist.gather_global(mk, mc)
+
+        res = okm_dist.run_pipelined(nsteps, count_into, consume)
+        if rank == 0:
+            np.savez(out_path, **{f"k{i}": r[0] for i, r in enumerate(res)}, **{f"c{i}": r[1] for i, r in enumerate(res)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_steps_equal_single_tables(tmp_path):
+    k, world, nsteps = 31, 2, 4
+    out = os.path.join(str(tmp_path), "pipe.npz")
+    mp.spawn(_pipe_worker, args=(world, _free_port(), k, nsteps, out), nprocs=world, join=True)
+    got = np.load(out)
+    for i in range(nsteps):
+        oc = OracleCounter(k)
+        oc.add_separated(_reads(3_000, 150, seed=20 + i))
+        ek, ec = oc.result(1)
+        assert np.array_equal(got[f"k{i}"], ek) and np.array_equal(got[f"c{i}"], ec), i
+
+
+def test_pipelined_worker_error_surfaces():
+    def count_into(i, j):
+        if i == 2:
+            raise RuntimeError("count failed")
+        return i
+
+    seen = []
+    with pytest.raises(RuntimeError, match="count failed"):
+        okm_dist.run_pipelined(5, count_into, lambda i, j, h, release: (release(), seen.append(h)))
+    assert seen == [0, 1]
