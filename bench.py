@@ -16,8 +16,9 @@ scaling) and the tables are merged.
 Batches in flight (--streams, default 2): at N=1 two engine contexts, each
 with its own HIP stream and table, count whole batches concurrently from two
 host threads (one batch's host syncs and latency-bound count phase overlap the
-other's streaming kernels); at N>1 one thread counts into two contexts in turn
-while the exchange + merge of the previous batch runs (RCCL on its own stream).
+other's streaming kernels); at N>1 three stages run at once: one thread counts
+batch i+2 into two contexts in turn, the main thread exchanges batch i+1 (RCCL
+on its own stream) and a third merges batch i into one of two merge contexts.
 Every step still counts one full batch into its own sorted table.
 
 Prints ONE JSON line on rank 0 (the driver's contract), including `roofline`
@@ -131,7 +132,11 @@ def main():
     S = max(1, args.streams)
     ctrs = [okm.KmerCounter(K, "count", device) for _ in range(2 if dist_on else S)]
     ctr = ctrs[0]
-    merger = okm.KmerCounter(K, "count", device) if dist_on else None
+    # N>1: the owner's merge runs on a third thread (two merge contexts in
+    # turn), so it overlaps the next batch's exchange and the one after's
+    # count; OKM_BENCH_MERGE_THREAD=0 keeps exchange+merge on one thread
+    merge_thread = dist_on and os.environ.get("OKM_BENCH_MERGE_THREAD", "1") != "0"
+    mergers = [okm.KmerCounter(K, "count", device) for _ in range(2 if merge_thread else 1)] if dist_on else []
     xs = torch.cuda.Stream() if dist_on and backend == "nccl" else None
     if dist_on:
         from okm import dist as okm_dist
@@ -162,7 +167,7 @@ def main():
 
     xt = [0.0, 0.0]  # exchange, merge wall time (N>1 path)
 
-    def exchange_merge(c, n, release):
+    def exchange_only(c, n, release):
         t_x = time.perf_counter()
         keys, counts = table_tensors(c, n)
         if backend == "nccl":
@@ -174,8 +179,12 @@ def main():
             rk, rc = rk.cuda(), rc.cuda()
             torch.cuda.synchronize()
         release()  # the table has been copied out: its context may count the next batch
+        xt[0] += time.perf_counter() - t_x
+        return rk, rc, rs
+
+    def merge_runs(merger, payload):
+        rk, rc, rs = payload
         t_m = time.perf_counter()
-        xt[0] += t_m - t_x
         # each rank's slice is sorted: the owner counts them in place (no copy,
         # no partition pass; okm_add_sorted_pairs_device)
         merger.reset()
@@ -185,8 +194,12 @@ def main():
                 merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
             off += sz
         n_m = merger.count()
+        merger.synchronize()  # rk / rc (torch memory) may be freed and reused once this returns
         xt[1] += time.perf_counter() - t_m
         return n_m
+
+    def exchange_merge(c, n, release):
+        return merge_runs(mergers[0], exchange_only(c, n, release))
 
     def run_steps(nsteps):
         """nsteps batches through the path; returns the distinct count (N=1)
@@ -219,8 +232,13 @@ def main():
             if err:
                 raise err[0]
             return res[-1]
-        res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
-                                     lambda i, j, n, release: exchange_merge(ctrs[j], n, release))
+        if merge_thread:
+            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
+                                         lambda i, j, n, release: exchange_only(ctrs[j], n, release),
+                                         lambda i, m, payload: merge_runs(mergers[m], payload))
+        else:
+            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
+                                         lambda i, j, n, release: exchange_merge(ctrs[j], n, release))
         return res[-1] if res else 0
 
     def barrier_sync():
@@ -331,7 +349,7 @@ def main():
                    "k": K, "reads_per_gpu": args.reads, "read_len": READ_LEN, "genome_bp": GENOME_BP,
                    "distinct_kmers": int(info["distinct"]) if world == 1 else None,
                    "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}",
-                   "batches_in_flight": 2 if dist_on else S},
+                   "batches_in_flight": (3 if merge_thread else 2) if dist_on else S},
         "roofline": roof,
         "cpu_baseline": cpu,
         "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,

@@ -163,16 +163,17 @@ COUNT_ESCAPE = 255
 
 def _send_counts_u8(counts: torch.Tensor, edges: torch.Tensor, ss: List[int], rs: List[int],
                     group: Optional[dist.ProcessGroup]) -> torch.Tensor:
-    """Counts over the wire as one byte each (a count >= 255 travels as 255 plus
-    an escape entry: its position in the destination's run and its full
-    value).  Tables of covered reads hold mostly small counts, so a pair costs
+    """Counts over the wire as one byte each: the count's low byte (one cast
+    pass, no clamp), and a count >= 256 also travels as an escape entry (its
+    position in the destination's run and its full value) that overwrites
+    the byte on arrival.  Tables of covered reads hold mostly small counts, so a pair costs
     9 bytes instead of 16 on the link; xGMI is point-to-point (one link per GPU
     pair), so at 2 and 4 ranks these bytes bound the exchange."""
     world = len(ss)
     dev = counts.device
     r8 = torch.empty(sum(rs), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(r8, torch.clamp(counts, max=COUNT_ESCAPE).to(torch.uint8), rs, ss, group=group)
-    esc = torch.nonzero(counts >= COUNT_ESCAPE).flatten()  # ascending positions
+    dist.all_to_all_single(r8, counts.to(torch.uint8), rs, ss, group=group)  # low byte (wraps)
+    esc = torch.nonzero(counts > COUNT_ESCAPE).flatten()  # ascending positions
     esend = (torch.searchsorted(esc, edges[1:]) - torch.searchsorted(esc, edges[:-1])).to(torch.int64)
     erecv = torch.empty_like(esend)
     dist.all_to_all_single(erecv, esend, group=group)
@@ -247,14 +248,22 @@ def gather_global(keys: torch.Tensor, counts: torch.Tensor,
 
 
 def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
-                  consume: Callable[[int, int, object, Callable[[], None]], object]) -> List[object]:
-    """Double-buffered N>1 step loop (bench.py): a worker thread counts batch i
+                  consume: Callable[[int, int, object, Callable[[], None]], object],
+                  finish: Optional[Callable[[int, int, object], object]] = None) -> List[object]:
+    """Pipelined N>1 step loop (bench.py).  A worker thread counts batch i
     into table buffer i % 2 (count_into(i, j) -> handle) while this thread
     consumes the previous one (consume(i, j, handle, release) -> result), so
     the exchange of batch i overlaps the count of batch i + 1.  consume calls
     release() once the table has been copied out (the buffer may then count
     batch i + 2).  Only this thread issues collectives, so every rank issues
-    them in the same order.  An exception in the worker is re-raised here."""
+    them in the same order.
+
+    With `finish`, consume's result is a payload handed to a third thread that
+    runs finish(i, m, payload) -> result on merge slot m = i % 2 (the owner's
+    merge, no collectives): the merge of batch i then overlaps the exchange of
+    batch i + 1 and the count of batch i + 2, and the slot is reused by batch
+    i + 2 only after its finish returned.  Results are in step order either
+    way.  An exception in any thread is re-raised here."""
     import queue
     import threading
     free = [threading.Semaphore(1), threading.Semaphore(1)]
@@ -262,29 +271,69 @@ def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
     err: List[BaseException] = []
     stop = threading.Event()
 
+    def acquire(sem: "threading.Semaphore") -> bool:
+        while not sem.acquire(timeout=0.1):
+            if stop.is_set():
+                return False
+        return True
+
     def producer():
         try:
             for i in range(nsteps):
-                j = i % 2
-                while not free[j].acquire(timeout=0.1):
-                    if stop.is_set():
-                        return
-                q.put((i, j, count_into(i, j)))
+                if not acquire(free[i % 2]):
+                    return
+                q.put((i, i % 2, count_into(i, i % 2)))
         except BaseException as e:  # surfaced on the consuming thread
             err.append(e)
+            stop.set()
             q.put(None)
+
+    out: List[object] = [None] * nsteps
+    mfree = [threading.Semaphore(1), threading.Semaphore(1)]
+    mq: "queue.Queue" = queue.Queue()
+
+    def finisher():
+        try:
+            while True:
+                item = mq.get()
+                if item is None:
+                    return
+                i, m, payload = item
+                out[i] = finish(i, m, payload)
+                mfree[m].release()
+        except BaseException as e:
+            err.append(e)
+            stop.set()
 
     th = threading.Thread(target=producer, daemon=True)
     th.start()
-    out = []
+    fth = threading.Thread(target=finisher, daemon=True) if finish is not None else None
+    if fth is not None:
+        fth.start()
     try:
         for _ in range(nsteps):
-            item = q.get()
-            if item is None:
-                raise err[0]
+            item = None
+            while item is None and not err:
+                try:
+                    item = q.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+            if err or item is None:
+                break
             i, j, h = item
-            out.append(consume(i, j, h, free[j].release))
+            r = consume(i, j, h, free[j].release)
+            if fth is None:
+                out[i] = r
+                continue
+            if not acquire(mfree[i % 2]):
+                break
+            mq.put((i, i % 2, r))
     finally:
+        if fth is not None:
+            mq.put(None)
+            fth.join()
         stop.set()
         th.join()
+    if err:
+        raise err[0]
     return out

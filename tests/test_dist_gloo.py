@@ -11,6 +11,7 @@ bench.py runs the same exchange over RCCL with the HIP engine.
 """
 
 import os
+import time
 import socket
 
 import numpy as np
@@ -33,7 +34,7 @@ def _free_port() -> int:
 def _reads(n_reads: int, read_len: int, seed: int) -> np.ndarray:
     b = okm.synth_reads(n_reads, read_len, genome_len=200_000, genome_seed=seed, seed=seed + 1,
                         sub_rate=0.01, n_rate=0.001)
-    if seed % 2:  # odd seeds: every 50th read a poly-A / ACGT repeat, so counts pass the 255 escape
+    if seed % 2:  # odd seeds: every 50th read a poly-A / ACGT repeat, so counts pass the one-byte escape (> 255)
         recs = b.reshape(n_reads, read_len + 1)
         recs[::50, :read_len] = np.frombuffer(b"A" * read_len, np.uint8)
         recs[25::100, :read_len] = np.frombuffer((b"ACGT" * read_len)[:read_len], np.uint8)
@@ -100,7 +101,7 @@ def test_merge_counts_past_the_byte_escape(narrow, tmp_path):
     # seed 11 is odd: poly-A and ACGT-repeat reads give counts in the
     # thousands, which travel as escapes when counts go as bytes
     gk, gc, ek, ec = _run(3, 31, seed=11, tmp_path=tmp_path, narrow=narrow)
-    assert (ec >= 255).sum() >= 2
+    assert (ec > 255).sum() >= 2  # past the byte: escape entries travel
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
 
 
@@ -205,7 +206,7 @@ def test_distributed_compare_equals_single_process(world, k, tmp_path):
 # bench.py's N>1 loop: double-buffered count / exchange+merge pipeline
 # ---------------------------------------------------------------------------
 
-def _pipe_worker(rank, world, port, k, nsteps, out_path):
+def _pipe_worker(rank, world, port, k, nsteps, out_path, staged=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -229,20 +230,37 @@ def _pipe_worker(rank, world, port, k, nsteps, out_path):
             rk, rc, _, _ = okm_dist.exchange_runs(keys, counts, k)
             busy[j] = False
             release()
+            if staged:  # the merge runs on the finish thread
+                return rk, rc
             mk, mc = _oracle_merge(k)(rk, rc)
             return okm_dist.gather_global(mk, mc)
 
-        res = okm_dist.run_pipelined(nsteps, count_into, consume)
+        mbusy = [False, False]
+
+        def finish(i, m, payload):  # no collectives off the main thread
+            assert not mbusy[m], "a merge slot was reused before its merge finished"
+            mbusy[m] = True
+            time.sleep(0.01 * (i % 2))  # let the exchange of the next batch run ahead
+            r = _oracle_merge(k)(*payload)
+            mbusy[m] = False
+            return r
+
+        if staged:
+            merged = okm_dist.run_pipelined(nsteps, count_into, consume, finish)
+            res = [okm_dist.gather_global(mk, mc) for mk, mc in merged]
+        else:
+            res = okm_dist.run_pipelined(nsteps, count_into, consume)
         if rank == 0:
             np.savez(out_path, **{f"k{i}": r[0] for i, r in enumerate(res)}, **{f"c{i}": r[1] for i, r in enumerate(res)})
     finally:
         dist.destroy_process_group()
 
 
-def test_pipelined_steps_equal_single_tables(tmp_path):
+@pytest.mark.parametrize("staged", [False, True], ids=["count|exchange+merge", "count|exchange|merge"])
+def test_pipelined_steps_equal_single_tables(tmp_path, staged):
     k, world, nsteps = 31, 2, 4
     out = os.path.join(str(tmp_path), "pipe.npz")
-    mp.spawn(_pipe_worker, args=(world, _free_port(), k, nsteps, out), nprocs=world, join=True)
+    mp.spawn(_pipe_worker, args=(world, _free_port(), k, nsteps, out, staged), nprocs=world, join=True)
     got = np.load(out)
     for i in range(nsteps):
         oc = OracleCounter(k)
@@ -261,3 +279,19 @@ def test_pipelined_worker_error_surfaces():
     with pytest.raises(RuntimeError, match="count failed"):
         okm_dist.run_pipelined(5, count_into, lambda i, j, h, release: (release(), seen.append(h)))
     assert seen == [0, 1]
+
+
+def test_pipelined_finish_error_surfaces():
+    def finish(i, m, payload):
+        if i == 1:
+            raise RuntimeError("merge failed")
+        return payload
+
+    with pytest.raises(RuntimeError, match="merge failed"):
+        okm_dist.run_pipelined(6, lambda i, j: i, lambda i, j, h, release: (release(), h)[1], finish)
+
+
+def test_pipelined_finish_results_in_order():
+    out = okm_dist.run_pipelined(7, lambda i, j: i, lambda i, j, h, release: (release(), h * 10)[1],
+                                 lambda i, m, p: (i, m, p))
+    assert out == [(i, i % 2, i * 10) for i in range(7)]
