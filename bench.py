@@ -13,10 +13,11 @@ random genome (0.1 % substitutions, 0.01 % N).  With
 --gpus N every rank counts its own 3,355,443 reads of the same genome (weak
 scaling) and the tables are merged.
 
-Batches in flight (--streams, default 2): at N=1 two engine contexts, each
-with its own HIP stream and table, count whole batches concurrently from two
+Batches in flight (--streams, default 3): at N=1 three engine contexts, each
+with its own HIP stream and table, count whole batches concurrently from three
 host threads (one batch's host syncs and latency-bound count phase overlap the
-other's streaming kernels); at N>1 three stages run at once: one thread counts
+others' streaming kernels; measured 2 / 3 / 4 in flight: 5.81-6.02 /
+5.70-5.74 / 5.73-5.90 ms per batch, tools/ab_streams.sh); at N>1 three stages run at once: one thread counts
 batch i+2 into two contexts in turn, the main thread exchanges batch i+1 (RCCL
 on its own stream) and a third merges batch i into one of two merge contexts.
 Every step still counts one full batch into its own sorted table.
@@ -85,7 +86,7 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=300_000,
                     help="reads in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
     return ap.parse_args()
 
@@ -127,8 +128,9 @@ def main():
     # table) driven by S host threads count whole batches concurrently, so one
     # batch's host syncs and latency-bound phases overlap another's streaming
     # kernels.  At N>1 one thread counts into two contexts in turn while this
-    # thread exchanges and merges the previous batch's table (RCCL on its own
-    # stream): the xGMI exchange overlaps the next count.
+    # thread exchanges the previous batch's table (RCCL on its own stream) and
+    # a third thread merges the one before: the xGMI exchange overlaps the
+    # next count and the previous merge.
     S = max(1, args.streams)
     ctrs = [okm.KmerCounter(K, "count", device) for _ in range(2 if dist_on else S)]
     ctr = ctrs[0]
