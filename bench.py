@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--reads", type=int, default=READS_PER_GPU, help="reads per GPU")
     ap.add_argument("--cpu-sample-reads", type=int, default=300_000,
                     help="reads in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-mt-reads", type=int, default=800_000,
+                    help="reads of the labelled restatement-MT CPU sample (0: skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--streams", type=int, default=3,
                     help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
@@ -292,6 +294,31 @@ def main():
                "sample": f"first {m} reads ({m * READ_LEN} bases) of the same batch, k=31, "
                          f"oracle/okm_oracle.c (faithful O(k) encode+rc per window, 1 thread, "
                          f"count.rs is single-threaded), {tcpu:.1f} s incl. filter+sort"}
+    # a labelled multi-threaded restatement beside it (NOT the
+    # reference's behaviour: count never uses rayon), on the host cores this
+    # process may use (OMP_NUM_THREADS on the box), checked against the engine
+    cpu_mt = None
+    if rank == 0 and world == 1 and args.cpu_sample_reads > 0 and args.cpu_mt_reads > 0:
+        from oracle import count_separated_mt
+        nproc = os.cpu_count() or 1
+        thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or nproc), nproc))
+        m = min(args.cpu_mt_reads, args.reads)
+        sample = batch[:m * (READ_LEN + 1)]
+        tc = time.perf_counter()
+        mk, mc = count_separated_mt(sample, K, thr)
+        tmt = time.perf_counter() - tc
+        with okm.KmerCounter(K, "count", device) as chk:  # the sample on the engine: same table
+            sb = okm.DeviceBuffer(len(sample), device)
+            sb.upload(sample)
+            chk.add_device_batch(sb.address, len(sample))
+            gk, gc = chk.result(1)
+            sb.free()
+        cpu_mt = {"value": m * READ_LEN / tmt, "unit": "bases/s", "threads": thr, "nproc": nproc,
+                  "kind": "restatement-MT (not reference behaviour: count.rs is single-threaded)",
+                  "sample": f"first {m} reads ({m * READ_LEN} bases) of the same batch, k=31, "
+                            f"{thr} shards counted by oracle/okm_oracle.c on {thr} threads + key-range "
+                            f"merge, {tmt:.1f} s",
+                  "engine_table_equal": bool(np.array_equal(mk, gk) and np.array_equal(mc, gc))}
 
     if rank != 0:
         if dist_on:
@@ -354,6 +381,7 @@ def main():
                    "batches_in_flight": (3 if merge_thread else 2) if dist_on else S},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "cpu_baseline_mt": cpu_mt,
         "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,
                             "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
                             "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),

@@ -192,3 +192,68 @@ class OracleCounterWide(OracleCounter):
         counts = np.empty(max(n, 1), dtype=np.uint64)
         m = load().oracle_counter_wide_result(self.h, min_count, keys.ctypes.data, counts.ctypes.data, n)
         return keys[:m].copy(), counts[:m].copy()
+
+
+def count_separated_mt(data: np.ndarray, k: int, threads: int, sep: int = ord("\n")) -> Tuple[np.ndarray, np.ndarray]:
+    """Restatement-MT (SURVEY.md §8(d) "cpu_ref --threads"): NOT the
+    reference's behaviour — count.rs:68-79 is single-threaded — but the same
+    per-window work split over host cores, as a labelled second CPU number.
+    The batch (records joined by `sep`) is cut at record boundaries into
+    `threads` shards, each counted by its own C counter on its own thread
+    (ctypes drops the GIL), and the sorted per-shard tables are merged by key
+    range, again one range per thread (numpy's sort drops the GIL too).
+    Returns the sorted (keys, counts) of the whole batch, min_count 1."""
+    import threading
+
+    load()  # built / loaded once, before the threads
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    threads = max(1, int(threads))
+    cut = np.flatnonzero(data == sep)
+    # shard ends: the separator nearest each 1/threads point (a record never splits)
+    ends = [0]
+    for t in range(1, threads):
+        i = int(np.searchsorted(cut, len(data) * t // threads))
+        ends.append(int(cut[i]) + 1 if i < len(cut) else len(data))
+    ends.append(len(data))
+    tables = [None] * threads
+
+    def count_shard(t: int) -> None:
+        oc = OracleCounter(k)
+        oc.add_separated(data[ends[t]:ends[t + 1]], sep)
+        tables[t] = oc.result(1)
+
+    ths = [threading.Thread(target=count_shard, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    # key-range merge: range r = keys in [b_r, b_{r+1}) of every shard's table
+    bounds = np.linspace(0, float(1 << (2 * k)) if k < 32 else float(2 ** 64), threads + 1)
+    bk = [np.uint64(min(int(b), 2 ** 64 - 1)) for b in bounds]
+    parts = [None] * threads
+
+    def merge_range(r: int) -> None:
+        ks, cs = [], []
+        for tk, tc in tables:
+            lo = np.searchsorted(tk, bk[r], side="left") if r else 0
+            hi = np.searchsorted(tk, bk[r + 1], side="left") if r + 1 < threads else len(tk)
+            ks.append(tk[lo:hi])
+            cs.append(tc[lo:hi])
+        kk = np.concatenate(ks)
+        cc = np.concatenate(cs)
+        order = np.argsort(kk, kind="stable")
+        kk, cc = kk[order], cc[order]
+        if len(kk) == 0:
+            parts[r] = (kk, cc)
+            return
+        first = np.concatenate([[True], kk[1:] != kk[:-1]])
+        starts = np.flatnonzero(first)
+        parts[r] = (kk[starts], np.add.reduceat(cc, starts).astype(np.uint64))
+
+    ths = [threading.Thread(target=merge_range, args=(r,)) for r in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return (np.concatenate([p[0] for p in parts]).astype(np.uint64),
+            np.concatenate([p[1] for p in parts]).astype(np.uint64))

@@ -246,3 +246,20 @@ def test_rust_f64_format():
              1e-6: "1e-6", 1.5e-7: "1.5e-7", 1e16: "1e16", 123.0: "123.0", 2.5e15: "2500000000000000.0"}
     for x, s in cases.items():
         assert R.rust_f64(x) == s, x
+
+
+@pytest.mark.parametrize("k,threads", [(31, 1), (31, 3), (21, 8), (32, 5), (5, 4)])
+def test_c_oracle_mt_equals_single(k, threads):
+    """The labelled restatement-MT CPU number (bench.py cpu_baseline_mt) counts
+    exactly what the single-threaded restatement counts."""
+    from oracle import count_separated_mt
+    rng = np.random.default_rng(k * 10 + threads)
+    recs = [bytes(rng.choice(list(b"ACGTNacgt"), size=int(rng.integers(0, 300)))) for _ in range(400)]
+    recs += [b"A" * 200] * 7  # a hot key across shards
+    rng.shuffle(recs)
+    data = np.frombuffer(b"\n".join(recs), dtype=np.uint8)
+    oc = OracleCounter(k)
+    oc.add_separated(data)
+    ek, ec = oc.result(1)
+    gk, gc = count_separated_mt(data, k, threads)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
