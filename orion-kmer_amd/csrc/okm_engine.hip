@@ -868,7 +868,18 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             return OKM_OK;
         }
     }
-    if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    if (hv[1]) {  // give every buffer of the step back before failing (long-lived contexts)
+        release_own();
+        if (one_pass && !dst) {
+            c->pool.put(rk);
+            c->pool.put(rc);
+        }
+        for (void *p : level_bufs) c->pool.put(p);
+        level_bufs.clear();
+        c->pool.put(d_segs);
+        c->pool.put(d_items);
+        return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    }
     const uint64_t nd = hv[0];
     const double staged = 8.0 * c->kw + (weighted ? 8.0 : 4.0);  // per distinct key: staged (key, count)
     const double dense = 8.0 * c->kw + 8.0;                      // ... and its dense result entry

@@ -129,16 +129,22 @@ def exchange_runs(keys: torch.Tensor, counts: Optional[torch.Tensor], k: int,
         bounds = shared_bounds([keys], k, group)
     bits = hist_bits(k)
     shift = 2 * k - bits
-    # key boundaries of the owners' ranges (first key of each range)
+    # key boundaries of the owners' ranges (first key of each range); a bound
+    # equal to the bin count is +infinity (b << shift would wrap to 0 at k=32)
+    nbins = 1 << bits
     kb = []
     for b in bounds[1:-1]:
-        v = b << shift
+        v = min(b, nbins - 1) << shift
         if v >= 1 << 63:
             v -= 1 << 64
         kb.append(v)
     kb_t = torch.tensor(kb, dtype=torch.int64, device=dev)
-    cuts = torch.searchsorted(_order_view(keys, k), _order_view(kb_t, k), right=False) if world > 1 \
-        else torch.zeros(0, dtype=torch.int64, device=dev)
+    if world > 1:
+        cuts = torch.searchsorted(_order_view(keys, k), _order_view(kb_t, k), right=False)
+        past = torch.tensor([b >= nbins for b in bounds[1:-1]], dtype=torch.bool, device=dev)
+        cuts = torch.where(past, torch.full_like(cuts, keys.numel()), cuts)
+    else:
+        cuts = torch.zeros(0, dtype=torch.int64, device=dev)
     edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts,
                        torch.tensor([keys.numel()], dtype=torch.int64, device=dev)])
     send_sizes = (edges[1:] - edges[:-1]).to(torch.int64)

@@ -110,6 +110,46 @@ def test_merge_with_an_empty_rank(tmp_path):
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
 
 
+def _top_bin_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # k = 32: most keys in the top 16-bit bin (0xFFFF), so an owner bound
+        # equals the bin count (+infinity, not key 0 after a wrap)
+        rng = np.random.default_rng(rank)
+        top = (np.uint64(0xFFFF) << np.uint64(48)) + rng.integers(0, 1 << 40, 900, dtype=np.uint64)
+        low = rng.integers(0, 1 << 60, 10, dtype=np.uint64)
+        keys = np.unique(np.concatenate([top, low]))
+        counts = np.full(len(keys), rank + 1, np.uint64)
+        rk, rc, bounds, rs = okm_dist.exchange_runs(torch.from_numpy(keys.view(np.int64).copy()),
+                                                    torch.from_numpy(counts.view(np.int64).copy()), 32)
+        assert all(s >= 0 for s in rs)
+        mk, mc = _oracle_merge(32)(rk, rc)
+        gk, gc = okm_dist.gather_global(mk, mc)
+        if rank == 0:
+            np.savez(out_path, keys=gk, counts=gc, bounds=np.array(bounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_owner_bound_at_the_top_bin_k32(tmp_path):
+    world = 3
+    out = os.path.join(str(tmp_path), "top.npz")
+    mp.spawn(_top_bin_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    oc = OracleCounter(32)
+    for rank in range(world):
+        rng = np.random.default_rng(rank)
+        top = (np.uint64(0xFFFF) << np.uint64(48)) + rng.integers(0, 1 << 40, 900, dtype=np.uint64)
+        low = rng.integers(0, 1 << 60, 10, dtype=np.uint64)
+        keys = np.unique(np.concatenate([top, low]))
+        oc.add_pairs(keys, np.full(len(keys), rank + 1, np.uint64))
+    ek, ec = oc.result(1)
+    assert int(got["bounds"][-2]) == 1 << 16  # the wrap case is exercised
+    assert np.array_equal(got["keys"], ek) and np.array_equal(got["counts"], ec)
+
+
 def test_owner_ranges_balance_and_cover():
     rng = np.random.default_rng(0)
     hist = rng.integers(0, 1000, 1 << 12)
