@@ -60,6 +60,12 @@ READ_LEN = 150
 GENOME_BP = 100_000_000
 GENOME_SEED = 2
 READ_SEED = 2
+# BASELINE configs[2] (C3): 50 GiB of 150 bp FASTQ = 167,772,160
+# reads = 25,165,824,000 bases from a 1 Gbp genome, seed 3, contiguous 1/P shards
+C3_READS = 167_772_160
+C3_GENOME_BP = 1_000_000_000
+C3_SEED = 3
+C3_BATCH_READS = 4_194_304  # 0.63 Gbases per okm_add_batch_device call
 
 
 def pmc_traffic():
@@ -71,6 +77,44 @@ def pmc_traffic():
         return None, None
     with open(files[-1]) as fh:
         return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
+
+
+def roofline_from_stats(stats, bases_timed):
+    """`roofline` for the dominant kernel (by device time) of a timing pass:
+    its algorithmic bytes per launch / its average HIP-event duration on the
+    engine stream, vs the 8 TB/s HBM peak; `traffic` from the newest committed
+    rocprofv3 PMC summary.  bases_timed: bases the timing pass covered."""
+    roof = None
+    kernels = {}
+    if not stats:
+        return roof, kernels
+    for name, s in stats.items():
+        if s["launches"]:
+            avg = s["total_ms"] / s["launches"]
+            per = s["alg_bytes"] / s["launches"]
+            kernels[name] = {"launches": s["launches"], "avg_ms": round(avg, 4),
+                             "alg_bytes_per_launch": per,
+                             "achieved_GBs": round(per / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
+    dom = max(kernels, key=lambda n: stats[n]["total_ms"])
+    dk = kernels[dom]
+    ach = dk["achieved_GBs"]
+    traffic, tsrc = pmc_traffic()
+    tk = (traffic or {}).get(dom)
+    roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+            "traffic": round(tk["traffic_bytes"]) if tk else None,
+            "traffic_unit": "bytes per launch (HBM, rocprofv3 PMC)",
+            "traffic_source": tsrc if tk else None,
+            "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"],
+            "measured": "HIP events on the engine stream, single-stream pass of the same K steps after the "
+                        "timed region"}
+    if tk:
+        roof["traffic_GBs"] = round(tk["traffic_bytes"] / (dk["avg_ms"] * 1e-3) / 1e9, 1)
+    tot_ms = sum(s["total_ms"] for s in stats.values())
+    tot_bytes = sum(s["alg_bytes"] for s in stats.values())
+    roof["path_achieved_GBs"] = round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1) if tot_ms > 0 else None
+    roof["path_alg_bytes_per_base"] = round(tot_bytes / bases_timed, 2)
+    return roof, kernels
 
 
 def log(*a):
@@ -90,12 +134,22 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--streams", type=int, default=3,
                     help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
+    ap.add_argument("--workload", choices=["c2", "c3"], default=None,
+                    help="c2: BASELINE configs[1] (1 GiB per GPU; default at N=1); c3: BASELINE configs[2] "
+                         "(50 GiB of reads from a 1 Gbp genome sharded 1/N over the ranks; default at N>1)")
+    ap.add_argument("--c3-reads", type=int, default=C3_READS,
+                    help="c3: total reads over all ranks (BASELINE configs[2]: 167,772,160)")
+    ap.add_argument("--batch-reads", type=int, default=C3_BATCH_READS,
+                    help="c3: reads per okm_add_batch_device call")
     return ap.parse_args()
 
 
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    workload = args.workload or ("c2" if world == 1 else "c3")
+    if workload == "c3":
+        return main_c3(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -279,46 +333,11 @@ def main():
     info = ctr.engine_info()
 
     # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) -------
-    cpu = None
+    # plus SURVEY §8(d)'s labelled multi-threaded restatement beside it
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        from oracle import OracleCounter
-        m = min(args.cpu_sample_reads, args.reads)
-        sample = batch[:m * (READ_LEN + 1)]
-        oc = OracleCounter(K)
-        tc = time.perf_counter()
-        oc.add_separated(sample)
-        keys_c, counts_c = oc.result(1)
-        tcpu = time.perf_counter() - tc
-        cpu = {"value": m * READ_LEN / tcpu, "unit": "bases/s", "cores": 1, "kind": "port",
-               "sample": f"first {m} reads ({m * READ_LEN} bases) of the same batch, k=31, "
-                         f"oracle/okm_oracle.c (faithful O(k) encode+rc per window, 1 thread, "
-                         f"count.rs is single-threaded), {tcpu:.1f} s incl. filter+sort"}
-    # a labelled multi-threaded restatement beside it (NOT the
-    # reference's behaviour: count never uses rayon), on the host cores this
-    # process may use (OMP_NUM_THREADS on the box), checked against the engine
-    cpu_mt = None
-    if rank == 0 and world == 1 and args.cpu_sample_reads > 0 and args.cpu_mt_reads > 0:
-        from oracle import count_separated_mt
-        nproc = os.cpu_count() or 1
-        thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or nproc), nproc))
-        m = min(args.cpu_mt_reads, args.reads)
-        sample = batch[:m * (READ_LEN + 1)]
-        tc = time.perf_counter()
-        mk, mc = count_separated_mt(sample, K, thr)
-        tmt = time.perf_counter() - tc
-        with okm.KmerCounter(K, "count", device) as chk:  # the sample on the engine: same table
-            sb = okm.DeviceBuffer(len(sample), device)
-            sb.upload(sample)
-            chk.add_device_batch(sb.address, len(sample))
-            gk, gc = chk.result(1)
-            sb.free()
-        cpu_mt = {"value": m * READ_LEN / tmt, "unit": "bases/s", "threads": thr, "nproc": nproc,
-                  "kind": "restatement-MT (not reference behaviour: count.rs is single-threaded)",
-                  "sample": f"first {m} reads ({m * READ_LEN} bases) of the same batch, k=31, "
-                            f"{thr} shards counted by oracle/okm_oracle.c on {thr} threads + key-range "
-                            f"merge, {tmt:.1f} s",
-                  "engine_table_equal": bool(np.array_equal(mk, gk) and np.array_equal(mc, gc))}
+        cpu, cpu_mt = cpu_baselines(batch, min(args.cpu_sample_reads, args.reads),
+                                    min(args.cpu_mt_reads, args.reads), device, "the same batch")
 
     if rank != 0:
         if dist_on:
@@ -326,36 +345,7 @@ def main():
         return
 
     value = world * bases * args.steps / dt
-    # dominant kernel by device time in the timed region
-    roof = None
-    kernels = {}
-    if stats:
-        for name, s in stats.items():
-            if s["launches"]:
-                avg = s["total_ms"] / s["launches"]
-                per = s["alg_bytes"] / s["launches"]
-                kernels[name] = {"launches": s["launches"], "avg_ms": round(avg, 4),
-                                 "alg_bytes_per_launch": per,
-                                 "achieved_GBs": round(per / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
-        dom = max(kernels, key=lambda n: stats[n]["total_ms"])
-        dk = kernels[dom]
-        ach = dk["achieved_GBs"]
-        traffic, tsrc = pmc_traffic()
-        tk = (traffic or {}).get(dom)
-        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                "traffic": round(tk["traffic_bytes"]) if tk else None,
-                "traffic_unit": "bytes per launch (HBM, rocprofv3 PMC)",
-                "traffic_source": tsrc if tk else None,
-                "avg_ms": dk["avg_ms"], "alg_bytes_per_launch": dk["alg_bytes_per_launch"],
-                "measured": "HIP events on the engine stream, single-stream pass of the same K steps after the "
-                            "timed region"}
-        if tk:
-            roof["traffic_GBs"] = round(tk["traffic_bytes"] / (dk["avg_ms"] * 1e-3) / 1e9, 1)
-        tot_ms = sum(s["total_ms"] for s in stats.values())
-        tot_bytes = sum(s["alg_bytes"] for s in stats.values())
-        roof["path_achieved_GBs"] = round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1) if tot_ms > 0 else None
-        roof["path_alg_bytes_per_base"] = round(tot_bytes / (bases * args.steps), 2)
+    roof, kernels = roofline_from_stats(stats, bases * args.steps)
     # SURVEY §8(d) whole-path roofline: 1 B/base + 16 B per k-mer instance
     kmers = info["kmers"]
     surv_bytes = bases + 16.0 * kmers
@@ -397,6 +387,223 @@ def main():
     if dist_on:
         dist.destroy_process_group()
     dbuf.free()
+
+
+def main_c3(args):
+    """BASELINE configs[2] (C3): 167,772,160 reads (25,165,824,000 bases) of a
+    1 Gbp genome, split into contiguous 1/P shards by read index, one shard
+    per rank, generated on the device (okm_synth_reads_device, the same bytes
+    as the host generator).  One step = the whole job: every rank counts its
+    shard batch by batch into ONE table (count.rs:52-89: one map across all
+    inputs; the engine folds its uncounted batches into a sorted table when
+    they pass 8 % of HBM into sorted tables merged k-way, so memory grows with distinct keys), then at N>1
+    the tables merge by key-range owner over RCCL.  Strong scaling: the total
+    work is fixed, `value` = all ranks' bases / the slowest rank's time."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
+    dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
+    if dist_on:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+        from okm import dist as okm_dist
+
+    total = args.c3_reads
+    r0, r1 = total * rank // world, total * (rank + 1) // world
+    nreads = r1 - r0
+    stride = READ_LEN + 1
+    t0 = time.time()
+    dbuf = okm.DeviceBuffer(max(1, nreads * stride), device)
+    okm.synth_reads_device(dbuf.address, nreads, READ_LEN, genome_len=C3_GENOME_BP, genome_seed=C3_SEED,
+                           seed=C3_SEED, first_read=r0, sub_rate=0.001, n_rate=0.0001, device=device)
+    batches = []
+    for b0 in range(0, nreads, args.batch_reads):
+        b1 = min(nreads, b0 + args.batch_reads)
+        batches.append((b0 * stride, (b1 - b0) * stride))
+    log(f"[rank {rank}] C3 shard: reads [{r0}, {r1}) = {nreads * READ_LEN} bases in {len(batches)} batches, "
+        f"generated on the device ({time.time() - t0:.1f}s)")
+
+    ctr = okm.KmerCounter(K, "count", device)
+    merger = okm.KmerCounter(K, "count", device) if dist_on else None
+    xt = [0.0, 0.0, 0.0]  # count, exchange, merge (wall, this rank)
+
+    def step():
+        tc = time.perf_counter()
+        ctr.reset()
+        for off, nb in batches:
+            ctr.add_device_batch(dbuf.address + off, nb)
+        n = ctr.count()
+        xt[0] += time.perf_counter() - tc
+        if not dist_on:
+            return n
+        tx = time.perf_counter()
+        kp, cp, _ = ctr.result_device()
+        keys = torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda") if n else \
+            torch.empty(0, dtype=torch.int64, device="cuda")
+        counts = torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda") if n else \
+            torch.empty(0, dtype=torch.int64, device="cuda")
+        if backend == "nccl":
+            rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
+            torch.cuda.synchronize()
+        else:
+            rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
+            rk, rc = rk.cuda(), rc.cuda()
+            torch.cuda.synchronize()
+        xt[1] += time.perf_counter() - tx
+        tm = time.perf_counter()
+        merger.reset()
+        off = 0
+        for sz in rs:
+            if sz:
+                merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
+            off += sz
+        n_m = merger.count()
+        merger.synchronize()
+        xt[2] += time.perf_counter() - tm
+        return n_m
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        ctr.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    barrier_sync()
+    xt[:] = [0.0, 0.0, 0.0]
+    t_start = time.perf_counter()
+    n_last = 0
+    for _ in range(args.steps):
+        n_last = step()
+    barrier_sync()
+    dt = time.perf_counter() - t_start
+    info = ctr.engine_info()
+    distinct_global = n_last
+    if dist_on:
+        dev_t = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        nd = torch.tensor([n_last], dtype=torch.int64, device=dev_t)
+        dist.all_reduce(nd, op=dist.ReduceOp.SUM)  # owners' ranges partition the global table
+        distinct_global = int(nd.item())
+    # per-kernel HIP-event timing of the local count: one more step, single stream
+    stats = {}
+    if not args.no_timing:
+        ctr.set_timing(True)
+        ctr.reset()
+        for off, nb in batches:
+            ctr.add_device_batch(dbuf.address + off, nb)
+        ctr.count()
+        stats = ctr.kernel_stats()
+        ctr.set_timing(False)
+
+    cpu = cpu_mt = None
+    if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
+        m = min(args.cpu_sample_reads, nreads)
+        mm = min(max(m, args.cpu_mt_reads), nreads)
+        host = np.empty(mm * stride, dtype=np.uint8)
+        dbuf.download(host)
+        cpu, cpu_mt = cpu_baselines(host, m, min(args.cpu_mt_reads, nreads), device, "the C3 shard")
+
+    if rank != 0:
+        if dist_on:
+            dist.destroy_process_group()
+        return
+    shard_bases = nreads * READ_LEN
+    all_bases = total * READ_LEN
+    value = all_bases * args.steps / dt
+    roof, kernels = roofline_from_stats(stats, shard_bases)
+    kmers = info["kmers"]
+    surv_bytes = shard_bases + 16.0 * kmers
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "bases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1000, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded reads from a random 1 Gbp genome, generated on the device, resident in HBM)",
+        "config": {"workload": f"BASELINE configs[2] (C3): k=31, {total} reads x {READ_LEN} bp = {all_bases} bases "
+                               f"(50 GiB as FASTQ) from a 1 Gbp genome (seed 3), contiguous 1/{world} shard per "
+                               f"GPU counted into one table"
+                               + (", tables merged by key-range owner over RCCL" if dist_on else ""),
+                   "k": K, "reads_total": total, "reads_per_gpu_rank0": nreads, "read_len": READ_LEN,
+                   "genome_bp": C3_GENOME_BP, "batches_per_gpu": len(batches), "batch_reads": args.batch_reads,
+                   "distinct_kmers": distinct_global, "kmer_instances_rank0": int(kmers),
+                   "folds_rank0": int(info.get("folds", 0)), "groups_rank0": int(info.get("groups", 0)),
+                   "parallelism": f"reads sharded x{world}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "cpu_baseline_mt": cpu_mt,
+        "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,
+                            "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
+                            "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
+                            "input_stream_frac": round(shard_bases * args.steps / dt / 8e12, 5)},
+        "phase_ms_per_step_rank0": {"count": round(xt[0] / args.steps * 1e3, 2),
+                                    "exchange": round(xt[1] / args.steps * 1e3, 2),
+                                    "merge": round(xt[2] / args.steps * 1e3, 2)},
+        "kernels": kernels,
+        "engine": info,
+    }
+    print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+    dbuf.free()
+
+
+def cpu_baselines(host, m, m_mt, device, what):
+    """`cpu_baseline` (the C restatement, one thread: count.rs is
+    single-threaded) on the first m reads of `host` and the labelled
+    restatement-MT sample on the first m_mt reads, checked equal to the
+    engine's table of the same sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleCounter, count_separated_mt
+    stride = READ_LEN + 1
+    sample = host[:m * stride]
+    oc = OracleCounter(K)
+    tc = time.perf_counter()
+    oc.add_separated(sample)
+    oc.result(1)
+    tcpu = time.perf_counter() - tc
+    cpu = {"value": m * READ_LEN / tcpu, "unit": "bases/s", "cores": 1, "kind": "port",
+           "sample": f"first {m} reads ({m * READ_LEN} bases) of {what}, k=31, oracle/okm_oracle.c (faithful "
+                     f"O(k) encode+rc per window, 1 thread, count.rs is single-threaded), {tcpu:.1f} s incl. "
+                     f"filter+sort",
+           "note": "the port's open-addressing mix64 map is cheaper than the reference's DashMap + SipHash-1-3 + "
+                   "shard locks (count.rs:31-34), so this likely overstates the reference's own speed"}
+    cpu_mt = None
+    if m_mt > 0:
+        nproc = os.cpu_count() or 1
+        thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or nproc), nproc))
+        sample = host[:m_mt * stride]
+        tc = time.perf_counter()
+        mk, mc = count_separated_mt(sample, K, thr)
+        tmt = time.perf_counter() - tc
+        with okm.KmerCounter(K, "count", device) as chk:
+            sb = okm.DeviceBuffer(len(sample), device)
+            sb.upload(sample)
+            chk.add_device_batch(sb.address, len(sample))
+            gk, gc = chk.result(1)
+            sb.free()
+        cpu_mt = {"value": m_mt * READ_LEN / tmt, "unit": "bases/s", "threads": thr, "nproc": nproc,
+                  "kind": "restatement-MT (not reference behaviour: count.rs is single-threaded)",
+                  "sample": f"first {m_mt} reads ({m_mt * READ_LEN} bases) of {what}, k=31, {thr} shards "
+                            f"counted by oracle/okm_oracle.c on {thr} threads + key-range merge, {tmt:.1f} s",
+                  "engine_table_equal": bool(np.array_equal(mk, gk) and np.array_equal(mc, gc))}
+    return cpu, cpu_mt
 
 
 if __name__ == "__main__":

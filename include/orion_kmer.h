@@ -255,7 +255,7 @@ typedef struct okm_engine_info {
     uint64_t max_partition;  /* largest partition (instances) */
     uint64_t device_bytes;   /* device memory held */
     uint32_t groups;         /* key-range groups counted one after the other (0/1 = one) */
-    uint32_t reserved;
+    uint32_t folds;          /* times the uncounted batches were folded into a sorted table */
 } okm_engine_info;
 okm_status okm_engine_info_get(okm_ctx *ctx, okm_engine_info *info);
 
@@ -357,6 +357,12 @@ void okm_db_free(okm_db *db);
 okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t seed,
                            uint64_t first_read, uint64_t n_reads, uint32_t read_len,
                            double sub_rate, double n_rate, uint8_t *out, int threads);
+/* The same bytes generated on the device into d_out (n_reads*(read_len+1)
+ * bytes of device memory on `device`), without a host copy: BASELINE
+ * configs[2] (C3) shards are made resident this way.  Synchronous. */
+okm_status okm_synth_reads_device(uint64_t genome_seed, uint64_t genome_len, uint64_t seed,
+                                  uint64_t first_read, uint64_t n_reads, uint32_t read_len,
+                                  double sub_rate, double n_rate, uint8_t *d_out, int device);
 
 #ifdef __cplusplus
 }

@@ -22,9 +22,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
+#include "okm_hip_try.h"
 #include "okm_internal.h"
 #include "okm_key.h"
 
@@ -39,29 +41,34 @@ okm_status fail(okm_status s, const std::string &msg) {
     return s;
 }
 
-#define HIP_TRY(expr)                                                                            \
-    do {                                                                                         \
-        hipError_t e_ = (expr);                                                                  \
-        if (e_ != hipSuccess)                                                                    \
-            return fail(e_ == hipErrorOutOfMemory ? OKM_E_NOMEM : OKM_E_DEVICE,                  \
-                        std::string(#expr) + ": " + hipGetErrorString(e_));                      \
-    } while (0)
-
-#define OKM_TRY(expr)                    \
-    do {                                 \
-        okm_status s_ = (expr);          \
-        if (s_ != OKM_OK) return s_;     \
-    } while (0)
-
 // ---------------------------------------------------------------------------
 // Device memory pool (best-fit free list; GB-sized buffers are reused across
 // okm_count calls instead of hipMalloc/hipFree in the hot loop).
 // ---------------------------------------------------------------------------
+struct DevPool;
+static bool pool_trace() {
+    static const bool on = getenv("OKM_POOL_TRACE") != nullptr;
+    return on;
+}
+static std::mutex g_pools_mu;
+static std::vector<DevPool *> g_pools;  // every live context's pool (cross-pool trim on OOM)
+
 struct DevPool {
     std::multimap<size_t, void *> free_;
     std::map<void *, size_t> size_;
     size_t held = 0;
+    int device = 0;
+    std::mutex mu;  // the owning context's thread, or another pool trimming this one on OOM
 
+    void attach(int dev) {
+        device = dev;
+        std::lock_guard<std::mutex> g(g_pools_mu);
+        g_pools.push_back(this);
+    }
+    void detach() {
+        std::lock_guard<std::mutex> g(g_pools_mu);
+        g_pools.erase(std::remove(g_pools.begin(), g_pools.end(), this), g_pools.end());
+    }
     okm_status get(size_t bytes, void **out) {
         bytes = (bytes + 255) & ~size_t(255);
         if (bytes == 0) bytes = 256;
@@ -70,41 +77,94 @@ struct DevPool {
             while ((g << 5) <= bytes) g <<= 1;
             bytes = (bytes + g - 1) & ~(g - 1);
         }
-        auto it = free_.lower_bound(bytes);
-        if (it != free_.end() && it->first <= bytes * 2) {
-            *out = it->second;
-            free_.erase(it);
-            return OKM_OK;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = free_.lower_bound(bytes);
+            // GB-sized requests take a block at most 1/8 larger (a 2x block would strand HBM)
+            const size_t slack = bytes > (size_t(1) << 30) ? bytes / 8 : bytes;
+            if (it != free_.end() && it->first <= bytes + slack) {
+                *out = it->second;
+                if (pool_trace()) fprintf(stderr, "[pool] reuse %zu for %zu held %zu\n", it->first, bytes, held);
+                free_.erase(it);
+                return OKM_OK;
+            }
         }
         void *p = nullptr;
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
-            // release cached blocks and retry once
-            trim();
+            // release cached blocks, largest first, until the block fits (the
+            // rest stay cached for the sizes that come back every step); then
+            // every other pool's on the device
             (void)hipGetLastError();
-            e = hipMalloc(&p, bytes);
-            if (e != hipSuccess)
-                return fail(OKM_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+            size_t freed = 0;
+            while (e != hipSuccess) {
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (free_.empty()) break;
+                    auto big = std::prev(free_.end());
+                    (void)hipFree(big->second);
+                    held -= size_[big->second];
+                    freed += big->first;
+                    size_.erase(big->second);
+                    free_.erase(big);
+                }
+                if (freed + (size_t(256) << 20) < bytes) continue;  // not enough back yet
+                (void)hipGetLastError();
+                e = hipMalloc(&p, bytes);
+            }
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                e = hipMalloc(&p, bytes);
+            }
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                trim_others();
+                e = hipMalloc(&p, bytes);
+            }
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                size_t fr = 0, tot = 0;
+                (void)hipMemGetInfo(&fr, &tot);
+                (void)hipGetLastError();
+                return fail(OKM_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e) +
+                                             " (context holds " + std::to_string(held) + " B in " +
+                                             std::to_string(size_.size()) + " blocks, " + std::to_string(cached()) +
+                                             " B cached; device free " + std::to_string(fr) + " of " +
+                                             std::to_string(tot) + " B)");
+            }
         }
+        std::lock_guard<std::mutex> g(mu);
         size_[p] = bytes;
         held += bytes;
         *out = p;
-        if (getenv("OKM_PROFILE_HOST"))
-            fprintf(stderr, "[okm pool] hipMalloc %zu bytes (held %zu, free blocks %zu)\n", bytes, held, free_.size());
+        if (getenv("OKM_PROFILE_HOST") || pool_trace())
+            fprintf(stderr, "[okm pool] hipMalloc %zu bytes (held %zu, free blocks %zu) %p\n", bytes, held, free_.size(),
+                    p);
         return OKM_OK;
     }
     void put(void *p) {
         if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
         auto it = size_.find(p);
         if (it == size_.end()) return;
+        if (pool_trace()) fprintf(stderr, "[pool] put %zu %p\n", it->second, p);
         free_.emplace(it->second, p);
     }
-    size_t cached() const {
+    size_t size_of(const void *p) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = size_.find(const_cast<void *>(p));
+        return it == size_.end() ? 0 : it->second;
+    }
+    size_t cached() {
+        std::lock_guard<std::mutex> g(mu);
         size_t b = 0;
         for (auto &kv : free_) b += kv.first;
         return b;
     }
+    // hipFree synchronises the device, so a block freed here is idle even if
+    // its owner put it back while its kernels were still queued
     void trim() {
+        std::lock_guard<std::mutex> g(mu);
         for (auto &kv : free_) {
             (void)hipFree(kv.second);
             held -= size_[kv.second];
@@ -112,7 +172,13 @@ struct DevPool {
         }
         free_.clear();
     }
+    void trim_others() {
+        std::lock_guard<std::mutex> g(g_pools_mu);
+        for (DevPool *o : g_pools)
+            if (o != this && o->device == device) o->trim();
+    }
     void release_all() {
+        std::lock_guard<std::mutex> g(mu);
         for (auto &kv : size_) (void)hipFree(kv.first);
         size_.clear();
         free_.clear();
@@ -255,6 +321,7 @@ struct Run {
     uint64_t n = 0;              // keys (sorted runs)
     bool sorted = false;         // strictly ascending unique keys (okm_add_sorted_pairs_device)
     bool borrowed = false;       // caller-owned memory: never returned to the pool
+    bool folded = false;         // a counted table kept as a weighted L1 run (fold(), bins by binary search)
     uint64_t len(uint32_t b) const { return (end.empty() ? off[b + 1] : end[b]) - off[b]; }
 };
 
@@ -294,6 +361,11 @@ struct okm_ctx {
     uint8_t *hpin = nullptr;             // pinned staging of small host->device tables (recycled at sync)
     size_t hpin_used = 0;
     unsigned long long *hres = nullptr;  // pinned landing area of small device->host reads
+
+    // fold: once the uncounted L1 runs hold more than this many bytes, they are
+    // counted and replaced by their sorted table (memory grows with distinct keys)
+    uint64_t fold_bytes = 0;
+    uint32_t folds = 0;
 
     // result
     bool counted = false;
@@ -488,10 +560,129 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     return OKM_OK;
 }
 
+static okm_status do_count(okm_ctx *c);
+
+static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, uint64_t n, double slack);
+static okm_status count_general(okm_ctx *c);
+
+// L1 bin bounds of a sorted run by binary search (a sorted table is already
+// partitioned by key range: nothing moves).
+static okm_status sorted_run_bins(okm_ctx *c, Run &run) {
+    OKM_TRY(ensure_hg(c, c->nbins + 1));
+    launch_bin_bounds(c->stream, run.keys, run.n, c->shift1, c->nbins, c->Hg, c->wide);
+    HIP_TRY(hipGetLastError());
+    run.off.assign(c->nbins + 1, 0);
+    HIP_TRY(hipMemcpyAsync(run.off.data(), c->Hg, (c->nbins + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    return OKM_OK;
+}
+
+// The counted result becomes a folded run: a sorted weighted table owned by
+// the context, at its exact size (the count sized it by its instances).
+static okm_status result_to_folded_run(okm_ctx *c, Run *out) {
+    OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.25));
+    Run run;
+    run.keys = c->res_keys;
+    run.counts = c->res_counts;
+    run.n = c->n_res;
+    run.sorted = true;
+    run.folded = true;
+    c->res_keys = c->res_counts = nullptr;
+    c->n_res = 0;
+    c->counted = false;
+    if (run.n) OKM_TRY(sorted_run_bins(c, run));
+    *out = std::move(run);
+    return OKM_OK;
+}
+
+static void release_runs(okm_ctx *c, std::vector<Run> &runs) {
+    for (auto &r : runs) {
+        if (r.borrowed) continue;
+        c->pool.put(r.keys);
+        c->pool.put(r.counts);
+    }
+    runs.clear();
+}
+
+// Count the context's unsorted runs (batches) alone into one sorted table and
+// keep it, as a folded run, beside the sorted runs already there.
+static okm_status count_unsorted_to_table(okm_ctx *c) {
+    std::vector<Run> keep, batches;
+    for (auto &r : c->runs) (r.sorted ? keep : batches).push_back(std::move(r));
+    c->runs = std::move(batches);
+    c->counted = false;
+    okm_status st = c->runs.empty() ? OKM_OK : count_general(c);
+    Run t;
+    if (st == OKM_OK && !c->runs.empty()) st = result_to_folded_run(c, &t);
+    release_runs(c, c->runs);
+    for (auto &r : keep) c->runs.push_back(std::move(r));
+    if (st != OKM_OK) return st;
+    if (t.n) {
+        c->runs.push_back(std::move(t));
+    } else if (t.keys) {
+        c->pool.put(t.keys);
+        c->pool.put(t.counts);
+    }
+    return OKM_OK;
+}
+
+// Fold (memory bounded by distinct keys, not by input): the batches added
+// since the last fold are counted into a sorted (key, count) table that
+// replaces their L1 runs; every kFoldMergeRuns tables are merged into one
+// (k-way LDS merge, okm_merge.hip).  okm_count merges the tables with the
+// last batches' table.  The reference's DashMap grows with distinct k-mers
+// only (count.rs:48); without folding every batch's instances would stay
+// resident until okm_count.
+static okm_status fold(okm_ctx *c) {
+    OKM_TRY(count_unsorted_to_table(c));
+    c->folds += 1;
+    static const uint32_t merge_runs = [] {
+        const char *e = getenv("OKM_FOLD_MERGE_RUNS");
+        return e ? std::max(2, atoi(e)) : 4;
+    }();
+    uint32_t tables = 0;
+    bool only_folded = true;
+    for (auto &r : c->runs) {
+        tables += r.folded;
+        only_folded &= r.folded;
+    }
+    if (tables >= merge_runs && only_folded) {
+        OKM_TRY(do_count(c));
+        release_runs(c, c->runs);
+        Run t;
+        OKM_TRY(result_to_folded_run(c, &t));
+        if (t.n) c->runs.push_back(std::move(t));
+    }
+    c->hprof.mark("fold");
+    if (c->hprof.on) {
+        uint64_t tb = 0;
+        for (auto &r : c->runs) tb += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
+        fprintf(stderr, "[okm fold] #%u: %zu runs holding %.1f GB; pool held %.1f GB, cached %.1f GB\n", c->folds,
+                c->runs.size(), tb / 1e9, c->pool.held / 1e9, c->pool.cached() / 1e9);
+    }
+    return OKM_OK;
+}
+
+// Fold before a batch of n bytes (<= n windows, 8 B per key word each) would
+// take the uncounted L1 runs past the context's fold threshold.
+static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
+    if (!c->fold_bytes) return OKM_OK;
+    uint64_t held = 0;
+    bool uncounted = false;
+    for (auto &r : c->runs) {
+        if (r.borrowed || r.folded) continue;
+        held += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);  // allocations, not keys
+        uncounted = true;
+    }
+    if (!uncounted || held + n * 8 * c->kw <= c->fold_bytes) return OKM_OK;
+    return fold(c);
+}
+
 // L1 pass over a device-resident batch (whitespace-free records joined by
 // OKM_RECORD_SEPARATOR, 16-byte aligned).
 static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     if (n == 0) return OKM_OK;
+    OKM_TRY(maybe_fold(c, n));
     c->hprof.mark("idle");
     const uint64_t tile = extract_tile();
     uint64_t tiles = (n + tile - 1) / tile;
@@ -780,6 +971,27 @@ static uint32_t log2_floor(uint64_t x) {
     return r;
 }
 
+// Move a (keys, counts) table of n entries into exact-size allocations when
+// its current ones are more than `slack` times larger (bound-sized result
+// tables hold one slot per instance).
+static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, uint64_t n, double slack) {
+    const uint64_t kb = std::max<uint64_t>(n, 1) * 8 * c->kw, cb = std::max<uint64_t>(n, 1) * 8;
+    if ((double)c->pool.size_of(*keys) <= slack * (double)kb + (64u << 20)) return OKM_OK;
+    uint64_t *nk, *nc;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1) * c->kw, &nk));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1), &nc));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(nk, *keys, kb, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(nc, *counts, cb, hipMemcpyDeviceToDevice, c->stream));
+    }
+    OKM_TRY(sync(c));
+    c->pool.put(*keys);
+    c->pool.put(*counts);
+    *keys = nk;
+    *counts = nc;
+    return OKM_OK;
+}
+
 // A result table owned by the caller (key-range groups, do_count): entries
 // go to [off, off + distinct).
 struct ResDst {
@@ -822,7 +1034,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     c->hprof.mark("items.h2d");
     launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
                        d_nitems);
-    c->timer.end(c->stream, "count_items", (weighted ? 16.0 : 8.0) * (double)in_total);  // + output, added below
+    c->timer.end(c->stream, "count_items", (8.0 * c->kw + (weighted ? 8.0 : 0.0)) * (double)in_total);
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
     HIP_TRY(hipGetLastError());
@@ -955,12 +1167,77 @@ static okm_status partition_pairs(okm_ctx *c, const uint64_t *d_keys, const uint
 }
 
 
+// The k-way merge of sorted runs (okm_merge.hip) in two passes: distinct
+// keys per item, exclusive scan, then the merge writes every item's keys and
+// summed counts straight into the exact-size result table (no staging, no
+// compaction).  Releases bufs, d_items and d_segs.
+static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems, uint64_t in_total,
+                                     bool weighted, std::vector<void *> &bufs) {
+    unsigned long long *n_out, *dense_off, *scan_tmp;
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &n_out));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &dense_off));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    for (void *p : {(void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)d_items, (void *)d_segs})
+        bufs.push_back(p);
+    auto release = [&]() {
+        for (void *p : bufs) c->pool.put(p);
+        bufs.clear();
+    };
+    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_merge_items(c->stream, d_items, nitems, d_segs, n_out, nullptr, nullptr, nullptr, c->flag, weighted,
+                       c->wide, false);
+    c->timer.end(c->stream, "merge_count", 8.0 * c->kw * (double)in_total);
+    HIP_TRY(hipGetLastError());
+    launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
+    HIP_TRY(hipGetLastError());
+    unsigned long long *hv = c->hres + 1024;
+    HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    if (hv[1]) {
+        release();
+        return fail(OKM_E_DEVICE, "merge_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    }
+    const uint64_t nd = hv[0];
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    c->timer.begin(c->stream);
+    launch_merge_items(c->stream, d_items, nitems, d_segs, n_out, dense_off, c->res_keys, c->res_counts, c->flag,
+                       weighted, c->wide, true);
+    c->timer.end(c->stream, "merge_write",
+                 (8.0 * c->kw + (weighted ? 8.0 : 0.0)) * (double)in_total + (8.0 * c->kw + 8.0) * (double)nd);
+    HIP_TRY(hipGetLastError());
+    OKM_TRY(sync(c));  // borrowed runs (okm_add_sorted_pairs_device) may be freed once okm_count returns
+    release();
+    c->n_res = nd;
+    c->info.distinct = nd;
+    c->counted = true;
+    c->hprof.mark("merge");
+    return OKM_OK;
+}
+
 // All runs sorted (okm_add_sorted_pairs_device, e.g. the per-rank slices an
 // owner receives in the multi-GPU merge): every L1 part is split into
 // key-range children by binary search in each run — no key moves — and each
 // child is one multi-segment item.  *fallback: a child is still too big for
 // one item (a hot key); the caller takes the partitioning path instead.
+static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra);
+
+// All runs sorted (see count_sorted_plan).  A child above one item's capacity
+// (canonical-key density gradients inside an L1 bin, a dense run) re-plans
+// with one more key bit for every part, up to 4 times, before giving up to
+// the partitioning path.
 static okm_status count_sorted(okm_ctx *c, bool *fallback) {
+    for (uint32_t extra = 0;; ++extra) {
+        OKM_TRY(count_sorted_plan(c, fallback, extra));
+        if (!*fallback || extra == 4) return OKM_OK;
+        c->hprof.mark("sorted.replan");
+    }
+}
+
+static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) {
     *fallback = false;
     const uint32_t R = (uint32_t)c->runs.size();
     const uint64_t item_max = count_item_capacity();
@@ -979,6 +1256,7 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
         uint32_t bits = 0;
         if (len > item_max && c->shift1 > capbits)
             while (bits < 20 && bits < c->shift1 && (len >> bits) > target) ++bits;
+        if (bits) bits = std::min<uint32_t>(std::min<uint32_t>(bits + extra, 20u), c->shift1);
         parts.push_back(DevSortedPart{b, bits, nitems, (uint32_t)parts.size()});
         nitems += 1u << bits;
         in_total += len;
@@ -1038,6 +1316,11 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
         return OKM_OK;
     }
     c->info.max_partition = hf[1];
+    // k-way LDS merge of the runs' sorted slices; the hashing count kernel
+    // only for more runs than one merge workgroup tracks
+    const bool no_merge = getenv("OKM_NO_MERGE_KERNEL") != nullptr;  // A/B and tests
+    const bool merge = !no_merge && R <= merge_max_runs() && item_max <= merge_item_capacity();
+    if (merge) return merge_sorted_items(c, d_items, d_segs, nitems, in_total, weighted, bufs);
     return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
 }
 
@@ -1053,27 +1336,55 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
 static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
                                 const CountPlan &cp);
 
+static okm_status count_general(okm_ctx *c);
+static okm_status count_unsorted_to_table(okm_ctx *c);
+
 static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
     invalidate_result(c);
+    if (c->runs.size() == 1 && c->runs[0].folded) {  // nothing added since the fold: its table is the result
+        Run &r = c->runs[0];
+        c->res_keys = r.keys;
+        c->res_counts = r.counts;
+        c->n_res = r.n;
+        c->info.distinct = r.n;
+        c->runs.clear();
+        c->counted = true;
+        return OKM_OK;
+    }
     bool any_sorted = false, all_sorted = !c->runs.empty();
     for (auto &r : c->runs) {
         any_sorted |= r.sorted;
         all_sorted &= r.sorted;
     }
+    if (any_sorted && !all_sorted) {
+        // sorted tables beside batches: count the batches into one more sorted
+        // table, then merge all of them (no key of a sorted table moves)
+        OKM_TRY(count_unsorted_to_table(c));
+        if (c->runs.size() == 1 && c->runs[0].folded) return do_count(c);
+        all_sorted = !c->runs.empty();
+    }
     if (all_sorted) {
         bool fallback = false;
         OKM_TRY(count_sorted(c, &fallback));
         if (!fallback) return OKM_OK;
-    }
-    if (any_sorted) {  // mixed with unsorted input (or a hot key): partition the sorted runs
+        // a key range too dense for one merge item: partition the sorted runs
         for (auto &r : c->runs) {
-            if (!r.sorted) continue;
             Run owned;
             OKM_TRY(partition_pairs(c, r.keys, r.counts, r.n, owned));
+            if (!r.borrowed) {
+                c->pool.put(r.keys);
+                c->pool.put(r.counts);
+            }
             r = std::move(owned);
         }
     }
+    return count_general(c);
+}
+
+// Every run an L1-partitioned batch (or partitioned pairs): key-range passes
+// + LDS counting + compaction.
+static okm_status count_general(okm_ctx *c) {
     const uint32_t twok = 2u * c->k;
     // sort-mode items hold at most count_item_capacity() instances; items with
     // at most count_dense_bits() remaining key bits are counted by direct
@@ -1328,14 +1639,17 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
                                 const CountPlan &cp) {
     uint64_t total = 0;
     for (const Part &p : parts) total += p.len;
-    const double ws_key = 8.0 * c->kw * 4 + 8.0;  // level + fan-out copy + staging keys (+ slack) + counts
+    // per instance: level + fan-out copy + staged keys (+ slack) + staged counts (+ weights of both levels)
+    const double ws_key = 8.0 * c->kw * 4 + 8.0 + (weighted ? 16.0 : 0.0);
     const double res_key = 8.0 * c->kw + 8.0;     // result entry (instance bound)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
         (void)hipGetLastError();
         free_b = 0;
     }
-    const double avail = 0.9 * (double)(free_b + c->pool.cached());
+    // 3/4 of what is free: sampled capacities, line padding and the pool's size
+    // classes make a pass hold more than its keys
+    const double avail = 0.75 * (double)(free_b + c->pool.cached());
     uint64_t group_keys = total;
     int mode = 0;  // 0: one group (no grouping)
     const char *ge = getenv("OKM_GROUP_KEYS");
@@ -1345,12 +1659,15 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         mode = (gm && gm[0] == 'B') ? 2 : 1;
     } else if ((double)total * (ws_key + res_key) > avail) {
         const double room_a = avail - (double)total * res_key;  // beside a bound-sized table
-        if (room_a >= (double)total * ws_key / 64.0) {
+        // a bound-sized table is only worth it when it is a small share of HBM
+        // (dense inputs such as k=63 long reads); with duplicated keys (a fold
+        // of covered reads) exact per-group tables hold a fraction of it
+        if (room_a >= (double)total * ws_key / 64.0 && (double)total * res_key <= 0.5 * avail) {
             mode = 1;
             group_keys = (uint64_t)(room_a / ws_key);
         } else {
-            mode = 2;
-            group_keys = (uint64_t)(avail / 2.0 / ws_key);
+            mode = 2;  // a bound-sized table per group, plus the finished groups' exact tables
+            group_keys = (uint64_t)(avail * 0.6 / (ws_key + res_key));
         }
         group_keys = std::max<uint64_t>(group_keys, 1);
     }
@@ -1384,6 +1701,9 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         if (mode == 1) {
             d.off += c->n_res;
         } else {
+            // keep the group's table at its exact size: the bound-sized one goes
+            // back to the pool and serves the next group
+            OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.0));
             tabs.push_back(Tab{c->res_keys, c->res_counts, c->n_res});
             c->res_keys = c->res_counts = nullptr;
         }
@@ -1513,6 +1833,14 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins()), 2u * k);
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
+    {
+        // fold threshold: OKM_FOLD_BYTES (tests), else 8 % of the device's memory
+        // (the count of the folded runs needs ~6x their bytes of working set)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) (void)hipGetLastError();
+        const char *fe = getenv("OKM_FOLD_BYTES");
+        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(0.08 * (double)total_b);
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess ||
@@ -1523,6 +1851,7 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
         delete c;
         return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
     }
+    c->pool.attach(device);
     *out = c;
     return OKM_OK;
 }
@@ -1532,6 +1861,7 @@ void okm_destroy(okm_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->timer.destroy();
+    c->pool.detach();
     c->pool.release_all();
     if (c->HC) (void)hipFree(c->HC);
     if (c->Hg) (void)hipFree(c->Hg);
@@ -1563,6 +1893,7 @@ okm_status okm_reset(okm_ctx *c) {
     }
     c->runs.clear();
     c->info = okm_engine_info{};
+    c->folds = 0;
     c->hprof.mark("reset");
     return OKM_OK;
 }
@@ -1640,12 +1971,7 @@ okm_status okm_add_sorted_pairs_device(okm_ctx *c, const uint64_t *d_keys, const
     run.sorted = true;
     run.borrowed = true;
     // L1 bin boundaries by binary search: the run stays where it is
-    OKM_TRY(ensure_hg(c, c->nbins + 1));
-    launch_bin_bounds(c->stream, d_keys, n, c->shift1, c->nbins, c->Hg, c->wide);
-    HIP_TRY(hipGetLastError());
-    run.off.assign(c->nbins + 1, 0);
-    HIP_TRY(hipMemcpyAsync(run.off.data(), c->Hg, (c->nbins + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    OKM_TRY(sync(c));
+    OKM_TRY(sorted_run_bins(c, run));
     c->runs.push_back(std::move(run));
     return OKM_OK;
 }
@@ -1893,6 +2219,7 @@ okm_status okm_kernel_stats(okm_ctx *c, okm_kernel_stat *stats, int cap, int *n)
 okm_status okm_engine_info_get(okm_ctx *c, okm_engine_info *info) {
     if (!c || !info) return fail(OKM_E_ARG, "null argument");
     *info = c->info;
+    info->folds = c->folds;
     info->device_bytes = c->pool.held + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
     return OKM_OK;
 }

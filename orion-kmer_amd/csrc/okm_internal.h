@@ -138,6 +138,18 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
                         const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr);
 
+// k-way merge of sorted runs (okm_merge.hip): items as built by
+// launch_sorted_items (each segment of an item a sorted unique run of keys),
+// at most merge_item_capacity() instances and merge_max_runs() segments per
+// item (else ctl[0] = 3).  write=0: n_out[item] = the item's distinct keys;
+// write=1: its sorted distinct keys and summed u64 counts at
+// out_keys/out_counts + dense_off[item] (the exclusive scan of n_out).
+uint32_t merge_item_capacity();
+uint32_t merge_max_runs();
+void launch_merge_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
+                        unsigned long long *n_out, const unsigned long long *dense_off, uint64_t *out_keys,
+                        uint64_t *out_counts, unsigned long long *ctl, bool weighted, bool wide, bool write);
+
 // A part that took part in a device-side split round: its children are the
 // output bins [out_base, out_base + nlocal) of the round.
 struct DevParent {

@@ -24,7 +24,7 @@ from ._lib import (OKM_E_DEVICE, OKM_E_INVALID_K, OKM_E_IO, OKM_E_PARSE, OKM_E_R
 __all__ = [
     "seq_to_u64", "u64_to_seq", "reverse_complement_u64", "canonical_u64",
     "KmerCounter", "DeviceBuffer", "device_count", "device_arch", "pack_records",
-    "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads",
+    "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads", "synth_reads_device",
     "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
     "KmerSet", "Classifier", "run_query", "run_classify", "read_fastx_records",
 ]
@@ -223,6 +223,16 @@ def synth_reads(n_reads: int, read_len: int = 150, genome_len: int = 100_000_000
     check(lib().okm_synth_reads(genome_seed, genome_len, seed, first_read, n_reads, read_len, sub_rate,
                                 n_rate, out.ctypes.data, threads), "okm_synth_reads")
     return out
+
+
+def synth_reads_device(d_out: int, n_reads: int, read_len: int = 150, genome_len: int = 100_000_000,
+                       genome_seed: int = 2, seed: int = 2, first_read: int = 0, sub_rate: float = 0.001,
+                       n_rate: float = 0.0001, device: int = 0) -> int:
+    """synth_reads' bytes generated straight into device memory at d_out
+    (n_reads * (read_len + 1) bytes); returns that byte count."""
+    check(lib().okm_synth_reads_device(genome_seed, genome_len, seed, first_read, n_reads, read_len, sub_rate,
+                                       n_rate, c_void_p(d_out), device), "okm_synth_reads_device")
+    return n_reads * (read_len + 1)
 
 
 # ---------------------------------------------------------------------------

@@ -55,7 +55,7 @@ class EngineInfo(Structure):
     _fields_ = [("kmers", c_uint64), ("distinct", c_uint64), ("l1_bits", c_uint32),
                 ("l2_bits", c_uint32), ("levels", c_uint32), ("work_items", c_uint32),
                 ("max_partition", c_uint64), ("device_bytes", c_uint64), ("groups", c_uint32),
-                ("reserved", c_uint32)]
+                ("folds", c_uint32)]
 
 
 class Key128(Structure):
@@ -137,6 +137,8 @@ PROTOTYPES = {
                                         _P64]),
     "okm_synth_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                 c_double, c_void_p, c_int]),
+    "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
+                                       c_double, c_void_p, c_int]),
 }
 
 _lib = None

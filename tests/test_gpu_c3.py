@@ -1,0 +1,192 @@
+"""BASELINE configs[2] (C3) on the device: the device read generator, batch
+folding (memory bounded by distinct keys), and one 1/8 shard of C3 at full
+size (20,971,520 reads = 3,145,728,000 bases, the per-GPU share at P=8).
+
+Parity: the device generator is byte-identical to the host generator; a
+folded count equals the unfolded count and the oracle exactly; at full shard
+size, size-independent properties are checked on the device (sum of counts ==
+valid windows, strictly sorted canonical keys, fold invariance), plus exact
+parity with the restatement on a 1,000,000-read sample of the shard.
+count.rs:52-89: one table across all inputs, batches in any grouping.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import okm
+from oracle import OracleCounter, count_separated_mt
+
+pytestmark = pytest.mark.gpu
+
+C3_READS = 167_772_160
+C3_GENOME = 1_000_000_000
+C3_SEED = 3
+
+
+class _View:
+    """__cuda_array_interface__ of engine / okm.DeviceBuffer device memory."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def dev_tensor(ptr, n, typestr="<i8"):
+    if n == 0:
+        return torch.empty(0, dtype=torch.uint8 if typestr == "|u1" else torch.int64, device="cuda")
+    return torch.as_tensor(_View(ptr, n, typestr), device="cuda")
+
+
+def torch_revcomp(v, k):
+    x = ~v
+    for s, m in ((2, 0x3333333333333333), (4, 0x0F0F0F0F0F0F0F0F), (8, 0x00FF00FF00FF00FF),
+                 (16, 0x0000FFFF0000FFFF)):
+        x = ((x >> s) & m) | ((x & m) << s)
+    x = ((x >> 32) & 0xFFFFFFFF) | (x << 32)
+    return (x >> (64 - 2 * k)) & ((1 << (2 * k)) - 1)
+
+
+def device_valid_windows(seq_u8, read_len, k, chunk_reads=1 << 21):
+    """Valid k-windows of a device batch of fixed-stride reads (read_len bases
+    + separator): windows whose bytes are all A/C/G/T (count.rs:28-36)."""
+    stride = read_len + 1
+    n = seq_u8.numel() // stride
+    lut = torch.ones(256, dtype=torch.int32, device="cuda")
+    lut[torch.tensor(list(b"ACGTacgtUu"), device="cuda")] = 0
+    total = 0
+    for r0 in range(0, n, chunk_reads):
+        r1 = min(n, r0 + chunk_reads)
+        rows = seq_u8[r0 * stride:r1 * stride].view(r1 - r0, stride)[:, :read_len]
+        bad = lut[rows.long()]
+        c = torch.nn.functional.pad(torch.cumsum(bad, dim=1, dtype=torch.int32), (1, 0))
+        total += int(((c[:, k:] - c[:, :-k]) == 0).sum().item())
+    return total
+
+
+@pytest.mark.parametrize("n_reads,read_len,first,glen,sub,nr", [
+    (10_000, 150, 0, 100_000_000, 0.001, 0.0001),
+    (7_777, 150, 123_456_789, C3_GENOME, 0.001, 0.0001),
+    (3_001, 15, 5, 1_000, 0.05, 0.02),     # 16-byte thread spans more than two reads
+    (513, 1_000, 9, 10_000, 0.0, 0.0),
+])
+def test_synth_device_matches_host(n_reads, read_len, first, glen, sub, nr):
+    host = okm.synth_reads(n_reads, read_len, genome_len=glen, genome_seed=C3_SEED, seed=7, first_read=first,
+                           sub_rate=sub, n_rate=nr)
+    buf = okm.DeviceBuffer(len(host))
+    okm.synth_reads_device(buf.address, n_reads, read_len, genome_len=glen, genome_seed=C3_SEED, seed=7,
+                           first_read=first, sub_rate=sub, n_rate=nr)
+    dev = np.empty_like(host)
+    buf.download(dev)
+    buf.free()
+    assert np.array_equal(dev, host)
+
+
+def test_fold_equals_unfolded_and_oracle(monkeypatch):
+    k = 31
+    batches = [okm.synth_reads(150_000, 150, genome_len=2_000_000, genome_seed=5, seed=5, first_read=i * 150_000)
+               for i in range(6)]
+    ref = OracleCounter(k)
+    for b in batches:
+        ref.add_separated(b)
+    ek, ec = ref.result(1)
+    tables = {}
+    for fold_bytes in (None, 300_000_000, 1):
+        if fold_bytes is None:
+            monkeypatch.delenv("OKM_FOLD_BYTES", raising=False)
+        else:
+            monkeypatch.setenv("OKM_FOLD_BYTES", str(fold_bytes))
+        with okm.KmerCounter(k) as ctr:
+            for b in batches:
+                buf = okm.DeviceBuffer(len(b))
+                buf.upload(b)
+                ctr.add_device_batch(buf.address, len(b))
+                buf.free()  # consumed before the call returned
+            gk, gc = ctr.result(1)
+            info = ctr.engine_info()
+            # min_count filter over a folded table (count.rs:110)
+            fk, fc = ctr.result(3)
+        tables[fold_bytes] = info["folds"]
+        assert np.array_equal(gk, ek) and np.array_equal(gc, ec), f"fold_bytes={fold_bytes}"
+        sel = ec >= 3
+        assert np.array_equal(fk, ek[sel]) and np.array_equal(fc, ec[sel])
+        assert info["kmers"] == int(ec.sum())
+    assert tables[None] == 0 and tables[300_000_000] >= 1 and tables[1] == len(batches) - 1
+
+
+def test_fold_then_nothing_added(monkeypatch):
+    # a fold followed by count with no new batch: the folded table is the result
+    monkeypatch.setenv("OKM_FOLD_BYTES", "1")
+    k = 21
+    b = okm.synth_reads(50_000, 150, genome_len=500_000, seed=9)
+    ref = OracleCounter(k)
+    ref.add_separated(b)
+    ref.add_separated(b)
+    ek, ec = ref.result(1)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records([bytes(r) for r in b.tobytes().split(b"\n") if r], normalized=True)
+        ctr.add_records([bytes(r) for r in b.tobytes().split(b"\n") if r], normalized=True)
+        n1 = ctr.count()
+        gk, gc = ctr.result(1)
+        assert ctr.engine_info()["folds"] == 1
+        # count again (idempotent) and reset
+        assert ctr.count() == n1
+        ctr.reset()
+        assert ctr.count() == 0
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_c3_shard_full_size(monkeypatch):
+    """Rank 0's shard of C3 at P=8 (bench.py --workload c3 --gpus 8)."""
+    k, read_len = 31, 150
+    world, rank = 8, 0
+    r0, r1 = C3_READS * rank // world, C3_READS * (rank + 1) // world
+    n = r1 - r0
+    stride = read_len + 1
+    buf = okm.DeviceBuffer(n * stride)
+    okm.synth_reads_device(buf.address, n, read_len, genome_len=C3_GENOME, genome_seed=C3_SEED, seed=C3_SEED,
+                           first_read=r0, sub_rate=0.001, n_rate=0.0001)
+    batch_reads = 4_194_304
+    spans = [(b0 * stride, (min(n, b0 + batch_reads) - b0) * stride) for b0 in range(0, n, batch_reads)]
+    results = []
+    ctrs = []
+    for fold_bytes in (0, 6_000_000_000):  # 0: folding off
+        monkeypatch.setenv("OKM_FOLD_BYTES", str(fold_bytes))
+        ctr = okm.KmerCounter(k)
+        for off, nb in spans:
+            ctr.add_device_batch(buf.address + off, nb)
+        nd = ctr.count()
+        kp, cp, nn = ctr.result_device()
+        assert nn == nd
+        results.append((dev_tensor(kp, nd), dev_tensor(cp, nd), ctr.engine_info()))
+        ctrs.append(ctr)  # keeps the device table alive
+    (keys, counts, info), (fk, fc, finfo) = results
+    assert finfo["folds"] >= 1 and info["folds"] == 0
+    assert torch.equal(keys, fk) and torch.equal(counts, fc), "fold invariance"
+    seq = dev_tensor(buf.address, n * stride, "|u1")
+    vw = device_valid_windows(seq, read_len, k)
+    assert int(counts.sum().item()) == vw == info["kmers"]
+    assert bool((keys[1:] > keys[:-1]).all().item()), "strictly increasing (count.rs:119)"
+    assert bool((keys >= 0).all().item()) and bool((keys < (1 << 62)).all().item())
+    assert bool((counts >= 1).all().item())
+    for o in range(0, keys.numel(), 1 << 27):
+        kk = keys[o:o + (1 << 27)]
+        assert bool((kk <= torch_revcomp(kk, k)).all().item()), "canonical (kmer.rs:99-106)"
+    # a 1/P shard of a 1 Gbp genome at ~3.1x coverage: ~1e9 distinct
+    assert 0.7e9 < info["distinct"] < 1.3e9
+    del keys, counts, fk, fc, results
+    for c in ctrs:
+        c.close()
+    # exact parity on the first 1,000,000 reads of the shard (sharded restatement)
+    m = 1_000_000
+    host = np.empty(m * stride, dtype=np.uint8)
+    buf.download(host)
+    thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+    ek, ec = count_separated_mt(host, k, thr)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_device_batch(buf.address, m * stride)
+        gk, gc = ctr.result(1)
+    buf.free()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)

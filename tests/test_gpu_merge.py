@@ -1,0 +1,133 @@
+"""The k-way LDS merge of sorted runs (okm_merge.hip) behind
+okm_add_sorted_pairs_device: the multi-GPU owner's merge of per-rank slices
+(SURVEY.md §8(e)), set unions (compare.rs:51-66, db_types.rs:43-53) and
+folded batch tables (count.rs:52-89).  Exact against numpy, for u64 and
+128-bit keys, weighted and unweighted runs, many runs, dense key ranges, and
+against the hashing count kernel (OKM_NO_MERGE_KERNEL=1)."""
+
+import numpy as np
+import pytest
+
+import okm
+
+pytestmark = pytest.mark.gpu
+
+
+def _upload(arr):
+    arr = np.ascontiguousarray(arr, dtype=np.uint64)
+    buf = okm.DeviceBuffer(max(arr.nbytes, 8))
+    if arr.nbytes:
+        buf.upload(arr)
+    return buf
+
+
+def _expected(runs, weighted):
+    keys = np.concatenate([r[0] for r in runs])
+    w = np.concatenate([r[1] if weighted else np.ones(len(r[0]), np.uint64) for r in runs])
+    u, inv = np.unique(keys, return_inverse=True)
+    s = np.zeros(len(u), np.uint64)
+    np.add.at(s, inv, w)
+    return u, s
+
+
+def _runs(rng, nruns, n, span, k):
+    out = []
+    for _ in range(nruns):
+        m = int(rng.integers(0, n + 1))
+        keys = np.unique(rng.integers(0, span, m, dtype=np.uint64))
+        # canonical-looking: any value below 4^k is a valid key for the engine
+        keys = keys[keys < (np.uint64(1) << np.uint64(2 * k))] if k < 32 else keys
+        counts = rng.integers(1, 1000, len(keys)).astype(np.uint64)
+        out.append((keys, counts))
+    return out
+
+
+@pytest.mark.parametrize("nruns,n,span,weighted", [
+    (2, 200_000, 1 << 40, True),
+    (8, 300_000, 1 << 30, True),        # heavy overlap between runs
+    (20, 50_000, 1 << 24, False),       # dense key range, sets (unions)
+    (64, 20_000, 1 << 22, True),        # the most runs one merge item tracks
+    (70, 10_000, 1 << 22, True),        # more: the hashing count kernel takes over
+])
+def test_merge_runs_vs_numpy(nruns, n, span, weighted):
+    rng = np.random.default_rng(nruns * 7 + n)
+    k = 31
+    runs = _runs(rng, nruns, n, span, k)
+    ek, ec = _expected(runs, weighted)
+    bufs = []
+    with okm.KmerCounter(k) as m:
+        for keys, counts in runs:
+            bk = _upload(keys)
+            bc = _upload(counts) if weighted else None
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address if bc else None, len(keys))
+        gk, gc = m.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_merge_kernel_equals_count_kernel(monkeypatch):
+    # keys spread over the 2k-bit space like canonical k-mers: the work list
+    # splits key ranges by key bits, so the merge kernel takes every item
+    # (keys crowded into a sliver of the space fall back to the partition path,
+    # still exact: the 1 << 24 / 1 << 22 cases above)
+    rng = np.random.default_rng(5)
+    runs = _runs(rng, 6, 400_000, 1 << 62, 31)
+    out = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("OKM_NO_MERGE_KERNEL", "1")
+        bufs = []
+        with okm.KmerCounter(31) as m:
+            m.set_timing(True)
+            for keys, counts in runs:
+                bk, bc = _upload(keys), _upload(counts)
+                bufs += [bk, bc]
+                m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
+            out.append(m.result(1))
+            names = set(m.kernel_stats())
+        assert ("merge_write" in names) == (env is None)
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+def test_merge_wide_keys():
+    rng = np.random.default_rng(11)
+    k = 45
+    runs = []
+    for _ in range(5):
+        m = 100_000
+        hi = rng.integers(0, 1 << 20, m, dtype=np.uint64)
+        lo = rng.integers(0, 1 << 62, m, dtype=np.uint64)
+        v = np.unique(hi.astype(object) * (1 << 64) + lo.astype(object))
+        keys = np.array([[int(x) & ((1 << 64) - 1), int(x) >> 64] for x in v], dtype=np.uint64)
+        runs.append((keys, rng.integers(1, 50, len(keys)).astype(np.uint64)))
+    allk = {}
+    for keys, counts in runs:
+        for (lo, hi), c in zip(keys.tolist(), counts.tolist()):
+            key = (hi << 64) | lo
+            allk[key] = allk.get(key, 0) + c
+    bufs = []
+    with okm.KmerCounter(k, wide=True) as m:
+        for keys, counts in runs:
+            bk, bc = _upload(keys.reshape(-1)), _upload(counts)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(counts))
+        gk, gc = m.result(1)
+    got = dict(zip(okm.keys128_to_int(gk), gc.tolist()))
+    assert got == allk
+    assert okm.keys128_to_int(gk) == sorted(allk)
+
+
+def test_merge_hot_range_many_runs():
+    # every run holds the same dense block of keys: items split down to key
+    # ranges of a few keys x 64 runs
+    base = np.arange(100_000, dtype=np.uint64) + np.uint64(12345)
+    runs = [(base, np.full(len(base), i + 1, np.uint64)) for i in range(64)]
+    bufs = []
+    with okm.KmerCounter(31) as m:
+        for keys, counts in runs:
+            bk, bc = _upload(keys), _upload(counts)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
+        gk, gc = m.result(1)
+    assert np.array_equal(gk, base)
+    assert (gc == np.uint64(64 * 65 // 2)).all()

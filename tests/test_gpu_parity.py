@@ -22,7 +22,7 @@ import okm
 import restate as R
 from conftest import case_file_bytes, materialize
 from okm import _lib
-from oracle import OracleCounter
+from oracle import OracleCounter, count_separated_mt
 
 pytestmark = pytest.mark.gpu
 
@@ -375,15 +375,11 @@ def test_full_size_properties():
     assert int(counts.sum()) == valid_windows(batch, k) == info["kmers"]
     assert_table_invariants(keys, counts, k)
     assert np.array_equal(keys, k2) and np.array_equal(counts, c2), "determinism"
-    # exact parity on a prefix sample against the oracle
-    m = 150_000
-    oc = OracleCounter(k)
-    oc.add_separated(batch[:m * 151])
-    with okm.KmerCounter(k) as ctr:
-        ctr.add_records([bytes(r) for r in batch[:m * 151].tobytes().split(b"\n") if r], normalized=True)
-        gk, gc = ctr.result(1)
-    ek, ec = oc.result(1)
-    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    # exact parity of the WHOLE table against the restatement (sharded over
+    # the host cores and merged by key range, oracle.count_separated_mt)
+    thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+    ek, ec = count_separated_mt(batch, k, thr)
+    assert np.array_equal(keys, ek) and np.array_equal(counts, ec)
 
 
 def _upload(arr):
