@@ -121,6 +121,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# stdout carries exactly ONE JSON line (the driver's contract): whatever
+# libraries print there (RCCL's version banner, gloo's peer count) goes to
+# stderr; emit() writes the line to the saved stdout
+_STDOUT_FD = os.dup(1)
+os.dup2(2, 1)
+
+
+def emit(out):
+    sys.stdout.flush()
+    os.write(_STDOUT_FD, (json.dumps(out) + "\n").encode())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +151,8 @@ def parse():
                          "(50 GiB of reads from a 1 Gbp genome sharded 1/N over the ranks; default at N>1)")
     ap.add_argument("--c3-reads", type=int, default=C3_READS,
                     help="c3: total reads over all ranks (BASELINE configs[2]: 167,772,160)")
+    ap.add_argument("--c3-genome-bp", type=int, default=C3_GENOME_BP,
+                    help="c3: genome size (BASELINE configs[2]: 1 Gbp; smaller values for A/B runs)")
     ap.add_argument("--batch-reads", type=int, default=C3_BATCH_READS,
                     help="c3: reads per okm_add_batch_device call")
     return ap.parse_args()
@@ -383,7 +397,7 @@ def main():
         out["config"]["owned_distinct_rank0"] = int(n_owned)
         out["exchange_ms_per_step_rank0"] = {"exchange": round(xt[0] / args.steps * 1e3, 3),
                                              "merge": round(xt[1] / args.steps * 1e3, 3)}
-    print(json.dumps(out), flush=True)
+    emit(out)
     if dist_on:
         dist.destroy_process_group()
     dbuf.free()
@@ -404,14 +418,23 @@ def main_c3(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
+    # product path: the library's own RCCL communicator (okm_comm, okm_merge_owned:
+    # HIP pack/unpack kernels + grouped ncclSend/ncclRecv over xGMI); torch.distributed
+    # (gloo, host) only hands out the communicator id, barriers and the max-time
+    # reduce.  OKM_BENCH_BACKEND=gloo rehearses the exchange through torch on one
+    # GPU instead (RCCL refuses two ranks on one device).
     backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
+    comm = None
     if dist_on:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
         from okm import dist as okm_dist
+        if backend == "nccl":
+            uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
+            dist.broadcast(uid, 0)
+            comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
 
     total = args.c3_reads
     r0, r1 = total * rank // world, total * (rank + 1) // world
@@ -419,7 +442,7 @@ def main_c3(args):
     stride = READ_LEN + 1
     t0 = time.time()
     dbuf = okm.DeviceBuffer(max(1, nreads * stride), device)
-    okm.synth_reads_device(dbuf.address, nreads, READ_LEN, genome_len=C3_GENOME_BP, genome_seed=C3_SEED,
+    okm.synth_reads_device(dbuf.address, nreads, READ_LEN, genome_len=args.c3_genome_bp, genome_seed=C3_SEED,
                            seed=C3_SEED, first_read=r0, sub_rate=0.001, n_rate=0.0001, device=device)
     batches = []
     for b0 in range(0, nreads, args.batch_reads):
@@ -429,7 +452,9 @@ def main_c3(args):
         f"generated on the device ({time.time() - t0:.1f}s)")
 
     ctr = okm.KmerCounter(K, "count", device)
-    merger = okm.KmerCounter(K, "count", device) if dist_on else None
+    # the owner's merge reuses the counting context (okm_merge_owned allows
+    # owner == local): one device pool per rank, no cross-context trimming
+    merger = (ctr if comm is not None else okm.KmerCounter(K, "count", device)) if dist_on else None
     xt = [0.0, 0.0, 0.0]  # count, exchange, merge (wall, this rank)
 
     def step():
@@ -441,19 +466,21 @@ def main_c3(args):
         xt[0] += time.perf_counter() - tc
         if not dist_on:
             return n
+        if comm is not None:
+            n_m = comm.merge_owned(ctr, merger)
+            t = comm.last_times()
+            xt[1] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
+            xt[2] += t["merge_ms"] * 1e-3
+            return n_m
         tx = time.perf_counter()
         kp, cp, _ = ctr.result_device()
         keys = torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda") if n else \
             torch.empty(0, dtype=torch.int64, device="cuda")
         counts = torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda") if n else \
             torch.empty(0, dtype=torch.int64, device="cuda")
-        if backend == "nccl":
-            rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
-            torch.cuda.synchronize()
-        else:
-            rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
-            rk, rc = rk.cuda(), rc.cuda()
-            torch.cuda.synchronize()
+        rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)  # gloo rehearsal
+        rk, rc = rk.cuda(), rc.cuda()
+        torch.cuda.synchronize()
         xt[1] += time.perf_counter() - tx
         tm = time.perf_counter()
         merger.reset()
@@ -487,7 +514,7 @@ def main_c3(args):
     info = ctr.engine_info()
     distinct_global = n_last
     if dist_on:
-        dev_t = "cuda" if backend == "nccl" else "cpu"
+        dev_t = "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -514,6 +541,8 @@ def main_c3(args):
         cpu, cpu_mt = cpu_baselines(host, m, min(args.cpu_mt_reads, nreads), device, "the C3 shard")
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         if dist_on:
             dist.destroy_process_group()
         return
@@ -541,7 +570,7 @@ def main_c3(args):
                                f"GPU counted into one table"
                                + (", tables merged by key-range owner over RCCL" if dist_on else ""),
                    "k": K, "reads_total": total, "reads_per_gpu_rank0": nreads, "read_len": READ_LEN,
-                   "genome_bp": C3_GENOME_BP, "batches_per_gpu": len(batches), "batch_reads": args.batch_reads,
+                   "genome_bp": args.c3_genome_bp, "batches_per_gpu": len(batches), "batch_reads": args.batch_reads,
                    "distinct_kmers": distinct_global, "kmer_instances_rank0": int(kmers),
                    "folds_rank0": int(info.get("folds", 0)), "groups_rank0": int(info.get("groups", 0)),
                    "parallelism": f"reads sharded x{world}"},
@@ -552,13 +581,17 @@ def main_c3(args):
                             "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
                             "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
                             "input_stream_frac": round(shard_bases * args.steps / dt / 8e12, 5)},
+        "exchange_impl": ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, k-way LDS merge)"
+                          if comm is not None else ("torch gloo rehearsal" if dist_on else None)),
         "phase_ms_per_step_rank0": {"count": round(xt[0] / args.steps * 1e3, 2),
                                     "exchange": round(xt[1] / args.steps * 1e3, 2),
                                     "merge": round(xt[2] / args.steps * 1e3, 2)},
         "kernels": kernels,
         "engine": info,
     }
-    print(json.dumps(out), flush=True)
+    emit(out)
+    if comm is not None:
+        comm.close()
     if dist_on:
         dist.destroy_process_group()
     dbuf.free()

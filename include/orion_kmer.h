@@ -52,7 +52,7 @@ typedef enum okm_status {
     OKM_E_INVALID_K = 1,   /* errors.rs:6 InvalidKmerSize */
     OKM_E_NOMEM = 2,       /* host or device allocation failed */
     OKM_E_DEVICE = 3,      /* no usable GPU / HIP runtime error */
-    OKM_E_COMM = 4,        /* reserved (multi-GPU exchange) */
+    OKM_E_COMM = 4,        /* multi-GPU exchange: RCCL missing or failed */
     OKM_E_ARG = 5,         /* bad argument (null pointer, bad length ...) */
     OKM_E_OVERFLOW = 6,    /* capacity exceeded (caller buffer too small) */
     OKM_E_IO = 7,          /* file open/read/write failed */
@@ -227,6 +227,45 @@ void okm_classifier_destroy(okm_classifier *c);
 okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, const uint64_t *ref_offsets,
                                    uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
                                    uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth);
+
+/* ------------------------------------------------------------------------
+ * Multi-GPU — replaces nothing in the reference (its count
+ * is one process on one map, count.rs:48); it is how ONE table spans several
+ * GPUs: reads shard by record, every rank counts its shard into its own
+ * context, and okm_merge_owned turns the P local tables into the global one
+ * over RCCL (xGMI).  Value-range ownership: rank r ends up holding a
+ * contiguous key range, so ranks 0..P-1 concatenated are the sorted global
+ * table of count.rs:106-119 with no final merge.
+ * ---------------------------------------------------------------------- */
+typedef struct okm_comm okm_comm;
+#define OKM_COMM_ID_BYTES 128
+/* A new communicator id (ncclGetUniqueId) for okm_comm_init_rank; rank 0
+ * creates it and the caller hands the bytes to every rank (MPI, a file,
+ * torch.distributed ...). */
+okm_status okm_comm_unique_id(uint8_t *id /* OKM_COMM_ID_BYTES */);
+/* One rank per process, on HIP device `device` (ncclCommInitRank). */
+okm_status okm_comm_init_rank(okm_comm **out, int nranks, int rank, const uint8_t *id, int device);
+/* Every rank in this process, rank i on devices[i] (NULL: device i)
+ * (ncclCommInitAll); out has n entries.  Each rank's calls then run on a host
+ * thread of its own. */
+okm_status okm_comm_init_all(okm_comm **out, int n, const int *devices);
+void okm_comm_destroy(okm_comm *comm);
+int okm_comm_rank(const okm_comm *comm);
+int okm_comm_size(const okm_comm *comm);
+/* Collective over every rank of `comm`: `local` (counted or not) holds this
+ * rank's shard; afterwards `owner` (reset first) holds this rank's key range
+ * of the union of all ranks' tables, counted and sorted, and *n_owned its
+ * distinct keys.  local, owner and comm share one device; k <= 32; owner may
+ * be local itself (its table is only read until the exchange completes).
+ * Set-mode contexts exchange keys only (build.rs / compare.rs sets). */
+okm_status okm_merge_owned(okm_ctx *local, okm_comm *comm, okm_ctx *owner, uint64_t *n_owned);
+/* Host wall ms of the last okm_merge_owned: [0] plan (histogram, all-reduce,
+ * sizes), [1] exchange (pack + send/recv + unpack), [2] reserved, [3] owner merge. */
+okm_status okm_comm_last_times(const okm_comm *comm, double *ms4);
+/* The owner split (host, no device): bounds[0] = 0 <= ... <= bounds[world] =
+ * nbins, rank r owns histogram bins [bounds[r], bounds[r+1]), cut where the
+ * running total first reaches r/world of the whole. */
+okm_status okm_owner_bounds(const uint64_t *hist, uint32_t nbins, int world, uint32_t *bounds);
 
 /* ------------------------------------------------------------------------
  * Instrumentation (bench.py measures kernels with HIP events on the

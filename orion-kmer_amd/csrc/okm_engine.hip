@@ -80,8 +80,8 @@ struct DevPool {
         {
             std::lock_guard<std::mutex> g(mu);
             auto it = free_.lower_bound(bytes);
-            // GB-sized requests take a block at most 1/8 larger (a 2x block would strand HBM)
-            const size_t slack = bytes > (size_t(1) << 30) ? bytes / 8 : bytes;
+            // GB-sized requests take a block at most 1/4 larger (a 2x block would strand HBM)
+            const size_t slack = bytes > (size_t(1) << 30) ? bytes / 4 : bytes;
             if (it != free_.end() && it->first <= bytes + slack) {
                 *out = it->second;
                 if (pool_trace()) fprintf(stderr, "[pool] reuse %zu for %zu held %zu\n", it->first, bytes, held);
@@ -92,6 +92,18 @@ struct DevPool {
         void *p = nullptr;
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
+            // HBM is full: any larger cached block beats freeing and re-mapping
+            // (hipFree + hipMalloc of tens of GB costs hundreds of ms per step)
+            (void)hipGetLastError();
+            {
+                std::lock_guard<std::mutex> g(mu);
+                auto it = free_.lower_bound(bytes);
+                if (it != free_.end()) {
+                    *out = it->second;
+                    free_.erase(it);
+                    return OKM_OK;
+                }
+            }
             // release cached blocks, largest first, until the block fits (the
             // rest stay cached for the sizes that come back every step); then
             // every other pool's on the device
@@ -366,6 +378,7 @@ struct okm_ctx {
     // counted and replaced by their sorted table (memory grows with distinct keys)
     uint64_t fold_bytes = 0;
     uint32_t folds = 0;
+    double l1_ratio = 0;  // largest windows-per-byte ratio of a batch so far (L1 run sizing)
 
     // result
     bool counted = false;
@@ -378,6 +391,8 @@ namespace okm {
 
 int ctx_device(const okm_ctx *c) { return c->device; }
 bool ctx_is_wide(const okm_ctx *c) { return c->wide; }
+uint32_t ctx_k(const okm_ctx *c) { return c->k; }
+bool ctx_is_set(const okm_ctx *c) { return c->mode == OKM_MODE_SET; }
 
 static okm_status ensure_hc(okm_ctx *c, size_t n_u32) {
     if (n_u32 <= c->HC_cap) return OKM_OK;
@@ -508,8 +523,13 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     const double scale = (double)n / (double)sbytes;
     const char *dbg = getenv("OKM_L1_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
     const double mul = dbg ? atof(dbg) : 1.0;
-    // sum_b scale s_b <= n (windows <= bytes); sum_b sqrt(s_b) <= sqrt(nb * sbytes)
-    const uint64_t limit = (uint64_t)(1.01 * ((double)n + 6.0 * scale * std::sqrt((double)nb * (double)sbytes) +
+    // sum_b scale s_b <= w n (windows <= bytes; w = the windows-per-byte ratio
+    // seen so far on this context, 1 before the first batch: the run is sized
+    // for the keys it gets, not for the bytes); sum_b sqrt(s_b) <= sqrt(nb * w * sbytes).
+    // A batch with more windows than that overflows its sampled placement and
+    // is redone exactly (correct, just slower).
+    const double w = c->l1_ratio > 0 ? std::min(1.0, c->l1_ratio * 1.02 + 0.002) : 1.0;
+    const uint64_t limit = (uint64_t)(1.01 * (w * (double)n + 6.0 * scale * std::sqrt((double)nb * w * (double)sbytes) +
                                               9.0 * scale * nb) +
                                       (double)nb * (256.0 + align)) + 64;
     OKM_TRY(ensure_hg(c, nb));
@@ -549,6 +569,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
         run.end[b] = (ends[b] + align - 1) / align * align;
     }
     c->timer.add_bytes("extract_scatter", 8.0 * c->kw * (double)total);
+    c->l1_ratio = std::max(c->l1_ratio, (double)total / (double)n);
     *placed = true;
     if (total == 0) {
         c->pool.put(run.keys);
@@ -666,7 +687,7 @@ static okm_status fold(okm_ctx *c) {
 // Fold before a batch of n bytes (<= n windows, 8 B per key word each) would
 // take the uncounted L1 runs past the context's fold threshold.
 static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
-    if (!c->fold_bytes) return OKM_OK;
+    if (!c->fold_bytes) return OKM_OK;  // OKM_FOLD_BYTES=0: folding off
     uint64_t held = 0;
     bool uncounted = false;
     for (auto &r : c->runs) {
@@ -674,7 +695,21 @@ static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
         held += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);  // allocations, not keys
         uncounted = true;
     }
-    if (!uncounted || held + n * 8 * c->kw <= c->fold_bytes) return OKM_OK;
+    const double w = c->l1_ratio > 0 ? std::min(1.0, c->l1_ratio * 1.03) : 1.0;
+    // ... and never more than OKM_FOLD_MAX_KEYS instances in one fold (0 / unset:
+    // no cap; the byte threshold bounds it; C3 on one GPU: 5-batch folds of
+    // 2.5 G instances 816 ms per job, 4-batch folds 1006 ms)
+    static const uint64_t kFoldMaxKeys = [] {
+        const char *e = getenv("OKM_FOLD_MAX_KEYS");
+        return e && atoll(e) > 0 ? (uint64_t)atoll(e) : ~0ull;
+    }();
+    uint64_t keys = 0;
+    for (auto &r : c->runs)
+        if (!r.borrowed && !r.folded && !r.off.empty())
+            for (uint32_t b = 0; b + 1 < r.off.size(); ++b) keys += r.len(b);
+    if (!uncounted) return OKM_OK;
+    if (held + (uint64_t)(w * (double)n) * 8 * c->kw <= c->fold_bytes && keys + (uint64_t)(w * (double)n) <= kFoldMaxKeys)
+        return OKM_OK;
     return fold(c);
 }
 
@@ -708,6 +743,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     Run run;
     uint64_t total = 0;  // bins start on 128-B lines; slot tails hold the empty key
     OKM_TRY(hist_to_offsets(c, c->nbins, run.off, 16 / c->kw, &total));
+    c->l1_ratio = std::max(c->l1_ratio, (double)total / (double)n);
     c->hprof.mark("l1.hist+sync");
     if (total == 0) return OKM_OK;
     OKM_TRY(pool_get(c->pool, run.off.back() * c->kw, &run.keys));
@@ -1242,7 +1278,9 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     const uint32_t R = (uint32_t)c->runs.size();
     const uint64_t item_max = count_item_capacity();
     const uint32_t capbits = count_dense_bits();
-    const uint64_t target = item_max * 3 / 4;
+    // children by key bits: half an item on average, so the density gradient
+    // inside an L1 bin of canonical keys stays below one item
+    const uint64_t target = item_max / 2;
     bool weighted = false;
     for (auto &r : c->runs) weighted |= r.counts != nullptr;
     std::vector<DevSortedPart> parts;
@@ -1309,6 +1347,23 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     if (hf[0]) {
+        if (c->hprof.on) {
+            uint64_t maxlen = 0, maxbits = 0;
+            for (auto &p : parts) maxbits = std::max<uint64_t>(maxbits, p.bits);
+            for (uint32_t b = 0; b < c->nbins; ++b) {
+                uint64_t len = 0;
+                for (auto &r : c->runs) len += r.len(b);
+                maxlen = std::max(maxlen, len);
+            }
+            fprintf(stderr, "[okm sorted] extra %u: %llu children too big (max %llu); %u runs, %zu parts, %u items, "
+                            "largest part %llu, max bits %llu\n",
+                    extra, (unsigned long long)hf[0], (unsigned long long)hf[1], R, parts.size(), nitems,
+                    (unsigned long long)maxlen, (unsigned long long)maxbits);
+            for (auto &r : c->runs)
+                fprintf(stderr, "[okm sorted]   run n=%llu sorted=%d folded=%d borrowed=%d off.back=%llu\n",
+                        (unsigned long long)r.n, r.sorted, r.folded, r.borrowed,
+                        (unsigned long long)(r.off.empty() ? 0 : r.off.back()));
+        }
         for (void *p : bufs) c->pool.put(p);
         c->pool.put(d_segs);
         c->pool.put(d_items);

@@ -20,6 +20,8 @@ constexpr uint64_t kEmptyKey = ~0ull;
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);
 bool ctx_is_wide(const okm_ctx *c);  // never a canonical key
+uint32_t ctx_k(const okm_ctx *c);
+bool ctx_is_set(const okm_ctx *c);
 
 // ----------------------------------------------------------------------------
 // Device-side launchers (okm_device.hip).  All take a hipStream_t as void*.

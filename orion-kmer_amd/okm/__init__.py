@@ -27,6 +27,7 @@ __all__ = [
     "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads", "synth_reads_device",
     "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
     "KmerSet", "Classifier", "run_query", "run_classify", "read_fastx_records",
+    "Comm", "comm_unique_id", "owner_bounds", "synth_reads_device",
 ]
 
 
@@ -359,6 +360,75 @@ class KmerCounter:
         info = _lib.EngineInfo()
         check(lib().okm_engine_info_get(self.ctx, byref(info)), "okm_engine_info_get")
         return {f: int(getattr(info, f)) for f, _ in _lib.EngineInfo._fields_}
+
+
+# ---------------------------------------------------------------------------
+# multi-GPU: key-range owners over RCCL (okm_dist.hip)
+# ---------------------------------------------------------------------------
+
+def owner_bounds(hist: np.ndarray, world: int) -> List[int]:
+    """okm_owner_bounds: histogram bins [b_r, b_{r+1}) owned by rank r (host code)."""
+    hist = np.ascontiguousarray(hist, dtype=np.uint64)
+    out = np.zeros(world + 1, dtype=np.uint32)
+    check(lib().okm_owner_bounds(hist.ctypes.data if len(hist) else None, len(hist), world, out.ctypes.data),
+          "okm_owner_bounds")
+    return [int(x) for x in out]
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(_lib.OKM_COMM_ID_BYTES)
+    check(lib().okm_comm_unique_id(buf), "okm_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """One rank of an RCCL communicator owned by the library (okm_comm)."""
+
+    def __init__(self, nranks: int, rank: int, unique_id: bytes, device: int = 0, _handle=None):
+        self.h = c_void_p()
+        if _handle is not None:
+            self.h = _handle
+            return
+        idb = ctypes.create_string_buffer(bytes(unique_id), _lib.OKM_COMM_ID_BYTES)
+        check(lib().okm_comm_init_rank(byref(self.h), nranks, rank, idb, device), "okm_comm_init_rank")
+
+    @classmethod
+    def init_all(cls, devices: Sequence[int]) -> List["Comm"]:
+        n = len(devices)
+        arr = (c_void_p * n)()
+        devs = (c_int * n)(*devices)
+        check(lib().okm_comm_init_all(arr, n, devs), "okm_comm_init_all")
+        return [cls(n, i, b"", devices[i], _handle=c_void_p(arr[i])) for i in range(n)]
+
+    @property
+    def rank(self) -> int:
+        return int(lib().okm_comm_rank(self.h))
+
+    @property
+    def size(self) -> int:
+        return int(lib().okm_comm_size(self.h))
+
+    def merge_owned(self, local: "KmerCounter", owner: "KmerCounter") -> int:
+        """Collective: owner <- this rank's key range of all ranks' tables."""
+        n = c_uint64()
+        check(lib().okm_merge_owned(local.ctx, self.h, owner.ctx, byref(n)), "okm_merge_owned")
+        return n.value
+
+    def last_times(self) -> Dict[str, float]:
+        v = (ctypes.c_double * 4)()
+        check(lib().okm_comm_last_times(self.h, v), "okm_comm_last_times")
+        return {"plan_ms": v[0], "exchange_ms": v[1], "merge_ms": v[3]}
+
+    def close(self) -> None:
+        if self.h:
+            lib().okm_comm_destroy(self.h)
+            self.h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def set_intersection_size(a: np.ndarray, b: np.ndarray, device: int = 0) -> int:

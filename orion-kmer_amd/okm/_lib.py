@@ -38,6 +38,7 @@ OKM_MODE_WIDE = 0x100  # flag: k in 33..64 (two-u64 keys)
 RECORD_SEPARATOR = ord("\n")
 OKM_READ_RAW = 1
 OKM_READ_IDS = 2
+OKM_COMM_ID_BYTES = 128
 
 
 class OkmError(RuntimeError):
@@ -137,6 +138,15 @@ PROTOTYPES = {
                                         _P64]),
     "okm_synth_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                 c_double, c_void_p, c_int]),
+    "okm_comm_unique_id": (c_int, [c_void_p]),
+    "okm_comm_init_rank": (c_int, [POINTER(c_void_p), c_int, c_int, c_void_p, c_int]),
+    "okm_comm_init_all": (c_int, [c_void_p, c_int, c_void_p]),
+    "okm_comm_destroy": (None, [c_void_p]),
+    "okm_comm_rank": (c_int, [c_void_p]),
+    "okm_comm_size": (c_int, [c_void_p]),
+    "okm_merge_owned": (c_int, [c_void_p, c_void_p, c_void_p, _P64]),
+    "okm_comm_last_times": (c_int, [c_void_p, POINTER(c_double)]),
+    "okm_owner_bounds": (c_int, [c_void_p, c_uint32, c_int, c_void_p]),
     "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                        c_double, c_void_p, c_int]),
 }

@@ -72,17 +72,11 @@ def local_histogram(keys: torch.Tensor, k: int) -> torch.Tensor:
 
 def owner_ranges(hist: np.ndarray, world: int) -> List[int]:
     """Bin boundaries b_0=0 <= b_1 <= ... <= b_world=len(hist): rank r owns
-    bins [b_r, b_{r+1}); cuts at the cumulative count closest to r/world."""
-    cum = np.cumsum(hist, dtype=np.float64)
-    total = cum[-1] if len(cum) else 0.0
-    bounds = [0]
-    for r in range(1, world):
-        target = total * r / world
-        b = int(np.searchsorted(cum, target, side="left")) + 1
-        b = max(bounds[-1], min(b, len(hist)))
-        bounds.append(b)
-    bounds.append(len(hist))
-    return bounds
+    bins [b_r, b_{r+1}); cuts where the running total first reaches r/world.
+    The library's host split (okm_owner_bounds, the same code okm_merge_owned
+    runs), so the gloo tests exercise it."""
+    from . import owner_bounds
+    return owner_bounds(np.asarray(hist, dtype=np.uint64), world)
 
 
 def _order_view(keys: torch.Tensor, k: int) -> torch.Tensor:

@@ -1,0 +1,110 @@
+"""The multi-GPU merge inside the library (okm_dist.hip): okm_comm over RCCL
+and okm_merge_owned, through the C ABI.  The GPU box has one MI355X, so the
+communicator here has one rank (RCCL self send/recv: every pack, send/recv,
+unpack and merge step runs, the owner range is the whole key space); the N>1
+split is covered by the CPU tests of okm_owner_bounds (test_host_abi.py) and
+the gloo tests (test_dist_gloo.py), and measured by the driver's 8-GPU run.
+Exact against the local table and the oracle (count.rs:48, one map)."""
+
+import numpy as np
+import pytest
+
+import okm
+from oracle import OracleCounter
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm1():
+    c = okm.Comm(1, 0, okm.comm_unique_id(), 0)
+    assert c.rank == 0 and c.size == 1
+    yield c
+    c.close()
+
+
+def _batch(n, genome, seed):
+    return okm.synth_reads(n, 150, genome_len=genome, genome_seed=seed, seed=seed)
+
+
+@pytest.mark.parametrize("genome", [10_000, 2_000_000])   # 10 kb: counts far past the 255 byte escape
+def test_merge_owned_single_rank_equals_local(comm1, genome):
+    k = 31
+    b = _batch(200_000, genome, 7)
+    ref = OracleCounter(k)
+    ref.add_separated(b)
+    ek, ec = ref.result(1)
+    assert (ec > 255).any() == (genome == 10_000)
+    buf = okm.DeviceBuffer(len(b))
+    buf.upload(b)
+    with okm.KmerCounter(k) as local, okm.KmerCounter(k) as owner:
+        local.add_device_batch(buf.address, len(b))
+        n = comm1.merge_owned(local, owner)
+        gk, gc = owner.result(1)
+        lk, lc = local.result(1)
+        t = comm1.last_times()
+        # again: the communicator's buffers are reused, the owner is reset
+        assert comm1.merge_owned(local, owner) == n
+        g2k, g2c = owner.result(1)
+    buf.free()
+    assert n == len(ek)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert np.array_equal(lk, ek) and np.array_equal(lc, ec)
+    assert np.array_equal(g2k, ek) and np.array_equal(g2c, ec)
+    assert t["plan_ms"] >= 0 and t["exchange_ms"] >= 0 and t["merge_ms"] >= 0
+
+
+def test_merge_owned_set_mode(comm1):
+    k = 21
+    b = _batch(50_000, 300_000, 3)
+    ref = OracleCounter(k)
+    ref.add_separated(b)
+    ek, _ = ref.result(1)
+    with okm.KmerCounter(k, "set") as local, okm.KmerCounter(k, "set") as owner:
+        local.add_records([bytes(r) for r in b.tobytes().split(b"\n") if r], normalized=True)
+        assert comm1.merge_owned(local, owner) == len(ek)
+        gk, _ = owner.result(1)
+    assert np.array_equal(gk, ek)
+
+
+def test_merge_owned_k32_and_empty(comm1):
+    # k = 32 (unsigned key order, the top histogram bin) and an empty local table
+    with okm.KmerCounter(32) as local, okm.KmerCounter(32) as owner:
+        local.add_records([b"T" * 40, b"A" * 40, b"ACGT" * 20])
+        ref = OracleCounter(32)
+        ref.add_records([b"T" * 40, b"A" * 40, b"ACGT" * 20])
+        ek, ec = ref.result(1)
+        assert comm1.merge_owned(local, owner) == len(ek)
+        gk, gc = owner.result(1)
+        assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    with okm.KmerCounter(25) as local, okm.KmerCounter(25) as owner:
+        assert comm1.merge_owned(local, owner) == 0
+
+
+def test_comm_init_all_one_device():
+    (c,) = okm.Comm.init_all([0])
+    with okm.KmerCounter(15) as local, okm.KmerCounter(15) as owner:
+        local.add_records([b"ACGTTGCAACGTAGCTAGCTAGGATCGA" * 10])
+        n = c.merge_owned(local, owner)
+        assert n == local.count()
+    c.close()
+
+
+def test_merge_owned_argument_errors(comm1):
+    with okm.KmerCounter(21) as a, okm.KmerCounter(25) as b:
+        with pytest.raises(okm.OkmError):
+            comm1.merge_owned(a, b)  # k mismatch
+
+
+def test_merge_owned_into_local_context(comm1):
+    # owner == local: the counting context takes its own range back
+    k = 27
+    b = _batch(100_000, 500_000, 4)
+    ref = OracleCounter(k)
+    ref.add_separated(b)
+    ek, ec = ref.result(1)
+    with okm.KmerCounter(k) as ctx:
+        ctx.add_records([bytes(r) for r in b.tobytes().split(b"\n") if r], normalized=True)
+        assert comm1.merge_owned(ctx, ctx) == len(ek)
+        gk, gc = ctx.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)

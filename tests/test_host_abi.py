@@ -305,3 +305,52 @@ def test_empty_gz_output_is_valid_gzip(tmp_path, no_libdeflate):
         env["OKM_NO_LIBDEFLATE"] = "1"
     subprocess.run([sys.executable, "-c", code], check=True, env=env)
     assert gzip.decompress(open(p, "rb").read()) == b""
+
+
+# ---------------------------------------------------------------------------
+# multi-GPU owner split (okm_owner_bounds: host code of okm_merge_owned)
+# ---------------------------------------------------------------------------
+
+def _owner_bounds_np(hist, world):
+    """Restatement: cut r just past the bin where the running total first
+    reaches r/world of the whole (okm_dist.hip owner_bounds)."""
+    cum = np.cumsum(np.asarray(hist, dtype=np.float64))
+    total = cum[-1] if len(cum) else 0.0
+    b = [0]
+    for r in range(1, world):
+        x = int(np.searchsorted(cum, total * r / world, side="left")) + 1
+        b.append(max(b[-1], min(x, len(hist))))
+    b.append(len(hist))
+    return b
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8, 16])
+def test_owner_bounds_vs_restatement(world):
+    rng = np.random.default_rng(world)
+    for hist in (rng.integers(0, 1000, 1 << 16).astype(np.uint64),
+                 np.zeros(1 << 16, np.uint64),
+                 np.eye(1, 1 << 16, (1 << 16) - 1, dtype=np.uint64)[0] * 10**9,   # k=32: all in the top bin
+                 (rng.pareto(1.0, 4096) * 100).astype(np.uint64),
+                 np.array([5], np.uint64)):
+        got = okm.owner_bounds(hist, world)
+        assert got == _owner_bounds_np(hist, world)
+        assert got[0] == 0 and got[-1] == len(hist) and all(a <= b for a, b in zip(got, got[1:]))
+
+
+def test_owner_bounds_balance():
+    # count-balanced: every rank's share within one bin of 1/world of the total
+    rng = np.random.default_rng(1)
+    hist = rng.integers(0, 50, 1 << 16).astype(np.uint64)
+    for world in (2, 4, 8):
+        b = okm.owner_bounds(hist, world)
+        shares = [int(hist[b[r]:b[r + 1]].sum()) for r in range(world)]
+        assert sum(shares) == int(hist.sum())
+        assert max(shares) - min(shares) <= 2 * int(hist.max()) + 1
+
+
+def test_multi_gpu_symbols_exported():
+    lib = okm._lib.load()
+    for name in ("okm_comm_unique_id", "okm_comm_init_rank", "okm_comm_init_all", "okm_comm_destroy",
+                 "okm_comm_rank", "okm_comm_size", "okm_merge_owned", "okm_comm_last_times", "okm_owner_bounds",
+                 "okm_synth_reads_device"):
+        assert hasattr(lib, name)
