@@ -267,6 +267,30 @@ okm_status okm_comm_last_times(const okm_comm *comm, double *ms4);
  * running total first reaches r/world of the whole. */
 okm_status okm_owner_bounds(const uint64_t *hist, uint32_t nbins, int world, uint32_t *bounds);
 
+/* One counting context per GPU in this process (`orion-kmer count --gpus N`),
+ * behind the same add / count / finish calls as a context: host batches go to
+ * the GPUs in turn and are counted on one worker thread per GPU while the
+ * caller parses the next batch (okm_group_add_batch copies the batch and
+ * returns); okm_group_count merges the GPUs' tables by key-range owner
+ * (okm_merge_owned over okm_comm_init_all communicators).  n_gpus <= 0: every
+ * visible device; 1: no RCCL at all.  devices: the n_gpus ordinals (NULL:
+ * 0..n_gpus-1).  k > 32 (OKM_MODE_WIDE) only with one GPU. */
+typedef struct okm_group okm_group;
+okm_status okm_group_create(okm_group **out, uint8_t k, okm_mode mode, int n_gpus, const int *devices,
+                            uint64_t distinct_hint);
+void okm_group_destroy(okm_group *g);
+int okm_group_size(const okm_group *g);
+okm_status okm_group_add_batch(okm_group *g, const uint8_t *seq, const uint64_t *offsets, uint64_t n_records,
+                               int normalized);
+okm_status okm_group_count(okm_group *g, uint64_t *n_distinct);
+/* Rank r's context after okm_group_count: its owned key range (okm_result_size,
+ * okm_fetch_counts, okm_result_device ...); ranges in rank order are the
+ * sorted global table. */
+okm_ctx *okm_group_owner(okm_group *g, int rank);
+/* okm_finish_counts over the group: the concatenated ranges, filtered. */
+okm_status okm_group_finish_counts(okm_group *g, uint64_t min_count, uint64_t **keys, uint64_t **counts,
+                                   uint64_t *n);
+
 /* ------------------------------------------------------------------------
  * Instrumentation (bench.py measures kernels with HIP events on the
  * context's own stream).

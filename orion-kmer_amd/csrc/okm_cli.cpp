@@ -6,7 +6,8 @@
 // TSV, build.rs:141-146 KmerDbV2, compare.rs:15-25,85-89 pretty JSON) and the
 // same outermost error contexts, printed as env_logger would print
 // `error!("Error: {}", e)` (main.rs:10-13), exit status 1; usage errors exit 2.
-// Opt-in extension: --device <N> selects the GPU.
+// Opt-in extensions: --device <N> selects the GPU; count --gpus <N> counts on
+// N GPUs of this node (okm_group: one table over RCCL key-range owners).
 #include <errno.h>
 #include <math.h>
 #include <stdio.h>
@@ -21,6 +22,7 @@
 
 static int g_verbose = 0;
 static int g_device = 0;
+static int g_gpus = 1;
 
 static std::string timestamp() {
     char buf[64];
@@ -197,7 +199,7 @@ static const char *kVersion = "orion-kmer 0.1.0";
 
 static void print_help(const std::string &cmd) {
     if (cmd == "count")
-        printf("Count k-mers in FASTA/FASTQ files\n\nUsage: orion-kmer count [OPTIONS] --kmer-size <KMER_SIZE> --input-files <INPUT_FILES>... --output-file <OUTPUT_FILE>\n\nOptions:\n  -k, --kmer-size <KMER_SIZE>      The length of the k-mer\n  -i, --input-files <INPUT_FILES>...  One or more input FASTA/FASTQ files. Supports .gz, .xz, .zst compression.\n  -o, --output-file <OUTPUT_FILE>  Output file for k-mer counts (kmer<TAB>count)\n  -m, --min-count <MIN_COUNT>      Minimum count to report a k-mer [default: 1]\n      --wide                       Allow k up to 64 (two-u64 keys; extension, not in the reference)\n  -t, --threads <THREADS>          Number of threads to use (0 for all logical cores) [default: 0]\n  -v, --verbose...                 Verbosity level (e.g., -v, -vv)\n      --device <DEVICE>            GPU ordinal (MI355X engine) [default: 0]\n  -h, --help                       Print help\n  -V, --version                    Print version\n");
+        printf("Count k-mers in FASTA/FASTQ files\n\nUsage: orion-kmer count [OPTIONS] --kmer-size <KMER_SIZE> --input-files <INPUT_FILES>... --output-file <OUTPUT_FILE>\n\nOptions:\n  -k, --kmer-size <KMER_SIZE>      The length of the k-mer\n  -i, --input-files <INPUT_FILES>...  One or more input FASTA/FASTQ files. Supports .gz, .xz, .zst compression.\n  -o, --output-file <OUTPUT_FILE>  Output file for k-mer counts (kmer<TAB>count)\n  -m, --min-count <MIN_COUNT>      Minimum count to report a k-mer [default: 1]\n      --wide                       Allow k up to 64 (two-u64 keys; extension, not in the reference)\n  -t, --threads <THREADS>          Number of threads to use (0 for all logical cores) [default: 0]\n  -v, --verbose...                 Verbosity level (e.g., -v, -vv)\n      --device <DEVICE>            GPU ordinal (MI355X engine) [default: 0]\n      --gpus <GPUS>                Count on this many GPUs of the node, one table over RCCL (0: all) [default: 1]\n  -h, --help                       Print help\n  -V, --version                    Print version\n");
     else if (cmd == "build")
         printf("Build a unique k-mer database from genome assemblies\n\nUsage: orion-kmer build [OPTIONS] --kmer-size <KMER_SIZE> --genomes <GENOME_FILES>... --output-file <OUTPUT_FILE>\n");
     else if (cmd == "compare")
@@ -247,6 +249,36 @@ static int open_engine(okm_ctx **ctx, uint8_t k, okm_mode mode) {
     return 0;
 }
 
+// Feed every record of `path` into a GPU group (count.rs:59-79): the group
+// copies each batch and counts it on a worker thread, so the reader parses the
+// next batch meanwhile.
+static int feed_file_group(okm_group *g, const std::string &path, const char *open_ctx) {
+    okm_reader *r = nullptr;
+    okm_status s = okm_reader_open(&r, path.c_str(), 1);
+    if (s == OKM_E_IO) return die(std::string(open_ctx) + path);
+    if (s != OKM_OK) return die("Failed to parse FASTA/Q content from: " + path);
+    info("orion_kmer::commands", "Processing records from " + path + "...");
+    for (;;) {
+        const uint8_t *seq;
+        const uint64_t *off;
+        uint64_t n;
+        s = okm_reader_next(r, 128ull << 20, &seq, &off, &n);
+        if (s != OKM_OK) {
+            okm_reader_close(r);
+            return die("Error reading record from " + path);
+        }
+        if (n == 0) break;
+        s = okm_group_add_batch(g, seq, off, n, 1);
+        if (s != OKM_OK) {
+            okm_reader_close(r);
+            return die("GPU engine failure on " + path + ": " + err_detail());
+        }
+    }
+    info("orion_kmer::commands", "Finished processing " + std::to_string(okm_reader_records(r)) + " records from " + path);
+    okm_reader_close(r);
+    return 0;
+}
+
 // count.rs:40-141
 static int run_count(const Args &a) {
     uint8_t k;
@@ -265,23 +297,28 @@ static int run_count(const Args &a) {
     const bool wide = get_one(a, "wide", wflag);
     if (k == 0 || k > (wide ? 64 : 32))
         return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and " + (wide ? "64." : "32."));
-    okm_ctx *ctx = nullptr;
-    if ((rc = open_engine(&ctx, k, (okm_mode)(OKM_MODE_COUNT | (wide ? OKM_MODE_WIDE : 0))))) return rc;
+    // one table across all inputs (count.rs:48), on g_gpus GPUs (default 1)
+    okm_group *grp = nullptr;
+    const int one = g_device;  // --device picks the GPU of a one-GPU count
+    okm_status gs = okm_group_create(&grp, k, (okm_mode)(OKM_MODE_COUNT | (wide ? OKM_MODE_WIDE : 0)), g_gpus,
+                                     g_gpus == 1 ? &one : nullptr, 0);
+    if (gs == OKM_E_INVALID_K) return die(err_detail());  // errors.rs:6 text (or its k<=64 form with --wide)
+    if (gs != OKM_OK) return die("MI355X engine unavailable: " + err_detail());
     for (auto &p : inputs) {
         info("orion_kmer::commands::count", "Processing file: " + p);
-        if ((rc = feed_file(ctx, p, true, "Failed to get input reader for file: "))) {
-            okm_destroy(ctx);
+        if ((rc = feed_file_group(grp, p, "Failed to get input reader for file: "))) {
+            okm_group_destroy(grp);
             return rc;
         }
     }
     uint64_t *keys = nullptr, *counts = nullptr, n = 0, nd = 0;
-    if (okm_count(ctx, &nd) != OKM_OK || okm_finish_counts(ctx, min_count, &keys, &counts, &n) != OKM_OK) {
+    if (okm_group_count(grp, &nd) != OKM_OK || okm_group_finish_counts(grp, min_count, &keys, &counts, &n) != OKM_OK) {
         std::string d = err_detail();
-        okm_destroy(ctx);
+        okm_group_destroy(grp);
         return die("GPU engine failure while counting: " + d);
     }
     info("orion_kmer::commands::count", "Finished processing all input files. Found " + std::to_string(nd) + " unique canonical k-mers.");
-    okm_destroy(ctx);
+    okm_group_destroy(grp);
     okm_status s = okm_write_counts_tsv(out.c_str(), k, keys, counts, n);
     okm_free_result(keys);
     okm_free_result(counts);
@@ -826,6 +863,7 @@ int main(int argc, char **argv) {
         spec.push_back({"output-file", 'o', true, false});
         spec.push_back({"min-count", 'm', true, false});
         spec.push_back({"wide", 0, false, false});
+        spec.push_back({"gpus", 0, true, false});
     } else if (cmd == "build") {
         spec.push_back({"kmer-size", 'k', true, false});
         spec.push_back({"genomes", 'g', true, true});
@@ -872,6 +910,12 @@ int main(int argc, char **argv) {
     if (!a.pos.empty()) return usage_error("unexpected argument '" + a.pos[0] + "' found");
     std::string dev;
     if (get_one(pre, "device", dev) || get_one(a, "device", dev)) g_device = atoi(dev.c_str());
+    std::string gp;
+    if (get_one(a, "gpus", gp)) {
+        uint64_t v;
+        if (!parse_u64(gp, v) || v > 64) return usage_error("invalid value '" + gp + "' for '--gpus <GPUS>'");
+        g_gpus = (int)v;
+    }
     if (cmd == "count") return run_count(a);
     if (cmd == "build") return run_build(a);
     if (cmd == "query") return run_query(a);

@@ -147,6 +147,13 @@ PROTOTYPES = {
     "okm_merge_owned": (c_int, [c_void_p, c_void_p, c_void_p, _P64]),
     "okm_comm_last_times": (c_int, [c_void_p, POINTER(c_double)]),
     "okm_owner_bounds": (c_int, [c_void_p, c_uint32, c_int, c_void_p]),
+    "okm_group_create": (c_int, [POINTER(c_void_p), c_uint8, c_int, c_int, c_void_p, c_uint64]),
+    "okm_group_destroy": (None, [c_void_p]),
+    "okm_group_size": (c_int, [c_void_p]),
+    "okm_group_add_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int]),
+    "okm_group_count": (c_int, [c_void_p, _P64]),
+    "okm_group_owner": (c_void_p, [c_void_p, c_int]),
+    "okm_group_finish_counts": (c_int, [c_void_p, c_uint64, _PP64, _PP64, _P64]),
     "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                        c_double, c_void_p, c_int]),
 }

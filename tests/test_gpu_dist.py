@@ -6,6 +6,8 @@ split is covered by the CPU tests of okm_owner_bounds (test_host_abi.py) and
 the gloo tests (test_dist_gloo.py), and measured by the driver's 8-GPU run.
 Exact against the local table and the oracle (count.rs:48, one map)."""
 
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -108,3 +110,43 @@ def test_merge_owned_into_local_context(comm1):
         assert comm1.merge_owned(ctx, ctx) == len(ek)
         gk, gc = ctx.result(1)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def _group_count(k, batches, n_gpus, min_count=1):
+    lib = okm._lib.load()
+    g = ctypes.c_void_p()
+    okm._lib.check(lib.okm_group_create(ctypes.byref(g), k, 0, n_gpus, None, 0), "okm_group_create")
+    try:
+        for b in batches:
+            data, offs = okm.pack_records([bytes(r) for r in b.tobytes().split(b"\n") if r])
+            okm._lib.check(lib.okm_group_add_batch(g, data.ctypes.data, offs.ctypes.data, len(offs) - 1, 1),
+                           "okm_group_add_batch")
+        nd = ctypes.c_uint64()
+        okm._lib.check(lib.okm_group_count(g, ctypes.byref(nd)), "okm_group_count")
+        kp, cp, n = ctypes.POINTER(ctypes.c_uint64)(), ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
+        okm._lib.check(lib.okm_group_finish_counts(g, min_count, ctypes.byref(kp), ctypes.byref(cp), ctypes.byref(n)),
+                       "okm_group_finish_counts")
+        keys = np.ctypeslib.as_array(kp, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint64)
+        counts = np.ctypeslib.as_array(cp, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint64)
+        lib.okm_free_result(kp)
+        lib.okm_free_result(cp)
+        assert lib.okm_group_size(g) >= 1 and lib.okm_group_owner(g, 0)
+        return nd.value, keys, counts
+    finally:
+        lib.okm_group_destroy(g)
+
+
+@pytest.mark.parametrize("n_gpus", [1, 0])  # 0: every visible device (one on the box)
+def test_group_pipelined_count(n_gpus):
+    k = 31
+    batches = [_batch(40_000, 400_000, 10 + i) for i in range(5)]
+    ref = OracleCounter(k)
+    for b in batches:
+        ref.add_separated(b)
+    ek, ec = ref.result(1)
+    nd, gk, gc = _group_count(k, batches, n_gpus)
+    assert nd == len(ek)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    _, fk, fc = _group_count(k, batches, n_gpus, min_count=3)
+    sel = ec >= 3
+    assert np.array_equal(fk, ek[sel]) and np.array_equal(fc, ec[sel])
