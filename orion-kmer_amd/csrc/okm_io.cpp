@@ -28,6 +28,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -754,10 +755,67 @@ using namespace okm;
 
 extern "C" {
 
+// Uncompressed TSV (count.rs:127-135, utils.rs:196 plain writer): every line's
+// length is known from its count's digits, so each block of lines gets its
+// byte offset from a prefix sum and the threads format and pwrite() their
+// blocks concurrently (the ordered-round writer above serialised the writes:
+// ~1.7 s for C2's 110 M lines).
+static okm_status write_counts_tsv_plain(const char *path, uint8_t k, const uint64_t *keys, const uint64_t *counts,
+                                         uint64_t n) {
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return fail(OKM_E_IO, std::string("cannot create ") + path);
+    const uint64_t step = 1 << 16;
+    const size_t nb = (size_t)((n + step - 1) / step);
+    std::vector<uint64_t> off(nb + 1, 0);
+    parallel_for(nb, [&](size_t b) {
+        const uint64_t at = b * step, m = std::min<uint64_t>(step, n - at);
+        uint64_t bytes = m * (uint64_t)(k + 2);  // k bases + tab + newline
+        for (uint64_t i = 0; i < m; ++i) {
+            uint64_t c = counts[at + i];
+            int d = 1;
+            while (c >= 10) {
+                c /= 10;
+                ++d;
+            }
+            bytes += d;
+        }
+        off[b + 1] = bytes;
+    });
+    for (size_t b = 0; b < nb; ++b) off[b + 1] += off[b];
+    std::atomic<int> bad{0};
+    const size_t nt = std::min<size_t>(std::max<size_t>(nb, 1), (size_t)host_threads());
+    parallel_for(nt, [&](size_t t) {
+        std::string buf;
+        for (size_t b = t; b < nb && !bad; b += nt) {
+            const uint64_t at = b * step, m = std::min<uint64_t>(step, n - at);
+            format_counts_tsv(k, keys + at * (k > 32 ? 2 : 1), counts + at, m, buf);
+            if (buf.size() != off[b + 1] - off[b]) {
+                bad = 2;
+                return;
+            }
+            size_t o = 0;
+            while (o < buf.size()) {
+                const ssize_t w = ::pwrite(fd, buf.data() + o, buf.size() - o, (off_t)(off[b] + o));
+                if (w <= 0) {
+                    bad = 1;
+                    return;
+                }
+                o += (size_t)w;
+            }
+        }
+    });
+    if (::close(fd) != 0 && !bad) bad = 1;
+    if (bad == 2) return fail(OKM_E_IO, "TSV block length mismatch");
+    if (bad) return fail(OKM_E_IO, std::string("write failed: ") + path);
+    return OKM_OK;
+}
+
 okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *keys, const uint64_t *counts,
                                 uint64_t n) {
     if (!path) return fail(OKM_E_ARG, "null path");
     if (k == 0 || k > 64) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
+    const std::string ext = lower_extension(path);
+    if (ext != "gz" && ext != "xz" && ext != "zst" && ext != "zstd") return write_counts_tsv_plain(path, k, keys, counts, n);
     OutWriter w;
     okm_status s = w.open(path);
     if (s != OKM_OK) return s;

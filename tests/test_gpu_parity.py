@@ -565,3 +565,25 @@ def test_grouped_count(k, wide, mode, maxb, monkeypatch):
             if wide:
                 fk = fk.reshape(-1, 2)
             assert np.array_equal(fk, xk) and np.array_equal(fc, xc), mc
+
+
+def test_c1_cli_full_size(tmp_path):
+    """BASELINE configs[0] (C1) through the CLI: byte-identical TSV with the
+    restatement's (tests/golden/c1_k21.json), for -m 1 and -m 2."""
+    import hashlib
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from make_c1_fasta import c1_fasta
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c1_k21.json")
+    with open(golden) as fh:
+        fx = json.load(fh)
+    inp = tmp_path / "c1.fasta"
+    inp.write_bytes(c1_fasta())
+    for m, key in (("1", "m1"), ("2", "m2")):
+        out = tmp_path / f"out_m{m}.tsv"
+        r = subprocess.run([_lib.CLI_PATH, "count", "-k", "21", "-i", str(inp), "-o", str(out), "-m", m],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        raw = out.read_bytes()
+        assert raw.count(b"\n") == fx[key]["lines"]
+        assert hashlib.sha256(raw).hexdigest() == fx[key]["sha256"]

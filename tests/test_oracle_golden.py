@@ -263,3 +263,37 @@ def test_c_oracle_mt_equals_single(k, threads):
     ek, ec = oc.result(1)
     gk, gc = count_separated_mt(data, k, threads)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs[0] (C1): 10 x 100 kb FASTA wrapped at 60 columns, k = 21
+# ---------------------------------------------------------------------------
+
+def test_c1_oracle_vs_restatement_fixture(tmp_path):
+    """The C oracle (+ the host reader's needletail normalisation and the TSV
+    writer) on the full C1 input equals the pure-Python restatement's output
+    (tests/golden/c1_k21.json, made by tests/golden/make_c1_golden.py)."""
+    import hashlib
+    import json
+    import os
+    import sys
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from make_c1_fasta import c1_fasta
+    import okm
+    from oracle import OracleCounter
+    with open(os.path.join(ROOT, "tests", "golden", "c1_k21.json")) as fh:
+        fx = json.load(fh)
+    data = c1_fasta()
+    assert hashlib.sha256(data).hexdigest() == fx["input_sha256"]
+    recs = okm.parse_fastx(data)  # host reader: multi-line join, normalize (count.rs:71)
+    assert len(recs) == 10 and all(len(r) == 100_000 for r in recs)
+    oc = OracleCounter(21)
+    oc.add_records(recs, normalized=True)
+    for m, key in ((1, "m1"), (2, "m2")):
+        keys, counts = oc.result(m)
+        out = tmp_path / f"c1_m{m}.tsv"
+        okm.write_counts_tsv(str(out), 21, keys, counts)
+        raw = out.read_bytes()
+        assert len(raw) == fx[key]["bytes"] and raw.count(b"\n") == fx[key]["lines"]
+        assert hashlib.sha256(raw).hexdigest() == fx[key]["sha256"]
