@@ -5,7 +5,7 @@ One step = one pass of the hot path over one batch of synthetic input with
 the batch already resident in HBM: extraction + canonicalisation + key-range
 partitioning + LDS counting + sorted (key, count) table on the device
 (count.rs:23-38 + :106-119), and for N>1 the owner-partitioned RCCL merge of
-the per-GPU tables (okm/dist.py).
+the per-GPU tables inside the library (okm_merge_owned).
 
 Workload (configs[1]): k=31, 1 GiB synthetic FASTQ of 150 bp reads =
 3,355,443 reads = 503,316,450 bases per GPU, sampled from a seeded 100 Mbp
@@ -17,10 +17,11 @@ Batches in flight (--streams, default 3): at N=1 three engine contexts, each
 with its own HIP stream and table, count whole batches concurrently from three
 host threads (one batch's host syncs and latency-bound count phase overlap the
 others' streaming kernels; measured 2 / 3 / 4 in flight: 5.81-6.02 /
-5.70-5.74 / 5.73-5.90 ms per batch, tools/ab_streams.sh); at N>1 three stages run at once: one thread counts
-batch i+2 into two contexts in turn, the main thread exchanges batch i+1 (RCCL
-on its own stream) and a third merges batch i into one of two merge contexts.
-Every step still counts one full batch into its own sorted table.
+5.70-5.74 / 5.73-5.90 ms per batch, tools/ab_streams.sh); at N>1 (--workload
+c2) one thread counts batch i+1 into two contexts in turn while the main thread
+runs okm_merge_owned on batch i (the library's RCCL stream) into one of two
+merge contexts.  Every step still counts one full batch into its own sorted
+table.  The default workload at N>1 is C3 (BASELINE configs[2], main_c3).
 
 Prints ONE JSON line on rank 0 (the driver's contract), including `roofline`
 for the dominant kernel (HIP events on the engine's own stream, from a
@@ -177,11 +178,21 @@ def main():
     # OKM_BENCH_EXCHANGE=1 runs the N>1 exchange + merge path at world size 1
     # too (torchrun --nproc-per-node 1): its cost on one GPU, RCCL self-send
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
+    comm = None
     if dist_on:
+        # product path: the library's own RCCL communicator (okm_comm +
+        # okm_merge_owned: HIP owner split / pack / unpack kernels, grouped
+        # ncclSend/ncclRecv over xGMI, k-way LDS merge); torch.distributed (gloo,
+        # host) only hands out the communicator id, barriers and the max-time
+        # reduce.  OKM_BENCH_BACKEND=gloo rehearses the exchange through torch
+        # (okm/dist.py) instead: RCCL refuses two ranks on one device.
+        dist.init_process_group("gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+            uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
+            dist.broadcast(uid, 0)
+            comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
 
     # ---- synthetic batch for this rank, made resident in HBM ---------------
     t0 = time.time()
@@ -207,9 +218,9 @@ def main():
     # N>1: the owner's merge runs on a third thread (two merge contexts in
     # turn), so it overlaps the next batch's exchange and the one after's
     # count; OKM_BENCH_MERGE_THREAD=0 keeps exchange+merge on one thread
-    merge_thread = dist_on and os.environ.get("OKM_BENCH_MERGE_THREAD", "1") != "0"
-    mergers = [okm.KmerCounter(K, "count", device) for _ in range(2 if merge_thread else 1)] if dist_on else []
-    xs = torch.cuda.Stream() if dist_on and backend == "nccl" else None
+    merge_thread = dist_on and comm is None and os.environ.get("OKM_BENCH_MERGE_THREAD", "1") != "0"
+    mergers = [okm.KmerCounter(K, "count", device) for _ in range(2 if comm is not None or merge_thread else 1)] \
+        if dist_on else []
     if dist_on:
         from okm import dist as okm_dist
 
@@ -242,14 +253,9 @@ def main():
     def exchange_only(c, n, release):
         t_x = time.perf_counter()
         keys, counts = table_tensors(c, n)
-        if backend == "nccl":
-            with torch.cuda.stream(xs):
-                rk, rc, _, rs = okm_dist.exchange_runs(keys, counts, K)
-                xs.synchronize()
-        else:
-            rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)
-            rk, rc = rk.cuda(), rc.cuda()
-            torch.cuda.synchronize()
+        rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)  # gloo rehearsal
+        rk, rc = rk.cuda(), rc.cuda()
+        torch.cuda.synchronize()
         release()  # the table has been copied out: its context may count the next batch
         xt[0] += time.perf_counter() - t_x
         return rk, rc, rs
@@ -272,6 +278,16 @@ def main():
 
     def exchange_merge(c, n, release):
         return merge_runs(mergers[0], exchange_only(c, n, release))
+
+    def merge_owned(i, c, release):
+        """okm_merge_owned: this rank's key range of every rank's table of
+        batch i, into merge context i % 2 (the library's RCCL path)."""
+        n_m = comm.merge_owned(c, mergers[i % 2])
+        release()
+        t = comm.last_times()
+        xt[0] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
+        xt[1] += t["merge_ms"] * 1e-3
+        return n_m
 
     def run_steps(nsteps):
         """nsteps batches through the path; returns the distinct count (N=1)
@@ -304,7 +320,10 @@ def main():
             if err:
                 raise err[0]
             return res[-1]
-        if merge_thread:
+        if comm is not None:
+            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
+                                         lambda i, j, n, release: merge_owned(i, ctrs[j], release))
+        elif merge_thread:
             res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
                                          lambda i, j, n, release: exchange_only(ctrs[j], n, release),
                                          lambda i, m, payload: merge_runs(mergers[m], payload))
@@ -331,7 +350,7 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t_start
     if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # per-kernel HIP-event timing: a separate single-stream pass of the same K
@@ -354,6 +373,8 @@ def main():
                                     min(args.cpu_mt_reads, args.reads), device, "the same batch")
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         if dist_on:
             dist.destroy_process_group()
         return
@@ -397,7 +418,11 @@ def main():
         out["config"]["owned_distinct_rank0"] = int(n_owned)
         out["exchange_ms_per_step_rank0"] = {"exchange": round(xt[0] / args.steps * 1e3, 3),
                                              "merge": round(xt[1] / args.steps * 1e3, 3)}
+        out["exchange_impl"] = ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, k-way LDS merge)"
+                                if comm is not None else "torch gloo rehearsal (okm/dist.py)")
     emit(out)
+    if comm is not None:
+        comm.close()
     if dist_on:
         dist.destroy_process_group()
     dbuf.free()

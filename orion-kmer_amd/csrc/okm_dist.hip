@@ -149,58 +149,66 @@ __device__ __forceinline__ uint32_t dest_of(const ull *cut, uint32_t P, uint64_t
     return lo;
 }
 
-// Low byte of every count (16 per thread: one 16-B store); WRITE=false counts
-// the escapes (count > 255) per destination, WRITE=true also writes them,
-// grouped by destination: (position in the destination's run, count).
+// Low byte of every count (4 per thread: two 16-B loads, one 4-B store, so
+// a wave's loads and stores are contiguous); WRITE=false counts the escapes
+// (count > 255) per destination, WRITE=true also writes them, grouped by
+// destination: (position in the destination's run, count).
+constexpr int kPackPer = 4;
+constexpr uint64_t kPackBlock = 256 * kPackPer;  // counts per workgroup
+
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_pack_counts(const uint64_t *__restrict__ counts, uint64_t n,
                                                      const ull *__restrict__ cut, uint32_t P, uint8_t *__restrict__ low,
                                                      ull *__restrict__ esc_cnt, ull *__restrict__ esc_cur,
-                                                     uint64_t *__restrict__ esc) {
-    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+                                                     uint64_t *__restrict__ esc, uint64_t skip0, uint64_t skip1) {
+    // [skip0, skip1): this rank's own slice when the owner borrows it (never sent)
+    const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlock;
+    if (b0 >= skip0 && b0 + kPackBlock <= skip1) return;  // block-uniform
+    const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPackPer;
     if (i0 >= n) return;
-    uint8_t b[16];
+    uint64_t c[kPackPer] = {0, 0, 0, 0};
+    if (i0 + kPackPer <= n) {
+        const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(counts + i0);
+        const ulonglong2 v0 = p[0], v1 = p[1];
+        c[0] = v0.x, c[1] = v0.y, c[2] = v1.x, c[3] = v1.y;
+    } else {
+        for (int j = 0; j < kPackPer && i0 + j < n; ++j) c[j] = counts[i0 + j];
+    }
+    uint32_t word = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < kPackPer; ++j) {
         const uint64_t i = i0 + j;
-        uint64_t c = 0;
-        if (i < n) {
-            c = counts[i];
-            if (c > 255) {
-                const uint32_t d = dest_of(cut, P, i);
-                if (WRITE) {
-                    const ull s = atomicAdd(&esc_cur[d], 1ull);
-                    esc[2 * s] = i - cut[d];
-                    esc[2 * s + 1] = c;
-                } else {
-                    atomicAdd(&esc_cnt[d], 1ull);
-                }
+        if (i >= skip0 && i < skip1) c[j] = 0;
+        if (c[j] > 255) {
+            const uint32_t d = dest_of(cut, P, i);
+            if (WRITE) {
+                const ull s = atomicAdd(&esc_cur[d], 1ull);
+                esc[2 * s] = i - cut[d];
+                esc[2 * s + 1] = c[j];
+            } else {
+                atomicAdd(&esc_cnt[d], 1ull);
             }
         }
-        b[j] = (uint8_t)c;
+        word |= (uint32_t)(c[j] & 0xFFu) << (8 * j);
     }
     if (WRITE) return;  // the bytes are written by the counting pass
-    if (i0 + 16 <= n) {
-        uint4 v;
-        memcpy(&v, b, 16);
-        *reinterpret_cast<uint4 *>(low + i0) = v;
-    } else {
-        for (int j = 0; j < 16 && i0 + j < n; ++j) low[i0 + j] = b[j];
-    }
+    if (i0 + kPackPer <= n)
+        *reinterpret_cast<uint32_t *>(low + i0) = word;
+    else
+        for (int j = 0; j < kPackPer && i0 + j < n; ++j) low[i0 + j] = (uint8_t)(word >> (8 * j));
 }
 
 __global__ __launch_bounds__(256) void k_widen_counts(const uint8_t *__restrict__ low, uint64_t n,
                                                       uint64_t *__restrict__ counts) {
-    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kPackPer;
     if (i0 >= n) return;
-    if (i0 + 16 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(low + i0);
-        uint8_t b[16];
-        memcpy(b, &v, 16);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) counts[i0 + j] = b[j];
+    if (i0 + kPackPer <= n) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(low + i0);
+        ulonglong2 *p = reinterpret_cast<ulonglong2 *>(counts + i0);
+        p[0] = make_ulonglong2(w & 0xFFu, (w >> 8) & 0xFFu);
+        p[1] = make_ulonglong2((w >> 16) & 0xFFu, w >> 24);
     } else {
-        for (int j = 0; j < 16 && i0 + j < n; ++j) counts[i0 + j] = low[i0 + j];
+        for (int j = 0; j < kPackPer && i0 + j < n; ++j) counts[i0 + j] = low[i0 + j];
     }
 }
 
@@ -416,12 +424,18 @@ okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t
     for (uint32_t r = 0; r < P; ++r) hs[r] = cut[r + 1] - cut[r];
     HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, P * sizeof(ull), s));
-    const uint64_t pblocks = (n + 16 * 256 - 1) / (16 * 256);
+    const uint64_t pblocks = (n + kPackBlock - 1) / kPackBlock;
+    // This rank's own slice never crosses RCCL when the owner is another
+    // context: the owner borrows it straight from the local table (it stays
+    // unchanged until okm_count(owner) returns below).  owner == local
+    // receives it through a self send/recv, since okm_reset(owner) releases it.
+    const bool self_borrow = owner != local;
+    const uint64_t skip0 = self_borrow ? cut[me] : 0, skip1 = self_borrow ? cut[me + 1] : 0;
     if (!set) {
         OKM_TRY(m->low.ensure(std::max<uint64_t>(n, 16)));
         if (pblocks)
             hipLaunchKernelGGL(k_pack_counts<false>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(),
-                               P, m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr);
+                               P, m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr, skip0, skip1);
         HIP_TRY(hipGetLastError());
     }
     NCCL_TRY(rccl().AllGather(m->sizes.p, m->gsizes.p, 2 * P, ncclUint64, m->nc, s));
@@ -438,12 +452,18 @@ okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t
         reoff[r + 1] = reoff[r] + er[r];
         eoff[r + 1] = eoff[r] + es[r];
     }
+    const uint64_t self_n = ss[me];
+    if (self_borrow) {
+        for (uint32_t r = me + 1; r <= P; ++r) roff[r] -= rs[me], reoff[r] -= er[me];
+        rs[me] = er[me] = 0;
+        ss[me] = es[me] = 0;
+    }
     const uint64_t nrecv = roff[P], nresc = reoff[P], nesc = eoff[P];
     if (!set && nesc) {  // escapes grouped by destination
         OKM_TRY(m->esc.ensure(2 * nesc * sizeof(uint64_t)));
         HIP_TRY(hipMemcpyAsync(m->esc_cur.p, eoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_pack_counts<true>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
-                           m->low.as<uint8_t>(), nullptr, m->esc_cur.as<ull>(), m->esc.as<uint64_t>());
+                           m->low.as<uint8_t>(), nullptr, m->esc_cur.as<ull>(), m->esc.as<uint64_t>(), skip0, skip1);
         HIP_TRY(hipGetLastError());
     }
     const double t_plan = ms_since(t0);
@@ -496,7 +516,7 @@ okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t
         NCCL_TRY(rccl().GroupEnd());
     }
     if (!set && nrecv) {
-        const uint64_t wb = (nrecv + 16 * 256 - 1) / (16 * 256);
+        const uint64_t wb = (nrecv + kPackBlock - 1) / kPackBlock;
         hipLaunchKernelGGL(k_widen_counts, dim3((uint32_t)wb), dim3(256), 0, s, m->rlow.as<uint8_t>(), nrecv,
                            m->rc.as<uint64_t>());
         if (nresc) {
@@ -517,6 +537,10 @@ okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t
     // 5. the owner merges the P sorted slices in place (k-way LDS merge)
     OKM_TRY(okm_reset(owner));
     for (uint32_t r = 0; r < P; ++r) {
+        if (r == me && self_borrow && self_n) {
+            OKM_TRY(okm_add_sorted_pairs_device(owner, dk + cut[me], set ? nullptr : dc + cut[me], self_n));
+            continue;
+        }
         if (!rs[r]) continue;
         OKM_TRY(okm_add_sorted_pairs_device(owner, m->rk.as<uint64_t>() + roff[r],
                                             set ? nullptr : m->rc.as<uint64_t>() + roff[r], rs[r]));

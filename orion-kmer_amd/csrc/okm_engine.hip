@@ -1419,6 +1419,34 @@ static okm_status do_count(okm_ctx *c) {
         if (c->runs.size() == 1 && c->runs[0].folded) return do_count(c);
         all_sorted = !c->runs.empty();
     }
+    if (all_sorted && c->runs.size() == 1 && c->runs[0].counts) {
+        // one sorted weighted table (e.g. the only slice a multi-GPU owner
+        // holds): it already is the result — copied, since it may be borrowed
+        Run &r = c->runs[0];
+        const uint64_t n = r.n;
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1) * c->kw, &c->res_keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1), &c->res_counts));
+        c->timer.begin(c->stream);
+        if (n) {
+            HIP_TRY(hipMemcpyAsync(c->res_keys, r.keys, n * c->kw * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                                   c->stream));
+            HIP_TRY(hipMemcpyAsync(c->res_counts, r.counts, n * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                                   c->stream));
+        }
+        c->timer.end(c->stream, "sorted_copy", 2.0 * (8.0 * c->kw + 8.0) * (double)n);
+        OKM_TRY(sync(c));  // a borrowed run may be freed once okm_count returns
+        if (!r.borrowed) {
+            c->pool.put(r.keys);
+            c->pool.put(r.counts);
+        }
+        c->runs.clear();
+        c->n_res = n;
+        c->info.distinct = n;
+        c->info.levels = 0;
+        c->info.work_items = 0;
+        c->counted = true;
+        return OKM_OK;
+    }
     if (all_sorted) {
         bool fallback = false;
         OKM_TRY(count_sorted(c, &fallback));
