@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint64, c_void_p
+from ctypes import c_uint32, POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint64, c_void_p
 from typing import Sequence, Tuple
 
 import numpy as np
@@ -63,6 +63,8 @@ def load() -> ctypes.CDLL:
     lib.oracle_counter_wide_add_record.argtypes = [c_void_p, c_char_p, c_size_t, c_int]
     lib.oracle_counter_wide_add_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int]
     lib.oracle_counter_wide_add_pairs.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64]
+    lib.oracle_counter_wide_add_separated_range.argtypes = [c_void_p, c_void_p, c_uint64, c_uint8, c_uint32,
+                                                            c_uint64, c_uint64]
     lib.oracle_counter_wide_distinct.restype = c_uint64
     lib.oracle_counter_wide_distinct.argtypes = [c_void_p]
     lib.oracle_counter_wide_windows.restype = c_uint64
@@ -178,6 +180,13 @@ class OracleCounterWide(OracleCounter):
         counts = np.ascontiguousarray(counts, dtype=np.uint64)
         load().oracle_counter_wide_add_pairs(self.h, keys.ctypes.data, counts.ctypes.data, len(counts))
 
+    def add_separated_range(self, data: np.ndarray, bits: int, lo: int, hi: int, sep: int = ord("\n")) -> None:
+        """Normalised records joined by `sep`; only keys whose top `bits` bits
+        lie in [lo, hi) are counted (rolling encode; range shards for large
+        tests, see okm_oracle.c)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        load().oracle_counter_wide_add_separated_range(self.h, data.ctypes.data, len(data), sep, bits, lo, hi)
+
     @property
     def distinct(self) -> int:
         return int(load().oracle_counter_wide_distinct(self.h))
@@ -257,3 +266,46 @@ def count_separated_mt(data: np.ndarray, k: int, threads: int, sep: int = ord("\
         th.join()
     return (np.concatenate([p[0] for p in parts]).astype(np.uint64),
             np.concatenate([p[1] for p in parts]).astype(np.uint64))
+
+
+def count_separated_wide_ranges(data: np.ndarray, k: int, threads: int, bits: int = 8, sep: int = ord("\n"),
+                                shards: int = 0, on_range=None, bins=None):
+    """k in 33..64 restatement sharded by key range for large tests (not
+    reference behaviour: a labelled restatement-MT helper).  Every shard scans
+    all of `data` (normalised records joined by `sep`) and counts only the
+    canonical keys whose top `bits` bits fall in its contiguous bin range; the
+    ranges are cut where the canonical-key density (min of a key and its
+    reverse complement: f(x) = 2(1 - x) over the key range) gives each shard
+    an equal share, and the per-range sorted tables concatenate in order.
+    `threads` workers run `shards` (default: threads) shards; with `on_range`,
+    on_range(lo, hi, keys, counts) gets each shard's table instead (nothing is
+    kept); `bins`: explicit [(lo, hi), ...] ranges instead of the cover.
+    Returns (keys (n, 2) [lo, hi] | None, counts | None, valid windows)."""
+    from concurrent.futures import ThreadPoolExecutor
+    nb = 1 << bits
+    ns = shards or threads
+    if bins is None:
+        cuts = [0] + [min(nb, int(round(nb * (1.0 - (1.0 - t / ns) ** 0.5)))) for t in range(1, ns)] + [nb]
+        cuts = sorted(set(cuts))
+        bins = list(zip(cuts[:-1], cuts[1:]))
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+
+    def shard(r):
+        oc = OracleCounterWide(k)
+        oc.add_separated_range(data, bits, r[0], r[1], sep)
+        keys, counts = oc.result(1)
+        w = oc.windows
+        del oc
+        if on_range is not None:
+            on_range(r[0], r[1], keys, counts)
+            return None, None, w
+        return keys, counts, w
+
+    with ThreadPoolExecutor(max_workers=max(1, min(threads, len(bins)))) as ex:
+        parts = list(ex.map(shard, bins))
+    w = parts[0][2] if parts else 0
+    if on_range is not None:
+        return None, None, w
+    keys = np.concatenate([p[0] for p in parts]) if parts else np.zeros((0, 2), np.uint64)
+    counts = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint64)
+    return keys, counts, w

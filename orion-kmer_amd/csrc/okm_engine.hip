@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -52,6 +53,16 @@ static bool pool_trace() {
 }
 static std::mutex g_pools_mu;
 static std::vector<DevPool *> g_pools;  // every live context's pool (cross-pool trim on OOM)
+
+// Share of HBM the pools aim to stay under (OKM_HBM_CAP, default 0.9).
+static double hbm_cap_frac() {
+    static const double frac = [] {
+        const char *e = getenv("OKM_HBM_CAP");
+        const double f = e ? atof(e) : 0.9;
+        return f > 0.0 && f <= 1.0 ? f : 0.9;
+    }();
+    return frac;
+}
 
 struct DevPool {
     std::multimap<size_t, void *> free_;
@@ -90,7 +101,14 @@ struct DevPool {
             }
         }
         void *p = nullptr;
-        hipError_t e = hipMalloc(&p, bytes);
+        // Soft cap on the device's memory in use (OKM_HBM_CAP, default 0.9 of
+        // HBM): past it, cached blocks are reused or released first, as when
+        // HBM is full; only then does the allocation go past the cap.
+        auto try_alloc = [&]() -> hipError_t {
+            if (over_cap(bytes)) return hipErrorOutOfMemory;
+            return hipMalloc(&p, bytes);
+        };
+        hipError_t e = try_alloc();
         if (e != hipSuccess) {
             // HBM is full: any larger cached block beats freeing and re-mapping
             // (hipFree + hipMalloc of tens of GB costs hundreds of ms per step)
@@ -122,15 +140,19 @@ struct DevPool {
                 }
                 if (freed + (size_t(256) << 20) < bytes) continue;  // not enough back yet
                 (void)hipGetLastError();
-                e = hipMalloc(&p, bytes);
+                e = try_alloc();
             }
             if (e != hipSuccess) {
                 (void)hipGetLastError();
-                e = hipMalloc(&p, bytes);
+                e = try_alloc();
             }
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 trim_others();
+                e = try_alloc();
+            }
+            if (e != hipSuccess) {  // nothing cached is left to give back: the cap is soft
+                (void)hipGetLastError();
                 e = hipMalloc(&p, bytes);
             }
             if (e != hipSuccess) {
@@ -153,6 +175,17 @@ struct DevPool {
             fprintf(stderr, "[okm pool] hipMalloc %zu bytes (held %zu, free blocks %zu) %p\n", bytes, held, free_.size(),
                     p);
         return OKM_OK;
+    }
+    // Would `bytes` more take the device past the soft cap?
+    bool over_cap(size_t bytes) const {
+        const double frac = hbm_cap_frac();
+        if (frac >= 1.0) return false;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return (double)(tot - fr) + (double)bytes > frac * (double)tot;
     }
     void put(void *p) {
         if (!p) return;
@@ -1732,7 +1765,11 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     }
     // 3/4 of what is free: sampled capacities, line padding and the pool's size
     // classes make a pass hold more than its keys
-    const double avail = 0.75 * (double)(free_b + c->pool.cached());
+    // ... and no more than the room under the pool's soft cap (OKM_HBM_CAP)
+    const double cached = (double)c->pool.cached();
+    double room = (double)free_b + cached;
+    if (total_b) room = std::min(room, hbm_cap_frac() * (double)total_b - (double)(total_b - free_b) + cached);
+    const double avail = 0.75 * std::max(room, 0.0);
     uint64_t group_keys = total;
     int mode = 0;  // 0: one group (no grouping)
     const char *ge = getenv("OKM_GROUP_KEYS");
@@ -1745,7 +1782,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         // a bound-sized table is only worth it when it is a small share of HBM
         // (dense inputs such as k=63 long reads); with duplicated keys (a fold
         // of covered reads) exact per-group tables hold a fraction of it
-        if (room_a >= (double)total * ws_key / 64.0 && (double)total * res_key <= 0.5 * avail) {
+        // ... and when the exact tables could not be joined anyway (their
+        // worst case is the bound itself, twice over while joining)
+        const bool a_fits = room_a >= (double)total * ws_key / 64.0;
+        if (a_fits && ((double)total * res_key <= 0.5 * avail || 2.0 * (double)total * res_key > avail)) {
             mode = 1;
             group_keys = (uint64_t)(room_a / ws_key);
         } else {
@@ -1892,6 +1932,29 @@ const char *okm_device_arch(int device) {
     return buf;
 }
 
+// OKM_CU_SLICES=n (experiment): contexts created in turn get streams on
+// disjoint CU subsets (CU i belongs to slice i % n, so every slice spans every
+// XCD), so batches in flight on different contexts run side by side instead
+// of taking the whole chip kernel by kernel.
+static hipError_t create_ctx_stream(int device, hipStream_t *st) {
+    static std::atomic<uint32_t> next{0};
+    const char *e = getenv("OKM_CU_SLICES");
+    const int n = e ? atoi(e) : 0;
+    if (n > 1) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount >= n) {
+            const uint32_t me = next.fetch_add(1) % (uint32_t)n;
+            const int ncu = prop.multiProcessorCount;
+            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+            for (int cu = 0; cu < ncu; ++cu)
+                if ((uint32_t)(cu % n) == me) mask[cu / 32] |= 1u << (cu % 32);
+            return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+        }
+        (void)hipGetLastError();
+    }
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint) {
     (void)distinct_hint;
     if (!out) return fail(OKM_E_ARG, "okm_create: out is NULL");
@@ -1924,7 +1987,7 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
         const char *fe = getenv("OKM_FOLD_BYTES");
         c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(0.08 * (double)total_b);
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (create_ctx_stream(device, &c->stream) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->curpad, (size_t)c->nbins * OKM_L1_CUR_STRIDE * sizeof(unsigned long long)) != hipSuccess ||

@@ -297,3 +297,19 @@ def test_c1_oracle_vs_restatement_fixture(tmp_path):
         raw = out.read_bytes()
         assert len(raw) == fx[key]["bytes"] and raw.count(b"\n") == fx[key]["lines"]
         assert hashlib.sha256(raw).hexdigest() == fx[key]["sha256"]
+
+
+@pytest.mark.parametrize("k", [33, 63, 64])
+def test_wide_range_shards_equal_the_restatement(k):
+    """The rolling range-sharded k<=64 helper (count_separated_wide_ranges,
+    used by the 1 Gbases k=63 GPU test) equals the O(k) restatement."""
+    from oracle import OracleCounterWide, count_separated_wide_ranges
+    import okm
+    batch = okm.synth_reads(3_000, 150, genome_len=100_000, genome_seed=k, seed=k + 1, sub_rate=0.02, n_rate=0.002)
+    batch.reshape(3_000, 151)[::97, :150] = ord("A")  # a hot key
+    oc = OracleCounterWide(k)
+    oc.add_records([r for r in batch.tobytes().split(b"\n") if r], normalized=True)
+    ek, ec = oc.result(1)
+    gk, gc, w = count_separated_wide_ranges(batch, k, threads=5)
+    assert w == oc.windows
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
