@@ -290,6 +290,11 @@ okm_ctx *okm_group_owner(okm_group *g, int rank);
 /* okm_finish_counts over the group: the concatenated ranges, filtered. */
 okm_status okm_group_finish_counts(okm_group *g, uint64_t min_count, uint64_t **keys, uint64_t **counts,
                                    uint64_t *n);
+/* count.rs:106-137 in one call: the group's table, filtered to count >=
+ * min_count, written as "KMER\tCOUNT\n" lines to `path` (.gz/.xz/.zst by
+ * extension, utils.rs:167-198), streamed off the GPUs in chunks while the host
+ * formats the previous one.  *n_lines (optional) = lines written. */
+okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t min_count, uint64_t *n_lines);
 
 /* ------------------------------------------------------------------------
  * Instrumentation (bench.py measures kernels with HIP events on the

@@ -14,13 +14,29 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orion_kmer.h"
 
 static int g_verbose = 0;
+
+// OKM_CLI_TIMES=1: wall time of each phase of a run on stderr (tools/e2e_cli.sh)
+static void phase(const char *what) {
+    static const bool on = getenv("OKM_CLI_TIMES") != nullptr;
+    if (!on) return;
+    static struct timespec t0 = [] {
+        struct timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        return t;
+    }();
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "[okm cli] %-14s %8.1f ms\n", what, (t.tv_sec - t0.tv_sec) * 1e3 + (t.tv_nsec - t0.tv_nsec) / 1e6);
+}
 static int g_device = 0;
 static int g_gpus = 1;
 
@@ -249,10 +265,57 @@ static int open_engine(okm_ctx **ctx, uint8_t k, okm_mode mode) {
     return 0;
 }
 
+// The count engine, brought up on a thread of its own (HIP runtime start-up
+// and device contexts take ~150-200 ms) while the reader parses the first
+// batch; get() waits for it.
+struct AsyncGroup {
+    okm_group *g = nullptr;
+    okm_status st = OKM_OK;
+    std::string err;
+    std::thread th;
+    bool joined = false;
+    void start(uint8_t k, okm_mode mode) {
+        th = std::thread([this, k, mode] {
+            const int one = g_device;  // --device picks the GPU of a one-GPU count
+            st = okm_group_create(&g, k, mode, g_gpus, g_gpus == 1 ? &one : nullptr, 0);
+            if (st != OKM_OK) err = okm_last_error();
+        });
+    }
+    okm_group *get() {
+        if (!joined) {
+            th.join();
+            joined = true;
+        }
+        return st == OKM_OK ? g : nullptr;
+    }
+    ~AsyncGroup() {
+        get();
+        okm_group_destroy(g);
+    }
+};
+
+// The output is complete and closed: leave without tearing down the GPU
+// contexts and the HIP runtime one by one (~150 ms for a C2-sized table; the
+// driver reclaims the device memory at exit).  Not under a profiler, whose
+// atexit handlers must run (rocprofv3 preloads its tool library), or with
+// OKM_CLI_NO_FAST_EXIT set.
+static void fast_exit() {
+    const char *pre = getenv("LD_PRELOAD");
+    if (getenv("OKM_CLI_NO_FAST_EXIT") || (pre && strstr(pre, "rocprof"))) return;
+    fflush(stdout);
+    fflush(stderr);
+    _exit(0);
+}
+
+static int engine_error(const AsyncGroup &ag) {
+    if (ag.st == OKM_E_INVALID_K) return die(ag.err);  // errors.rs:6 text (or its k<=64 form with --wide)
+    return die("MI355X engine unavailable: " + ag.err);
+}
+
 // Feed every record of `path` into a GPU group (count.rs:59-79): the group
 // copies each batch and counts it on a worker thread, so the reader parses the
 // next batch meanwhile.
-static int feed_file_group(okm_group *g, const std::string &path, const char *open_ctx) {
+static int feed_file_group(AsyncGroup &ag, const std::string &path, const char *open_ctx) {
     okm_reader *r = nullptr;
     okm_status s = okm_reader_open(&r, path.c_str(), 1);
     if (s == OKM_E_IO) return die(std::string(open_ctx) + path);
@@ -268,6 +331,11 @@ static int feed_file_group(okm_group *g, const std::string &path, const char *op
             return die("Error reading record from " + path);
         }
         if (n == 0) break;
+        okm_group *g = ag.get();
+        if (!g) {
+            okm_reader_close(r);
+            return engine_error(ag);
+        }
         s = okm_group_add_batch(g, seq, off, n, 1);
         if (s != OKM_OK) {
             okm_reader_close(r);
@@ -297,33 +365,29 @@ static int run_count(const Args &a) {
     const bool wide = get_one(a, "wide", wflag);
     if (k == 0 || k > (wide ? 64 : 32))
         return die("Invalid K-mer size: " + std::to_string(k) + ". Must be between 1 and " + (wide ? "64." : "32."));
-    // one table across all inputs (count.rs:48), on g_gpus GPUs (default 1)
-    okm_group *grp = nullptr;
-    const int one = g_device;  // --device picks the GPU of a one-GPU count
-    okm_status gs = okm_group_create(&grp, k, (okm_mode)(OKM_MODE_COUNT | (wide ? OKM_MODE_WIDE : 0)), g_gpus,
-                                     g_gpus == 1 ? &one : nullptr, 0);
-    if (gs == OKM_E_INVALID_K) return die(err_detail());  // errors.rs:6 text (or its k<=64 form with --wide)
-    if (gs != OKM_OK) return die("MI355X engine unavailable: " + err_detail());
+    // one table across all inputs (count.rs:48), on g_gpus GPUs (default 1),
+    // started while the first input is parsed
+    phase("start");
+    AsyncGroup ag;
+    ag.start(k, (okm_mode)(OKM_MODE_COUNT | (wide ? OKM_MODE_WIDE : 0)));
     for (auto &p : inputs) {
         info("orion_kmer::commands::count", "Processing file: " + p);
-        if ((rc = feed_file_group(grp, p, "Failed to get input reader for file: "))) {
-            okm_group_destroy(grp);
-            return rc;
-        }
+        if ((rc = feed_file_group(ag, p, "Failed to get input reader for file: "))) return rc;
     }
-    uint64_t *keys = nullptr, *counts = nullptr, n = 0, nd = 0;
-    if (okm_group_count(grp, &nd) != OKM_OK || okm_group_finish_counts(grp, min_count, &keys, &counts, &n) != OKM_OK) {
-        std::string d = err_detail();
-        okm_group_destroy(grp);
-        return die("GPU engine failure while counting: " + d);
-    }
+    phase("input parsed");
+    okm_group *grp = ag.get();
+    if (!grp) return engine_error(ag);
+    uint64_t nd = 0;
+    if (okm_group_count(grp, &nd) != OKM_OK) return die("GPU engine failure while counting: " + err_detail());
     info("orion_kmer::commands::count", "Finished processing all input files. Found " + std::to_string(nd) + " unique canonical k-mers.");
-    okm_group_destroy(grp);
-    okm_status s = okm_write_counts_tsv(out.c_str(), k, keys, counts, n);
-    okm_free_result(keys);
-    okm_free_result(counts);
+    // count.rs:106-137: filter, sort (the table already is) and write, streamed
+    // off the GPU while the previous chunk is formatted
+    phase("counted");
+    okm_status s = okm_group_write_counts_tsv(grp, out.c_str(), min_count, nullptr);
+    phase("written");
     if (s != OKM_OK) return die("Failed to get output writer for counts file: " + dbg_path(out));
     info("orion_kmer::commands::count", "Successfully wrote k-mer counts to " + dbg_path(out));
+    fast_exit();
     return 0;
 }
 

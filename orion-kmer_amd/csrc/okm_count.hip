@@ -277,7 +277,16 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     // key of every run (count.rs:33: a key's count = its run's length/weight);
     // the flags of the dead home counters' bytes (hc) are then compacted into
     // run starts by the whole block, so the emit below is coalesced
-    slice_sort<W>(sk, sw, a, n);
+    {
+        const uint32_t c3 = n - c0 - c1 - c2;
+        // homes are key ranges in order: sorting each home's run sorts the slice
+        // (k=63 reads are ~98 % distinct, ~2 keys per home: a whole-slice
+        // insertion sort compared every key with its neighbours' homes)
+        slice_sort<W>(sk, sw, a, c0);
+        slice_sort<W>(sk, sw, a + c0, c1);
+        slice_sort<W>(sk, sw, a + c0 + c1, c2);
+        slice_sort<W>(sk, sw, a + c0 + c1 + c2, c3);
+    }
     PMARK(13);
     uint8_t *rf = reinterpret_cast<uint8_t *>(hc);  // [kCapI] run-start flags
     {

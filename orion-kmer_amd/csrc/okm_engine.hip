@@ -427,6 +427,19 @@ bool ctx_is_wide(const okm_ctx *c) { return c->wide; }
 uint32_t ctx_k(const okm_ctx *c) { return c->k; }
 bool ctx_is_set(const okm_ctx *c) { return c->mode == OKM_MODE_SET; }
 
+void *host_pinned_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void host_pinned_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 static okm_status ensure_hc(okm_ctx *c, size_t n_u32) {
     if (n_u32 <= c->HC_cap) return OKM_OK;
     if (c->HC) (void)hipFree(c->HC);

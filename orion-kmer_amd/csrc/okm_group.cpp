@@ -10,6 +10,7 @@
 // one host thread per GPU, okm_comm_init_all communicators): rank r then owns
 // a contiguous key range, so the ranges in rank order are the sorted global
 // table (count.rs:106-119).  Only the public C ABI is used.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -21,6 +22,7 @@
 #include <vector>
 
 #include "okm_internal.h"
+#include "okm_io.h"
 
 namespace {
 
@@ -279,6 +281,102 @@ okm_status okm_group_finish_counts(okm_group *g, uint64_t min_count, uint64_t **
     *counts = C;
     *n = total;
     return OKM_OK;
+}
+
+// count.rs:106-137 straight from the device: every owner's range (rank
+// order = the sorted global table) is copied off the GPU in chunks into two
+// page-locked buffers by a copy thread while the host threads filter, format
+// and write the previous chunk (okm::write_counts_tsv_chunks), so the PCIe
+// copy hides behind the TSV work and no table-sized host array is touched.
+okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t min_count, uint64_t *n_lines) {
+    if (!g || !path) return okm::fail(OKM_E_ARG, "null argument");
+    okm_status s = okm_group_count(g, nullptr);
+    if (s != OKM_OK) return s;
+    const uint64_t kw = (g->k > 32) ? 2 : 1;
+    struct Chunk {
+        const uint64_t *k, *c;
+        uint64_t n;
+    };
+    std::vector<Chunk> chunks;
+    uint64_t per = uint64_t(1) << 24;  // entries per chunk (256 MB of keys + counts at k <= 32)
+    if (const char *e = getenv("OKM_TSV_CHUNK")) per = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
+    for (auto &W : g->w) {
+        const uint64_t *dk = nullptr, *dc = nullptr;
+        uint64_t n = 0;
+        if ((s = okm_result_device(W.ctx, &dk, &dc, &n)) != OKM_OK) return s;
+        for (uint64_t o = 0; o < n; o += per) chunks.push_back({dk + o * kw, dc + o, std::min(per, n - o)});
+    }
+    uint64_t cap = 0;
+    for (auto &c : chunks) cap = std::max(cap, c.n);
+    struct Slot {
+        uint64_t *k = nullptr, *c = nullptr;
+        long chunk = -1;  // chunk held (ready), -1: free
+    } slot[2];
+    const size_t kbytes = std::max<uint64_t>(cap, 1) * kw * 8, cbytes = std::max<uint64_t>(cap, 1) * 8;
+    for (auto &sl : slot) {
+        sl.k = (uint64_t *)okm::host_pinned_alloc(kbytes);
+        sl.c = (uint64_t *)okm::host_pinned_alloc(cbytes);
+    }
+    auto release = [&]() {
+        for (auto &sl : slot) {
+            okm::host_pinned_free(sl.k);
+            okm::host_pinned_free(sl.c);
+        }
+    };
+    if (!slot[0].k || !slot[0].c || !slot[1].k || !slot[1].c) {
+        release();
+        return okm::fail(OKM_E_NOMEM, "okm_group_write_counts_tsv: pinned host buffers");
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stop = false;
+    okm_status copy_st = OKM_OK;
+    std::string copy_msg;
+    size_t consumed = 0;  // chunks [0, consumed) are done with: their slots may be refilled
+    std::thread copier([&]() {
+        for (size_t i = 0; i < chunks.size(); ++i) {
+            Slot &sl = slot[i % 2];
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || i < consumed + 2; });
+                if (stop) return;
+            }
+            okm_status st = okm_memcpy_d2h(sl.k, chunks[i].k, chunks[i].n * kw * 8);
+            if (st == OKM_OK) st = okm_memcpy_d2h(sl.c, chunks[i].c, chunks[i].n * 8);
+            std::lock_guard<std::mutex> lk(mu);
+            if (st != OKM_OK) {
+                copy_st = st;
+                copy_msg = okm_last_error();
+                stop = true;
+            } else {
+                sl.chunk = (long)i;
+            }
+            cv.notify_all();
+            if (st != OKM_OK) return;
+        }
+    });
+    s = okm::write_counts_tsv_chunks(
+        path, g->k, min_count, chunks.size(),
+        [&](size_t i, const uint64_t **kp, const uint64_t **cp, uint64_t *np) -> okm_status {
+            std::unique_lock<std::mutex> lk(mu);
+            consumed = i;  // chunk i - 1 is written: its slot may take chunk i + 1
+            cv.notify_all();
+            cv.wait(lk, [&] { return stop || slot[i % 2].chunk == (long)i; });
+            if (slot[i % 2].chunk != (long)i) return okm::fail(copy_st != OKM_OK ? copy_st : OKM_E_DEVICE, copy_msg);
+            *kp = slot[i % 2].k;
+            *cp = slot[i % 2].c;
+            *np = chunks[i].n;
+            return OKM_OK;
+        },
+        n_lines);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+        cv.notify_all();
+    }
+    copier.join();
+    release();
+    return s;
 }
 
 }  // extern "C"

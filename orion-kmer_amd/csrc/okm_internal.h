@@ -17,6 +17,11 @@ okm_status fail(okm_status s, const std::string &msg);
 
 constexpr uint64_t kEmptyKey = ~0ull;
 
+// Page-locked host memory (hipHostMalloc) for the host translation units
+// (okm_group.cpp's device-to-file stream); nullptr on failure.
+void *host_pinned_alloc(size_t bytes);
+void host_pinned_free(void *p);
+
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);
 bool ctx_is_wide(const okm_ctx *c);  // never a canonical key

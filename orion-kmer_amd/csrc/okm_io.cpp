@@ -749,93 +749,162 @@ size_t format_counts_tsv(uint8_t k, const uint64_t *keys, const uint64_t *counts
     return out.size();
 }
 
+// Lines of keys[0, n) with count >= min_count, and their byte length.
+static uint64_t tsv_block_bytes(uint8_t k, const uint64_t *counts, uint64_t n, uint64_t min_count, uint64_t *lines) {
+    uint64_t bytes = 0, m = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t c = counts[i];
+        if (c < min_count) continue;
+        int d = 1;
+        while (c >= 10) {
+            c /= 10;
+            ++d;
+        }
+        bytes += (uint64_t)(k + 2) + d;  // k bases + tab + digits + newline
+        ++m;
+    }
+    *lines = m;
+    return bytes;
+}
+
+// format_counts_tsv over the entries with count >= min_count.
+static void format_filtered(uint8_t k, const uint64_t *keys, const uint64_t *counts, uint64_t n, uint64_t min_count,
+                            std::string &out, std::vector<uint64_t> &fk, std::vector<uint64_t> &fc) {
+    if (min_count <= 1) {
+        format_counts_tsv(k, keys, counts, n, out);
+        return;
+    }
+    const int kw = k > 32 ? 2 : 1;
+    fk.clear();
+    fc.clear();
+    for (uint64_t i = 0; i < n; ++i)
+        if (counts[i] >= min_count) {
+            fk.insert(fk.end(), keys + i * kw, keys + (i + 1) * kw);
+            fc.push_back(counts[i]);
+        }
+    format_counts_tsv(k, fk.data(), fc.data(), fc.size(), out);
+}
+
+okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_count, size_t nchunks,
+                                   const std::function<okm_status(size_t, const uint64_t **, const uint64_t **,
+                                                                  uint64_t *)> &get,
+                                   uint64_t *n_lines) {
+    if (!path) return fail(OKM_E_ARG, "null path");
+    if (k == 0 || k > 64) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
+    const int kw = k > 32 ? 2 : 1;
+    const std::string ext = lower_extension(path);
+    const bool plain = ext != "gz" && ext != "xz" && ext != "zst" && ext != "zstd";
+    int fd = -1;
+    OutWriter w;
+    if (plain) {
+        // no O_TRUNC: a rerun over an existing output overwrites its page-cache
+        // pages in place (truncating a multi-GB file first costs ~0.8 s); the
+        // length is set once at the end
+        fd = ::open(path, O_WRONLY | O_CREAT, 0644);
+        if (fd < 0) return fail(OKM_E_IO, std::string("cannot create ") + path);
+    } else {
+        okm_status s = w.open(path);
+        if (s != OKM_OK) return s;
+    }
+    const uint64_t step = plain ? (1 << 16) : (1 << 17);
+    uint64_t at_byte = 0, lines = 0;
+    std::atomic<int> bad{0};
+    for (size_t ci = 0; ci < nchunks && !bad; ++ci) {
+        const uint64_t *keys = nullptr, *counts = nullptr;
+        uint64_t n = 0;
+        okm_status s = get(ci, &keys, &counts, &n);
+        if (s != OKM_OK) {
+            if (fd >= 0) ::close(fd);
+            return s;
+        }
+        if (!n) continue;
+        const size_t nb = (size_t)((n + step - 1) / step);
+        if (plain) {
+            std::vector<uint64_t> off(nb + 1, 0), cnt(nb, 0);
+            parallel_for(nb, [&](size_t b) {
+                const uint64_t a = b * step, m = std::min<uint64_t>(step, n - a);
+                off[b + 1] = tsv_block_bytes(k, counts + a, m, min_count, &cnt[b]);
+            });
+            for (size_t b = 0; b < nb; ++b) {
+                off[b + 1] += off[b];
+                lines += cnt[b];
+            }
+            const size_t nt = std::min<size_t>(nb, (size_t)host_threads());
+            parallel_for(nt, [&](size_t t) {
+                std::string buf;
+                std::vector<uint64_t> fk, fc;
+                for (size_t b = t; b < nb && !bad; b += nt) {
+                    const uint64_t a = b * step, m = std::min<uint64_t>(step, n - a);
+                    format_filtered(k, keys + a * kw, counts + a, m, min_count, buf, fk, fc);
+                    if (buf.size() != off[b + 1] - off[b]) {
+                        bad = 2;
+                        return;
+                    }
+                    for (size_t o = 0; o < buf.size();) {
+                        const ssize_t wr = ::pwrite(fd, buf.data() + o, buf.size() - o, (off_t)(at_byte + off[b] + o));
+                        if (wr <= 0) {
+                            bad = 1;
+                            return;
+                        }
+                        o += (size_t)wr;
+                    }
+                }
+            });
+            at_byte += off[nb];
+        } else {
+            const size_t per_round = 2 * (size_t)host_threads();
+            std::vector<std::string> buf(per_round);
+            for (size_t b0 = 0; b0 < nb; b0 += per_round) {
+                const size_t rb = std::min(per_round, nb - b0);
+                std::vector<uint64_t> cnt(rb, 0);
+                parallel_for(rb, [&](size_t j) {
+                    std::vector<uint64_t> fk, fc;
+                    const uint64_t a = (b0 + j) * step, m = std::min<uint64_t>(step, n - a);
+                    format_filtered(k, keys + a * kw, counts + a, m, min_count, buf[j], fk, fc);
+                    cnt[j] = (uint64_t)std::count(buf[j].begin(), buf[j].end(), '\n');
+                });
+                std::vector<std::pair<const uint8_t *, size_t>> blocks;
+                for (size_t j = 0; j < rb; ++j) {
+                    blocks.emplace_back((const uint8_t *)buf[j].data(), buf[j].size());
+                    lines += cnt[j];
+                }
+                s = w.write_blocks(blocks);
+                if (s != OKM_OK) return s;
+            }
+        }
+    }
+    if (n_lines) *n_lines = lines;
+    if (plain) {
+        if (!bad && ::ftruncate(fd, (off_t)at_byte) != 0) bad = 1;
+        if (::close(fd) != 0 && !bad) bad = 1;
+        if (bad == 2) return fail(OKM_E_IO, "TSV block length mismatch");
+        if (bad) return fail(OKM_E_IO, std::string("write failed: ") + path);
+        return OKM_OK;
+    }
+    return w.close();
+}
+
 }  // namespace okm
 
 using namespace okm;
 
 extern "C" {
 
-// Uncompressed TSV (count.rs:127-135, utils.rs:196 plain writer): every line's
-// length is known from its count's digits, so each block of lines gets its
-// byte offset from a prefix sum and the threads format and pwrite() their
-// blocks concurrently (the ordered-round writer above serialised the writes:
-// ~1.7 s for C2's 110 M lines).
-static okm_status write_counts_tsv_plain(const char *path, uint8_t k, const uint64_t *keys, const uint64_t *counts,
-                                         uint64_t n) {
-    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (fd < 0) return fail(OKM_E_IO, std::string("cannot create ") + path);
-    const uint64_t step = 1 << 16;
-    const size_t nb = (size_t)((n + step - 1) / step);
-    std::vector<uint64_t> off(nb + 1, 0);
-    parallel_for(nb, [&](size_t b) {
-        const uint64_t at = b * step, m = std::min<uint64_t>(step, n - at);
-        uint64_t bytes = m * (uint64_t)(k + 2);  // k bases + tab + newline
-        for (uint64_t i = 0; i < m; ++i) {
-            uint64_t c = counts[at + i];
-            int d = 1;
-            while (c >= 10) {
-                c /= 10;
-                ++d;
-            }
-            bytes += d;
-        }
-        off[b + 1] = bytes;
-    });
-    for (size_t b = 0; b < nb; ++b) off[b + 1] += off[b];
-    std::atomic<int> bad{0};
-    const size_t nt = std::min<size_t>(std::max<size_t>(nb, 1), (size_t)host_threads());
-    parallel_for(nt, [&](size_t t) {
-        std::string buf;
-        for (size_t b = t; b < nb && !bad; b += nt) {
-            const uint64_t at = b * step, m = std::min<uint64_t>(step, n - at);
-            format_counts_tsv(k, keys + at * (k > 32 ? 2 : 1), counts + at, m, buf);
-            if (buf.size() != off[b + 1] - off[b]) {
-                bad = 2;
-                return;
-            }
-            size_t o = 0;
-            while (o < buf.size()) {
-                const ssize_t w = ::pwrite(fd, buf.data() + o, buf.size() - o, (off_t)(off[b] + o));
-                if (w <= 0) {
-                    bad = 1;
-                    return;
-                }
-                o += (size_t)w;
-            }
-        }
-    });
-    if (::close(fd) != 0 && !bad) bad = 1;
-    if (bad == 2) return fail(OKM_E_IO, "TSV block length mismatch");
-    if (bad) return fail(OKM_E_IO, std::string("write failed: ") + path);
-    return OKM_OK;
-}
-
+// count.rs:127-135 over a host table: one chunk of write_counts_tsv_chunks
+// (plain output: every line's length is known from its count's digits, so
+// each block of lines gets its byte offset from a prefix sum and the threads
+// format and pwrite() their blocks concurrently; compressed output: blocks
+// formatted in parallel rounds, compressed and written in order).
 okm_status okm_write_counts_tsv(const char *path, uint8_t k, const uint64_t *keys, const uint64_t *counts,
                                 uint64_t n) {
-    if (!path) return fail(OKM_E_ARG, "null path");
-    if (k == 0 || k > 64) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
-    const std::string ext = lower_extension(path);
-    if (ext != "gz" && ext != "xz" && ext != "zst" && ext != "zstd") return write_counts_tsv_plain(path, k, keys, counts, n);
-    OutWriter w;
-    okm_status s = w.open(path);
-    if (s != OKM_OK) return s;
-    // Blocks of `step` lines formatted on parallel threads, a round of
-    // 2 x host_threads() blocks at a time, written in order.
-    const uint64_t step = 1 << 17;
-    const size_t per_round = 2 * (size_t)host_threads();
-    std::vector<std::string> buf(per_round);
-    for (uint64_t o = 0; o < n; o += step * per_round) {
-        const size_t nb = (size_t)std::min<uint64_t>(per_round, (n - o + step - 1) / step);
-        parallel_for(nb, [&](size_t b) {
-            const uint64_t at = o + b * step, m = std::min(step, n - at);
-            format_counts_tsv(k, keys + at * (k > 32 ? 2 : 1), counts + at, m, buf[b]);
-        });
-        std::vector<std::pair<const uint8_t *, size_t>> blocks;
-        for (size_t b = 0; b < nb; ++b) blocks.emplace_back((const uint8_t *)buf[b].data(), buf[b].size());
-        s = w.write_blocks(blocks);
-        if (s != OKM_OK) return s;
-    }
-    return w.close();
+    return write_counts_tsv_chunks(path, k, 1, 1,
+                                   [&](size_t, const uint64_t **kp, const uint64_t **cp, uint64_t *np) {
+                                       *kp = keys;
+                                       *cp = counts;
+                                       *np = n;
+                                       return OKM_OK;
+                                   },
+                                   nullptr);
 }
 
 okm_status okm_write_file(const char *path, const uint8_t *data, uint64_t n) {

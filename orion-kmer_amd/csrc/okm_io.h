@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <functional>
 #include <memory>
 #include <utility>
 #include <atomic>
@@ -57,6 +58,18 @@ okm_status decompress_by_extension(const std::string &path, Bytes &data);
 // needletail 0.5.1 sniffing: gzip / bzip2 / xz magic bytes.
 okm_status sniff_decompress(Bytes &data);
 size_t format_counts_tsv(uint8_t k, const uint64_t *keys, const uint64_t *counts, size_t n, std::string &out);
+
+// The count.rs:127-135 TSV of a table that arrives in chunks (e.g. copied off
+// the device while the previous chunk is formatted): get(i, &keys, &counts,
+// &n) hands over chunk i of nchunks (host memory, valid until get(i + 1) is
+// called); lines with count < min_count are skipped.  Plain output is written
+// in place with pwrite (no truncation of an existing file's pages until the
+// end); .gz/.xz/.zst go through OutWriter in order.  *n_lines (optional)
+// receives the lines written.
+okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_count, size_t nchunks,
+                                   const std::function<okm_status(size_t, const uint64_t **, const uint64_t **,
+                                                                  uint64_t *)> &get,
+                                   uint64_t *n_lines);
 
 // utils.rs:167-198 get_output_writer: compressor chosen by extension.
 class OutWriter {

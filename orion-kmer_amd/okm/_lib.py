@@ -154,6 +154,7 @@ PROTOTYPES = {
     "okm_group_count": (c_int, [c_void_p, _P64]),
     "okm_group_owner": (c_void_p, [c_void_p, c_int]),
     "okm_group_finish_counts": (c_int, [c_void_p, c_uint64, _PP64, _PP64, _P64]),
+    "okm_group_write_counts_tsv": (c_int, [c_void_p, c_char_p, c_uint64, _P64]),
     "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                        c_double, c_void_p, c_int]),
 }

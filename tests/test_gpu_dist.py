@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import okm
+import restate as R
 from oracle import OracleCounter
 
 pytestmark = pytest.mark.gpu
@@ -150,3 +151,40 @@ def test_group_pipelined_count(n_gpus):
     _, fk, fc = _group_count(k, batches, n_gpus, min_count=3)
     sel = ec >= 3
     assert np.array_equal(fk, ek[sel]) and np.array_equal(fc, ec[sel])
+
+
+@pytest.mark.parametrize("ext,chunk", [("tsv", "1500"), ("tsv", ""), ("tsv.gz", "4096"), ("tsv.zst", "")])
+def test_group_write_counts_tsv_streamed(tmp_path, monkeypatch, ext, chunk):
+    """okm_group_write_counts_tsv: the table streamed off the GPU in chunks
+    (OKM_TSV_CHUNK entries) equals count.rs:127-135's TSV of the oracle table,
+    filtered by min_count, also when it overwrites a LONGER existing file
+    (written in place, then cut to length)."""
+    if chunk:
+        monkeypatch.setenv("OKM_TSV_CHUNK", chunk)
+    k = 21
+    batches = [_batch(20_000, 300_000, 50 + i) for i in range(3)]
+    ref = OracleCounter(k)
+    for b in batches:
+        ref.add_separated(b)
+    lib = okm._lib.load()
+    for m in (1, 2):
+        ek, ec = ref.result(m)
+        want = "".join(f"{okm.u64_to_seq(int(x), k).decode()}\t{int(c)}\n" for x, c in zip(ek, ec)).encode()
+        out = tmp_path / f"o{m}.{ext}"
+        if ext == "tsv":
+            out.write_bytes(b"X" * (len(want) + 12345))  # stale longer content
+        g = ctypes.c_void_p()
+        okm._lib.check(lib.okm_group_create(ctypes.byref(g), k, 0, 1, None, 0), "okm_group_create")
+        try:
+            for b in batches:
+                data, offs = okm.pack_records([bytes(r) for r in b.tobytes().split(b"\n") if r])
+                okm._lib.check(lib.okm_group_add_batch(g, data.ctypes.data, offs.ctypes.data, len(offs) - 1, 1),
+                               "okm_group_add_batch")
+            nl = ctypes.c_uint64()
+            okm._lib.check(lib.okm_group_write_counts_tsv(g, str(out).encode(), m, ctypes.byref(nl)),
+                           "okm_group_write_counts_tsv")
+        finally:
+            lib.okm_group_destroy(g)
+        assert nl.value == len(ek)
+        raw = R.decompress_by_extension(str(out), out.read_bytes())
+        assert raw == want, m
