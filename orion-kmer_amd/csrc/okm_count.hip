@@ -41,6 +41,9 @@ namespace okm {
 #ifndef OKM_COUNT_PROF
 #define OKM_COUNT_PROF 0
 #endif
+#ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
+#define OKM_FULL_RANK 1
+#endif
 // OKM_COUNT_PROF=1 builds: thread 0 of every block accumulates clock64()
 // deltas between phase marks (debug/tuning only; okm_debug_count_prof()).
 __device__ unsigned long long g_count_prof[16];
@@ -273,41 +276,77 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     }
     __syncthreads();
     PMARK(12);
-    // each thread's 4 homes are one slice of sk: sort it and flag the first
-    // key of every run (count.rs:33: a key's count = its run's length/weight);
-    // the flags of the dead home counters' bytes (hc) are then compacted into
-    // run starts by the whole block, so the emit below is coalesced
-    {
-        const uint32_t c3 = n - c0 - c1 - c2;
-        // homes are key ranges in order: sorting each home's run sorts the slice
-        // (k=63 reads are ~98 % distinct, ~2 keys per home: a whole-slice
-        // insertion sort compared every key with its neighbours' homes)
-        slice_sort<W>(sk, sw, a, c0);
-        slice_sort<W>(sk, sw, a + c0, c1);
-        slice_sort<W>(sk, sw, a + c0 + c1, c2);
-        slice_sort<W>(sk, sw, a + c0 + c1 + c2, c3);
-    }
-    PMARK(13);
-    uint8_t *rf = reinterpret_cast<uint8_t *>(hc);  // [kCapI] run-start flags
-    {
-        KT prev = KeyOps<KT>::empty();
-        for (uint32_t i = a; i < a + n; ++i) {
-            const KT x = sk[i];
-            rf[i] = KeyOps<KT>::eq(x, prev) ? 0 : 1;
+    uint32_t m = 0;  // run-start flags of positions p0 .. p0 + 7 (p0 = 8t)
+    constexpr int kPerT = kCapI / kCB;  // 8 positions per thread
+    static_assert(kPerT == 8, "8 flag bits per thread");
+    const uint32_t p0 = t * kPerT;
+    if (OKM_FULL_RANK) {
+        // every instance ranks itself inside its home (keys below it, and equal
+        // keys at earlier positions) and moves there: homes are key ranges in
+        // order, so this sorts the item; loops run over one home's keys (~2 at
+        // k=63, whose keys are ~98 % distinct) instead of a thread's whole slice
+        uint32_t dst[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            dst[u] = ~0u;
+            if ((uint32_t)u >= nrows) break;
+            if (!KeyOps<KT>::is_empty(kk[u])) {
+                const uint32_t h = hp[u] >> 16;
+                const uint32_t hs = half_of(hc[h >> 1], h);
+                const uint32_t he = h + 1 < (uint32_t)kHomes ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
+                const uint32_t me = hs + (hp[u] & 0xFFFFu);
+                uint32_t rank = hs;
+                for (uint32_t q = hs; q < he; ++q) {
+                    const KT y = sk[q];
+                    rank += (KeyOps<KT>::lt(y, kk[u]) || (q < me && KeyOps<KT>::eq(y, kk[u]))) ? 1u : 0u;
+                }
+                dst[u] = rank;
+            }
+        }
+        __syncthreads();  // every read of the home-ordered keys is done
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            if ((uint32_t)u >= nrows) break;
+            if (dst[u] != ~0u) {
+                sk[dst[u]] = kk[u];
+                if (W) sw[dst[u]] = ww[u];
+            }
+        }
+        __syncthreads();
+        PMARK(13);
+        // count.rs:33: a key's count = its run's length (weight); flag run starts
+        KT prev = p0 > 0 && p0 <= ntot ? sk[p0 - 1] : KeyOps<KT>::empty();
+#pragma unroll
+        for (int j = 0; j < kPerT; ++j) {
+            if (p0 + j >= ntot) break;
+            const KT x = sk[p0 + j];
+            m |= KeyOps<KT>::eq(x, prev) ? 0u : 1u << j;
             prev = x;
         }
-    }
-    __syncthreads();
-    uint32_t D;
-    {
-        constexpr int kPerT = kCapI / kCB;  // 8 positions per thread
-        static_assert(kPerT == 8, "two flag words per thread");
-        const uint32_t p0 = t * kPerT;
+    } else {
+        // each thread's 4 homes are one slice of sk: sort it and flag the first
+        // key of every run (count.rs:33: a key's count = its run's length/weight);
+        // the flags of the dead home counters' bytes (hc) are then compacted into
+        // run starts by the whole block, so the emit below is coalesced
+        slice_sort<W>(sk, sw, a, n);
+        PMARK(13);
+        uint8_t *rf = reinterpret_cast<uint8_t *>(hc);  // [kCapI] run-start flags
+        {
+            KT prev = KeyOps<KT>::empty();
+            for (uint32_t i = a; i < a + n; ++i) {
+                const KT x = sk[i];
+                rf[i] = KeyOps<KT>::eq(x, prev) ? 0 : 1;
+                prev = x;
+            }
+        }
+        __syncthreads();
         const uint32_t *rw = reinterpret_cast<const uint32_t *>(rf);
         const uint64_t fw = (uint64_t)rw[2 * t] | ((uint64_t)rw[2 * t + 1] << 32);
-        uint32_t m = 0;
 #pragma unroll
         for (int j = 0; j < kPerT; ++j) m |= ((fw >> (8 * j)) & 1u) && p0 + j < ntot ? 1u << j : 0u;
+    }
+    uint32_t D;
+    {
         uint32_t q = block_excl_scan32((uint32_t)__builtin_popcount(m), wsum, &D);
 #pragma unroll
         for (int j = 0; j < kPerT; ++j)
