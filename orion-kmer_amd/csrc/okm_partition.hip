@@ -273,21 +273,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
             __syncthreads();
             // tile-local bin offsets (nl <= kPartBlock: one bin per thread)
             const uint32_t my = t < nl ? hist[t] : 0u;
+            // sampled capacities: this tile's claim on its run of each bin is
+            // issued now and consumed after the scan and the staging, so the
+            // global atomic's round trip overlaps them
+            ull claim = 0;
+            if (!HC && my) claim = atomicAdd(&cursor[s.out_base + t], (ull)my);
             ull tile_n;
             const uint32_t off = (uint32_t)block_excl_scan<kPartBlock>(my, wsum, &tile_n);
             if (t < nl) lofs[t] = off;
-            if (!HC && t < nl) {  // sampled capacities: claim this tile's run
-                const uint32_t h = hist[t];
-                ull g = ~0ull;
-                if (h) {
-                    const ull p = atomicAdd(&cursor[s.out_base + t], (ull)h);
-                    if (p + h <= cap_end[s.out_base + t])
-                        g = p;
-                    else
-                        atomicOr(ovf, 1ull);
-                }
-                gcur[t] = g;
-            }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < P; ++u) {
@@ -296,6 +289,16 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                     stage[dst] = kk[u];
                     if (W) cstage[dst] = ww[u];
                 }
+            }
+            if (!HC && t < nl) {
+                ull g = ~0ull;
+                if (my) {
+                    if (claim + my <= cap_end[s.out_base + t])
+                        g = claim;
+                    else
+                        atomicOr(ovf, 1ull);
+                }
+                gcur[t] = g;
             }
             __syncthreads();
             // each bin's run is contiguous in `stage` and in the output slice
