@@ -375,7 +375,8 @@ struct Run {
 using namespace okm;
 
 static const size_t kHpinBytes = size_t(4) << 20;
-static const size_t kHresWords = 2048;  // [0, 1024): L1 readback; [1024, 1040): count readback
+static const size_t kHresWords = 4096;  // [0, 2048): L1 readback; [2048, 2064): count readback
+static const size_t kHresCount = 2048;
 
 struct okm_ctx {
     int device = 0;
@@ -596,7 +597,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     c->timer.end(c->stream, "extract_scatter", (double)n);
     launch_fill_line_tails(c->stream, cur, nb, run.keys, c->wide, c->l1cap);
     HIP_TRY(hipGetLastError());
-    unsigned long long *cap = c->hres, *ends = c->hres + 2 * nb + 2;  // 3 nb + 2 <= 1024 words
+    unsigned long long *cap = c->hres, *ends = c->hres + 2 * nb + 2;  // 3 nb + 2 <= kHresCount words
     HIP_TRY(hipMemcpyAsync(cap, c->l1cap, (2 * nb + 2) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipMemcpy2DAsync(ends, sizeof(unsigned long long), cur, OKM_L1_CUR_STRIDE * sizeof(unsigned long long),
@@ -1143,7 +1144,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
         HIP_TRY(hipGetLastError());
     }
-    unsigned long long *hv = c->hres + 1024;  // [0] distinct, [1] error word, [2..4] guard words
+    unsigned long long *hv = c->hres + kHresCount;  // [0] distinct, [1] error word, [2..4] guard words
     HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     if (guard)
@@ -1274,7 +1275,7 @@ static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_seg
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
     HIP_TRY(hipGetLastError());
-    unsigned long long *hv = c->hres + 1024;
+    unsigned long long *hv = c->hres + kHresCount;
     HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
@@ -1989,7 +1990,7 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->mode = mode;
     c->wide = k > 32;
     c->kw = c->wide ? 2 : 1;
-    c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins()), 2u * k);
+    c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins(k > 32)), 2u * k);
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
     {

@@ -52,10 +52,15 @@ static_assert(kScatBlock >= 256 && (16384 % kTile) == 0, "scatter tile must divi
 static_assert(kSegS % 16 == 0, "scan_windows loads whole 16-B words");
 constexpr int kSegH = 64;                      // hist: window starts per thread
 constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
-constexpr int kMaxL1Bins = 256;
+#ifndef OKM_L1_BITS  // first-level key-range bins of the k <= 32 extraction (2^bits <= kScatBlock)
+#define OKM_L1_BITS 8
+#endif
+constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
+constexpr int kMaxL1BinsW = 256;              // k in 33..64 kernels (256-thread blocks)
+static_assert(kMaxL1Bins <= kScatBlock, "one bin per scatter thread");
 
 uint32_t extract_tile() { return (uint32_t)kHTile; }  // chunks are multiples of both tiles
-uint32_t extract_max_bins() { return (uint32_t)kMaxL1Bins; }
+uint32_t extract_max_bins(bool wide) { return (uint32_t)(wide ? kMaxL1BinsW : kMaxL1Bins); }
 
 template <int K>
 __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq, ExtractGeom g,
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
         load_windows<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
-        if (t <= nb) hist[t] = 0;
+        for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
         __syncthreads();
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
         const bool live = w0 < end;
@@ -238,7 +243,7 @@ __device__ __forceinline__ uint32_t bin_of_wide(const K128 &key, uint32_t shift)
 __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8_t *__restrict__ seq, ExtractGeom g,
                                                                      uint32_t *__restrict__ HC,
                                                                      ull *__restrict__ Hg) {
-    __shared__ uint32_t lh[kMaxL1Bins + 1];
+    __shared__ uint32_t lh[kMaxL1BinsW + 1];
     for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
     __syncthreads();
     const uint64_t beg = (uint64_t)blockIdx.x * g.stride * g.chunk;  // stride > 1: a sample of the chunks
@@ -267,10 +272,10 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
                                                                         const ull *__restrict__ cap_end,
                                                                         ull *__restrict__ ovf) {
     __shared__ K128 stage[kTileW];
-    __shared__ ull gcur[kMaxL1Bins];
-    __shared__ uint32_t hist[kMaxL1Bins + 1];
-    __shared__ uint32_t lofs[kMaxL1Bins];
-    __shared__ uint32_t lcur[kMaxL1Bins];
+    __shared__ ull gcur[kMaxL1BinsW];
+    __shared__ uint32_t hist[kMaxL1BinsW + 1];
+    __shared__ uint32_t lofs[kMaxL1BinsW];
+    __shared__ uint32_t lcur[kMaxL1BinsW];
     __shared__ ull wsum[kExtractBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
@@ -329,10 +334,10 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const u
                                                                          const ull *__restrict__ cap_end,
                                                                          ull *__restrict__ ovf) {
     __shared__ K128 stage[kTileW + 64];  // + one dummy slot per lane for invalid windows
-    __shared__ ull gcur[kMaxL1Bins];
-    __shared__ uint32_t hist[kMaxL1Bins + 1];
-    __shared__ uint32_t lofs[kMaxL1Bins];
-    __shared__ uint32_t lcur[kMaxL1Bins];
+    __shared__ ull gcur[kMaxL1BinsW];
+    __shared__ uint32_t hist[kMaxL1BinsW + 1];
+    __shared__ uint32_t lofs[kMaxL1BinsW];
+    __shared__ uint32_t lcur[kMaxL1BinsW];
     __shared__ ull wsum[kExtractBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
@@ -480,14 +485,14 @@ void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_
 __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs, uint32_t nb, double scale,
                                                      double mul, uint32_t align, ull limit, ull *__restrict__ cursor,
                                                      ull *__restrict__ l1cap) {
-    __shared__ ull cap[kMaxL1Bins];
-    const uint32_t t = threadIdx.x;
-    if (t < nb) {
+    __shared__ ull cap[kMaxL1Bins > kMaxL1BinsW ? kMaxL1Bins : kMaxL1BinsW];
+    for (uint32_t t = threadIdx.x; t < nb; t += 256) {
         const double s = (double)Hs[t];
         const double r = sqrt(s) + 3.0;  // (sqrt(s) + 3)^2: the Poisson mean s allows at ~6 sigma
         const double c = (r * r * scale * 1.01 + 256.0) * mul;
         cap[t] = ((ull)c + align - 1) / align * align;
     }
+    const uint32_t t = threadIdx.x;
     __syncthreads();
     if (t == 0) {
         ull o = 0;

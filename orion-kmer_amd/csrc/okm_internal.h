@@ -123,7 +123,7 @@ void launch_part_capacity(void *stream, unsigned long long *H, uint32_t nout, co
 void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_t nbins, uint64_t *keys, bool wide,
                             const unsigned long long *cap = nullptr);
 uint32_t extract_tile();
-uint32_t extract_max_bins();
+uint32_t extract_max_bins(bool wide);  // L1 bins: k <= 32 kernels vs k in 33..64
 uint32_t part_max_bins(bool weighted);
 
 // Exclusive scan of n u64 values (in -> out, out may equal in); tmp >= scan_tmp_elems(n).
