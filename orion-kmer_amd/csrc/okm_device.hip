@@ -138,40 +138,44 @@ void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t 
                        parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw, fan);
 }
 
-// Fan-out split of one oversized child per job: its keys (<= kFanBlock *
-// kFanPer = 64 Ki) are counting-sorted by the next `bits` (<= 4) key bits into the
-// same index range of `dk` (order inside a sub-range is free: items are
-// multisets), and each sub-range becomes the item slot item0 + j.  Ranks come
-// from wave ballots (no LDS atomics on the few counters) and wait in LDS
-// between the two passes; the keys are read twice (the second time from L2:
-// a job is <= 1 MiB).
-constexpr int kFanBlock = 1024;
-constexpr int kFanPer = 64;
-constexpr int kFanWaves = kFanBlock / 64;
+// Fan-out split of one oversized child per job: its keys (<= 64 Ki) are
+// counting-sorted by the next `bits` (<= 4) key bits into the same index range
+// of `dk` (order inside a sub-range is free: items are multisets), and each
+// sub-range becomes the item slot item0 + j.  Ranks come from wave ballots (no
+// LDS atomics on the few counters) and wait in LDS between the two passes; the
+// keys are read twice (the second time from L2: a job is <= 1 MiB).  Jobs are
+// latency-bound (a few rows each), so two variants run: 512-thread
+// workgroups for jobs of <= 16 Ki keys (32 KiB of ranks: 4 workgroups per CU)
+// and 1024-thread ones with 128 KiB of ranks for the larger jobs.
 constexpr int kFanBins = 16;  // <= 4 bits per job
-uint64_t fan_split_max() { return (uint64_t)kFanBlock * kFanPer; }
+constexpr int kFanSmallBlock = 512, kFanSmallMax = 16384;
+constexpr int kFanBigBlock = 1024, kFanBigMax = 65536;
+uint64_t fan_split_max() { return (uint64_t)kFanBigMax; }
 
-template <typename KT, bool W>
-__global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__restrict__ jobs,
-                                                         const ull *__restrict__ flags, const KT *__restrict__ sk,
-                                                         const uint64_t *__restrict__ sc, KT *__restrict__ dk,
-                                                         uint64_t *__restrict__ dc, DevItem *__restrict__ items,
-                                                         DevSeg *__restrict__ segs, uint64_t item_max,
-                                                         uint32_t capbits, ull *__restrict__ oflags) {
-    __shared__ uint16_t brs[kFanBlock * kFanPer];  // per key: bin << 12 | rank within (wave, bin) (<= 64 rows x 64 lanes)
-    __shared__ uint32_t wtot[kFanWaves][kFanBins];  // per (wave, bin): count, then start in the job's range
+template <typename KT, bool W, int FB, int FMAX>
+__global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ jobs, const ull *__restrict__ flags,
+                                                  const KT *__restrict__ sk, const uint64_t *__restrict__ sc,
+                                                  KT *__restrict__ dk, uint64_t *__restrict__ dc,
+                                                  DevItem *__restrict__ items, DevSeg *__restrict__ segs,
+                                                  uint64_t item_max, uint32_t capbits, ull *__restrict__ oflags,
+                                                  uint64_t min_len) {
+    constexpr int kWaves = FB / 64;
+    static_assert(FMAX / FB * 64 <= 4096, "ranks fit 12 bits");
+    __shared__ uint16_t brs[FMAX];                // per key: bin << 12 | rank within (wave, bin)
+    __shared__ uint32_t wtot[kWaves][kFanBins];   // per (wave, bin): count, then start in the job's range
     __shared__ uint32_t btot[kFanBins];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
     for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
         const DevFanJob jb = jobs[jx];
+        if (jb.len <= min_len || jb.len > (uint64_t)FMAX) continue;  // the other variant's job (block-uniform)
         const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
-        const uint32_t rows = (uint32_t)((jb.len + kFanBlock - 1) / kFanBlock);  // block-uniform
+        const uint32_t rows = (uint32_t)((jb.len + FB - 1) / FB);  // block-uniform
         const ull lt = (1ull << lane) - 1ull;
         // pass 1: bins and ranks
         uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
         for (uint32_t u = 0; u < rows; ++u) {
-            const uint64_t idx = (uint64_t)u * kFanBlock + t;
+            const uint64_t idx = (uint64_t)u * FB + t;
             const KT key = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
             const bool v = !KeyOps<KT>::is_empty(key);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(key, shift) & (nb - 1)) : 0u;
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
                     run[q] += (uint32_t)__popcll(m);
                 }
             }
-            brs[u * kFanBlock + t] = (uint16_t)br;
+            brs[u * FB + t] = (uint16_t)br;
         }
 #pragma unroll
         for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
         __syncthreads();
         if (t < nb) {
             uint32_t s = 0;
-            for (int w = 0; w < kFanWaves; ++w) s += wtot[w][t];
+            for (int w = 0; w < kWaves; ++w) s += wtot[w][t];
             btot[t] = s;
         }
         __syncthreads();
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
             for (uint32_t q = 0; q < t; ++q) a += btot[q];
             const ull o = jb.off + a, len = btot[t];
             uint32_t w0 = a;
-            for (int w = 0; w < kFanWaves; ++w) {
+            for (int w = 0; w < kWaves; ++w) {
                 const uint32_t c = wtot[w][t];
                 wtot[w][t] = w0;
                 w0 += c;
@@ -232,11 +236,11 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
         __syncthreads();
         // pass 2: every key to its place (keys read again, from L2)
         for (uint32_t u = 0; u < rows; ++u) {
-            const uint64_t idx = (uint64_t)u * kFanBlock + t;
+            const uint64_t idx = (uint64_t)u * FB + t;
             if (idx >= jb.len) continue;
             const KT key = sk[jb.off + idx];
             if (KeyOps<KT>::is_empty(key)) continue;
-            const uint32_t br = brs[u * kFanBlock + t];
+            const uint32_t br = brs[u * FB + t];
             const ull o = jb.off + wtot[wv][br >> 12] + (br & 0xFFFu);
             dk[o] = key;
             if (W) dc[o] = sc ? sc[jb.off + idx] : 1ull;
@@ -245,30 +249,36 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_split(const DevFanJob *__rest
     }
 }
 
+template <typename KT, bool W>
+static void fan_launch(hipStream_t s, uint32_t max_jobs, const DevFanJob *jobs, const ull *flags, const KT *sk,
+                       const uint64_t *sc, KT *dk, uint64_t *dc, DevItem *items, DevSeg *segs, uint64_t item_max,
+                       uint32_t capbits, ull *oflags) {
+    const dim3 gs(max_jobs < 4096u ? max_jobs : 4096u), gb(max_jobs < 2048u ? max_jobs : 2048u);
+    hipLaunchKernelGGL((k_fan_split<KT, W, kFanSmallBlock, kFanSmallMax>), gs, dim3(kFanSmallBlock), 0, s, jobs,
+                       flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)0);
+    hipLaunchKernelGGL((k_fan_split<KT, W, kFanBigBlock, kFanBigMax>), gb, dim3(kFanBigBlock), 0, s, jobs, flags,
+                       sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)kFanSmallMax);
+}
+
 void launch_fan_split(void *stream, const DevFanJob *jobs, uint32_t max_jobs, const ull *flags, const uint64_t *sk,
                       const uint64_t *sc, uint64_t *dk, uint64_t *dc, DevItem *items, DevSeg *segs,
                       uint64_t item_max, uint32_t capbits, ull *oflags, bool wide) {
     if (!max_jobs) return;
-    const dim3 g(max_jobs < 2048u ? max_jobs : 2048u), b(kFanBlock);
     hipStream_t s = (hipStream_t)stream;
     if (wide) {
         const K128 *a = reinterpret_cast<const K128 *>(sk);
         K128 *d = reinterpret_cast<K128 *>(dk);
         if (sc)
-            hipLaunchKernelGGL((k_fan_split<K128, true>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
-                               item_max, capbits, oflags);
+            fan_launch<K128, true>(s, max_jobs, jobs, flags, a, sc, d, dc, items, segs, item_max, capbits, oflags);
         else
-            hipLaunchKernelGGL((k_fan_split<K128, false>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
-                               item_max, capbits, oflags);
+            fan_launch<K128, false>(s, max_jobs, jobs, flags, a, sc, d, dc, items, segs, item_max, capbits, oflags);
     } else {
         const ull *a = reinterpret_cast<const ull *>(sk);
         ull *d = reinterpret_cast<ull *>(dk);
         if (sc)
-            hipLaunchKernelGGL((k_fan_split<ull, true>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
-                               item_max, capbits, oflags);
+            fan_launch<ull, true>(s, max_jobs, jobs, flags, a, sc, d, dc, items, segs, item_max, capbits, oflags);
         else
-            hipLaunchKernelGGL((k_fan_split<ull, false>), g, b, 0, s, jobs, flags, a, sc, d, dc, items, segs,
-                               item_max, capbits, oflags);
+            fan_launch<ull, false>(s, max_jobs, jobs, flags, a, sc, d, dc, items, segs, item_max, capbits, oflags);
     }
 }
 
