@@ -147,6 +147,9 @@ void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t 
 // latency-bound (a few rows each), so two variants run: 512-thread
 // workgroups for jobs of <= 16 Ki keys (32 KiB of ranks: 4 workgroups per CU)
 // and 1024-thread ones with 128 KiB of ranks for the larger jobs.
+#ifndef OKM_FAN_REG  // unweighted jobs of <= 16 Ki keys: keys held in registers (read once)
+#define OKM_FAN_REG 1
+#endif
 constexpr int kFanBins = 16;  // <= 4 bits per job
 constexpr int kFanSmallBlock = 512, kFanSmallMax = 16384;
 constexpr int kFanBigBlock = 1024, kFanBigMax = 65536;
@@ -249,13 +252,117 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
     }
 }
 
+// Register variant for jobs of <= kFanRegMax keys (the common case: C3
+// shards, k=63): one 1024-thread workgroup per job holds the job's keys in
+// registers (16 rows), so they are read once — the LDS variants read them
+// twice (ranks first, keys again for the scatter) — and only the per-(wave,
+// bin) counters live in LDS (two workgroups per CU, VGPR-bound).
+constexpr int kFanRegBlock = 1024, kFanRegRows = 16, kFanRegMax = kFanRegBlock * kFanRegRows;
+
+template <typename KT>
+__global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob *__restrict__ jobs,
+                                                                const ull *__restrict__ flags,
+                                                                const KT *__restrict__ sk, KT *__restrict__ dk,
+                                                                DevItem *__restrict__ items,
+                                                                DevSeg *__restrict__ segs, uint64_t item_max,
+                                                                uint32_t capbits, ull *__restrict__ oflags) {
+    constexpr int kWaves = kFanRegBlock / 64;
+    __shared__ uint32_t wtot[kWaves][kFanBins];
+    __shared__ uint32_t btot[kFanBins];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
+    const ull lt = (1ull << lane) - 1ull;
+    for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
+        const DevFanJob jb = jobs[jx];
+        if (jb.len > (uint64_t)kFanRegMax) continue;  // the LDS variant's job (block-uniform)
+        const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
+        const uint32_t len = (uint32_t)jb.len;
+        KT kk[kFanRegRows];
+        uint32_t br[kFanRegRows];  // bin << 16 | rank within (wave, bin); ~0: no key
+#pragma unroll
+        for (int u = 0; u < kFanRegRows; ++u) {
+            const uint32_t idx = (uint32_t)u * kFanRegBlock + t;
+            kk[u] = idx < len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+        }
+        uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
+#pragma unroll
+        for (int u = 0; u < kFanRegRows; ++u) {
+            br[u] = ~0u;
+            if ((uint32_t)u * kFanRegBlock >= len) continue;  // block-uniform
+            const bool v = !KeyOps<KT>::is_empty(kk[u]);
+            const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(kk[u], shift) & (nb - 1)) : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q) {
+                if (q < nb) {  // block-uniform
+                    const ull m = __ballot(v && b == q);
+                    if (v && b == q) br[u] = (q << 16) | (run[q] + (uint32_t)__popcll(m & lt));
+                    run[q] += (uint32_t)__popcll(m);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
+            if (lane == 0) wtot[wv][q] = q < nb ? run[q] : 0u;
+        __syncthreads();
+        if (t < nb) {
+            uint32_t s = 0;
+            for (int w = 0; w < kWaves; ++w) s += wtot[w][t];
+            btot[t] = s;
+        }
+        __syncthreads();
+        if (t < nb) {  // thread q: bin q's item, and every wave's start in bin q
+            uint32_t a = 0;
+            for (uint32_t q = 0; q < t; ++q) a += btot[q];
+            const ull o = jb.off + a, n = btot[t];
+            uint32_t w0 = a;
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = wtot[w][t];
+                wtot[w][t] = w0;
+                w0 += c;
+            }
+            DevSeg sg;
+            sg.keys = reinterpret_cast<const uint64_t *>(dk + o);
+            sg.counts = nullptr;
+            sg.len = n;
+            sg.key_base = 0;
+            sg.out_base = 0;
+            sg.shift = kSingleBin;
+            sg.nlocal = 1;
+            sg.pad = 0;
+            segs[jb.item0 + t] = sg;
+            DevItem it;
+            it.seg_begin = jb.item0 + t;
+            it.seg_count = 1;
+            it.out_off = o;
+            it.rem_bits = jb.rem - jb.bits;
+            it.pad = n ? 0u : kItemEmpty;
+            it.total = n;
+            it.keys0 = sg.keys;
+            it.counts0 = nullptr;
+            items[jb.item0 + t] = it;
+            if (n > item_max && it.rem_bits > capbits) atomicAdd(&oflags[0], 1ull);
+            atomicMax(&oflags[2], n);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kFanRegRows; ++u)
+            if (br[u] != ~0u) dk[jb.off + wtot[wv][br[u] >> 16] + (br[u] & 0xFFFFu)] = kk[u];
+        __syncthreads();  // wtot reuse by the next job
+    }
+}
+
 template <typename KT, bool W>
 static void fan_launch(hipStream_t s, uint32_t max_jobs, const DevFanJob *jobs, const ull *flags, const KT *sk,
                        const uint64_t *sc, KT *dk, uint64_t *dc, DevItem *items, DevSeg *segs, uint64_t item_max,
                        uint32_t capbits, ull *oflags) {
     const dim3 gs(max_jobs < 4096u ? max_jobs : 4096u), gb(max_jobs < 2048u ? max_jobs : 2048u);
-    hipLaunchKernelGGL((k_fan_split<KT, W, kFanSmallBlock, kFanSmallMax>), gs, dim3(kFanSmallBlock), 0, s, jobs,
-                       flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)0);
+    if (!W && OKM_FAN_REG) {
+        hipLaunchKernelGGL((k_fan_split_reg<KT>), gb, dim3(kFanRegBlock), 0, s, jobs, flags, sk, dk, items, segs,
+                           item_max, capbits, oflags);
+    } else {
+        hipLaunchKernelGGL((k_fan_split<KT, W, kFanSmallBlock, kFanSmallMax>), gs, dim3(kFanSmallBlock), 0, s, jobs,
+                           flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)0);
+    }
     hipLaunchKernelGGL((k_fan_split<KT, W, kFanBigBlock, kFanBigMax>), gb, dim3(kFanBigBlock), 0, s, jobs, flags,
                        sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)kFanSmallMax);
 }
