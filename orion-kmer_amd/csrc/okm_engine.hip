@@ -1792,14 +1792,19 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         group_keys = (uint64_t)atoll(ge);
         mode = (gm && gm[0] == 'B') ? 2 : 1;
     } else if ((double)total * (ws_key + res_key) > avail) {
-        const double room_a = avail - (double)total * res_key;  // beside a bound-sized table
+        // beside a bound-sized table (its size is exact: the 3/4 margin is for
+        // the groups' working sets only)
+        const double room_a = 0.75 * (std::max(room, 0.0) - (double)total * res_key);
         // a bound-sized table is only worth it when it is a small share of HBM
         // (dense inputs such as k=63 long reads); with duplicated keys (a fold
         // of covered reads) exact per-group tables hold a fraction of it
         // ... and when the exact tables could not be joined anyway (their
         // worst case is the bound itself, twice over while joining)
+        // (then even at up to 256 groups: slower, but the join is what fails)
+        const double bound = (double)total * res_key;
         const bool a_fits = room_a >= (double)total * ws_key / 64.0;
-        if (a_fits && ((double)total * res_key <= 0.5 * avail || 2.0 * (double)total * res_key > avail)) {
+        const bool a_last = 2.0 * bound > avail && room_a >= (double)total * ws_key / 256.0;
+        if ((a_fits && (bound <= 0.5 * avail || 2.0 * bound > avail)) || a_last) {
             mode = 1;
             group_keys = (uint64_t)(room_a / ws_key);
         } else {
