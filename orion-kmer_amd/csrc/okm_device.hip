@@ -14,6 +14,11 @@ constexpr int kScanBlock = 256;
 constexpr int kScanPer = 8;
 constexpr uint64_t kScanTile = (uint64_t)kScanBlock * kScanPer;
 
+// Fan-out jobs of at most this many keys are "small" (the register / 512-thread
+// variants of k_fan_split); k_make_items files them from the front of the job
+// list and the larger ones from the back.
+constexpr uint64_t kFanSmallJob = 16384;
+
 __global__ __launch_bounds__(kScanBlock) void k_scan_block(const ull *__restrict__ in,
                                                            ull *__restrict__ out, uint64_t n,
                                                            ull *__restrict__ block_sums) {
@@ -123,7 +128,10 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
         items[(uint64_t)i * F + j] = it;
     }
     if (b) {
-        const ull jb = atomicAdd(&flags[3], 1ull);
+        // jobs of <= fan_split_small() keys from the front (flags[3] of them),
+        // larger ones from the back (flags[4]): each fan-out kernel variant
+        // walks only its own
+        const ull jb = len <= kFanSmallJob ? atomicAdd(&flags[3], 1ull) : nout - 1 - atomicAdd(&flags[4], 1ull);
         fan.jobs[jb] = DevFanJob{o, len, i * F, b, rem, 0};
     } else {
         atomicMax(&flags[2], len);
@@ -154,6 +162,7 @@ constexpr int kFanBins = 16;  // <= 4 bits per job
 constexpr int kFanSmallBlock = 512, kFanSmallMax = 16384;
 constexpr int kFanBigBlock = 1024, kFanBigMax = 65536;
 uint64_t fan_split_max() { return (uint64_t)kFanBigMax; }
+static_assert(kFanSmallMax == kFanSmallJob, "the job list's small/large cut is the small variants' capacity");
 
 template <typename KT, bool W, int FB, int FMAX>
 __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ jobs, const ull *__restrict__ flags,
@@ -161,17 +170,20 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
                                                   KT *__restrict__ dk, uint64_t *__restrict__ dc,
                                                   DevItem *__restrict__ items, DevSeg *__restrict__ segs,
                                                   uint64_t item_max, uint32_t capbits, ull *__restrict__ oflags,
-                                                  uint64_t min_len) {
+                                                  uint32_t max_jobs) {
     constexpr int kWaves = FB / 64;
     static_assert(FMAX / FB * 64 <= 4096, "ranks fit 12 bits");
     __shared__ uint16_t brs[FMAX];                // per key: bin << 12 | rank within (wave, bin)
     __shared__ uint32_t wtot[kWaves][kFanBins];   // per (wave, bin): count, then start in the job's range
     __shared__ uint32_t btot[kFanBins];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
+    // the small jobs sit at the front of `jobs` (flags[3]), the large ones at
+    // the back (flags[4])
+    constexpr bool kBig = FMAX > kFanSmallMax;
+    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[kBig ? 4 : 3]);
+    const uint32_t j0 = kBig ? max_jobs - njobs : 0u;
     for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
-        const DevFanJob jb = jobs[jx];
-        if (jb.len <= min_len || jb.len > (uint64_t)FMAX) continue;  // the other variant's job (block-uniform)
+        const DevFanJob jb = jobs[j0 + jx];
         const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
         const uint32_t rows = (uint32_t)((jb.len + FB - 1) / FB);  // block-uniform
         const ull lt = (1ull << lane) - 1ull;
@@ -258,6 +270,7 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
 // twice (ranks first, keys again for the scatter) — and only the per-(wave,
 // bin) counters live in LDS (two workgroups per CU, VGPR-bound).
 constexpr int kFanRegBlock = 1024, kFanRegRows = 16, kFanRegMax = kFanRegBlock * kFanRegRows;
+static_assert(kFanRegMax == kFanSmallJob, "the register variant takes every small job");
 
 template <typename KT>
 __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob *__restrict__ jobs,
@@ -270,11 +283,10 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
     __shared__ uint32_t wtot[kWaves][kFanBins];
     __shared__ uint32_t btot[kFanBins];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);
+    const uint32_t njobs = __builtin_amdgcn_readfirstlane((uint32_t)flags[3]);  // the small jobs
     const ull lt = (1ull << lane) - 1ull;
     for (uint32_t jx = blockIdx.x; jx < njobs; jx += gridDim.x) {
         const DevFanJob jb = jobs[jx];
-        if (jb.len > (uint64_t)kFanRegMax) continue;  // the LDS variant's job (block-uniform)
         const uint32_t nb = 1u << jb.bits, shift = jb.rem - jb.bits;
         const uint32_t len = (uint32_t)jb.len;
         KT kk[kFanRegRows];
@@ -361,10 +373,12 @@ static void fan_launch(hipStream_t s, uint32_t max_jobs, const DevFanJob *jobs, 
                            item_max, capbits, oflags);
     } else {
         hipLaunchKernelGGL((k_fan_split<KT, W, kFanSmallBlock, kFanSmallMax>), gs, dim3(kFanSmallBlock), 0, s, jobs,
-                           flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)0);
+                           flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags, max_jobs);
     }
-    hipLaunchKernelGGL((k_fan_split<KT, W, kFanBigBlock, kFanBigMax>), gb, dim3(kFanBigBlock), 0, s, jobs, flags,
-                       sk, sc, dk, dc, items, segs, item_max, capbits, oflags, (uint64_t)kFanSmallMax);
+    // the large jobs are rare: a small grid walks them
+    hipLaunchKernelGGL((k_fan_split<KT, W, kFanBigBlock, kFanBigMax>), dim3(max_jobs < 512u ? max_jobs : 512u),
+                       dim3(kFanBigBlock), 0, s, jobs, flags, sk, sc, dk, dc, items, segs, item_max, capbits, oflags,
+                       max_jobs);
 }
 
 void launch_fan_split(void *stream, const DevFanJob *jobs, uint32_t max_jobs, const ull *flags, const uint64_t *sk,

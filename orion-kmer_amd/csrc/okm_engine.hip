@@ -1629,10 +1629,10 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
             // the first host sync of the round comes after the compaction.
             for (int attempt = 0;; ++attempt) {
                 unsigned long long *flags;  // [0] children too big, [1] 1: slot overflow | 2: 64-bit counts, [2] max,
-                                            // [3] fan-out jobs
-                OKM_TRY(pool_get(c->pool, 4, &flags));
+                                            // [3] / [4] fan-out jobs (small / large)
+                OKM_TRY(pool_get(c->pool, 5, &flags));
                 level_bufs.push_back(flags);
-                HIP_TRY(hipMemsetAsync(flags, 0, 4 * sizeof(unsigned long long), c->stream));
+                HIP_TRY(hipMemsetAsync(flags, 0, 5 * sizeof(unsigned long long), c->stream));
                 Level L;
                 OKM_TRY(split_launch(c, segtab, parts, all, bits, weighted, level_bufs, L,
                                      try_sampled && !attempt ? flags + 1 : nullptr));

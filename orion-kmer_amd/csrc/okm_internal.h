@@ -188,7 +188,8 @@ uint64_t fan_split_max();
 // the device offsets (nout + 1 entries; bin b ends at ends[b], or at
 // offs[b + 1] when ends is null).  flags[0] += children that are still too
 // big for one item; flags[1] |= 2 when a child needs 64-bit counting;
-// flags[2] = max child length; flags[3] = fan-out jobs.  Count and compact
+// flags[2] = max child length; flags[3] / flags[4] = fan-out jobs of <= / >
+// 16 Ki keys (filed from the front / the back of fan.jobs[nout]).  Count and compact
 // kernels given `guard` (= flags) return at once when guard[0] or guard[1] is
 // set.  With fan.bits, item/segment slot i * 2^bits + j belongs to child i.
 void launch_make_items(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
