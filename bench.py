@@ -182,7 +182,7 @@ def main():
     if dist_on:
         # product path: the library's own RCCL communicator (okm_comm +
         # okm_merge_owned: HIP owner split / pack / unpack kernels, grouped
-        # ncclSend/ncclRecv over xGMI, k-way LDS merge); torch.distributed (gloo,
+        # ncclSend/ncclRecv over xGMI, owner count of the sorted slices); torch.distributed (gloo,
         # host) only hands out the communicator id, barriers and the max-time
         # reduce.  OKM_BENCH_BACKEND=gloo rehearses the exchange through torch
         # (okm/dist.py) instead: RCCL refuses two ranks on one device.
@@ -418,7 +418,7 @@ def main():
         out["config"]["owned_distinct_rank0"] = int(n_owned)
         out["exchange_ms_per_step_rank0"] = {"exchange": round(xt[0] / args.steps * 1e3, 3),
                                              "merge": round(xt[1] / args.steps * 1e3, 3)}
-        out["exchange_impl"] = ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, k-way LDS merge)"
+        out["exchange_impl"] = ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
                                 if comm is not None else "torch gloo rehearsal (okm/dist.py)")
     emit(out)
     if comm is not None:
@@ -606,7 +606,7 @@ def main_c3(args):
                             "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
                             "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
                             "input_stream_frac": round(shard_bases * args.steps / dt / 8e12, 5)},
-        "exchange_impl": ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, k-way LDS merge)"
+        "exchange_impl": ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
                           if comm is not None else ("torch gloo rehearsal" if dist_on else None)),
         "phase_ms_per_step_rank0": {"count": round(xt[0] / args.steps * 1e3, 2),
                                     "exchange": round(xt[1] / args.steps * 1e3, 2),

@@ -196,6 +196,47 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
     }
 }
 
+// A multi-segment item (sorted runs: every run's slice of one key range) with
+// its segment descriptors staged in LDS first — one parallel load instead of
+// seg_count dependent ones before the keys can be fetched.  Block-uniform
+// call (it contains barriers); seg_count <= kSegCache.
+constexpr int kSegCache = 64;
+template <bool W, typename KT = ull>
+__device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *__restrict__ segs, KT (&kk)[kPer],
+                                               ull (&ww)[kPer], const uint64_t **ck, const uint64_t **cc,
+                                               uint32_t *coff) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t R = __builtin_amdgcn_readfirstlane(it.seg_count);
+    if (t < R) {
+        const DevSeg s = segs[it.seg_begin + t];
+        ck[t] = s.keys;
+        cc[t] = s.counts;
+        coff[t + 1] = (uint32_t)s.len;
+    }
+    __syncthreads();
+    if (t == 0) {
+        coff[0] = 0;
+        for (uint32_t r = 0; r < R; ++r) coff[r + 1] += coff[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        kk[u] = KeyOps<KT>::empty();
+        ww[u] = 1;
+        const uint32_t f = (uint32_t)u * kCB + t;
+        if (f < coff[R]) {
+            uint32_t lo = 0, hi = R;  // segment of f: last r with coff[r] <= f
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (coff[mid] <= f) lo = mid; else hi = mid;
+            }
+            const uint32_t p = f - coff[lo];
+            kk[u] = reinterpret_cast<const KT *>(ck[lo])[p];
+            if (W && cc[lo]) ww[u] = cc[lo][p];
+        }
+    }
+}
+
 // Insertion sort of sk[a, a + n) (+ weights), n small.
 template <bool W, typename KT>
 __device__ __forceinline__ void slice_sort(KT *sk, ull *sw, uint32_t a, uint32_t n) {
@@ -633,6 +674,12 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
+    // multi-segment items: their descriptors are staged in the rest buffer,
+    // which is free until tag_item's step 3 (the keys are in registers by then)
+    const uint64_t **seg_k = reinterpret_cast<const uint64_t **>(reinterpret_cast<char *>(lds) + Lds<W>::kFixed);
+    const uint64_t **seg_c = seg_k + kSegCache;
+    uint32_t *seg_off = reinterpret_cast<uint32_t *>(seg_c + kSegCache);
+    static_assert(kSegCache * 20 + 4 <= Lds<W>::kRest * 8, "segment cache fits the rest buffer");
     const uint32_t t = threadIdx.x;
     tag_reset<W>(lds);
     if (OKM_COUNT_PROF && t == 0) g_prof_last = clock64();
@@ -650,7 +697,12 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
         if (it.rem_bits > (uint32_t)kDenseBits && total <= (uint64_t)kCapI) {
             ull kk[kPer];
             ull ww[kPer];
-            load_item<W>(it, segs, kk, ww);
+            // (weighted launches only: the unweighted kernel sits at its 64-VGPR
+            // cap and the staged load costs it spills)
+            if (W && it.seg_count > 1 && it.seg_count <= (uint32_t)kSegCache)
+                load_item_segs<W>(it, segs, kk, ww, seg_k, seg_c, seg_off);
+            else
+                load_item<W>(it, segs, kk, ww);
             PMARK(1);
             const uint32_t nrows = (uint32_t)((total + kCB - 1) / kCB);  // rows of kk in use (block-uniform)
             written = tag_item<W>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);

@@ -19,8 +19,9 @@
 //      (position, value) that overwrites the byte on arrival, k_apply_escapes):
 //      9 B per pair on a point-to-point xGMI link instead of 16;
 //   4. the owner adds every rank's slice — each one sorted — without copying
-//      (okm_add_sorted_pairs_device) and counts them with the k-way LDS merge
-//      (okm_merge.hip): counts add, the fetch_add of count.rs:31-34.
+//      (okm_add_sorted_pairs_device) and counts them as key-range items split
+//      out of every slice by binary search: counts add, the fetch_add of
+//      count.rs:31-34.
 //
 // RCCL is loaded at run time (dlopen), so the library still loads where no
 // RCCL is installed; only the okm_comm_* calls then fail, with OKM_E_COMM.
@@ -534,7 +535,7 @@ okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t
     HIP_TRY(hipStreamSynchronize(s));  // received: the owner's stream may read the slices
     const double t_x = ms_since(t0);
 
-    // 5. the owner merges the P sorted slices in place (k-way LDS merge)
+    // 5. the owner counts the P sorted slices in place (key-range items)
     OKM_TRY(okm_reset(owner));
     for (uint32_t r = 0; r < P; ++r) {
         if (r == me && self_borrow && self_n) {

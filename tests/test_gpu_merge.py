@@ -1,9 +1,11 @@
-"""The k-way LDS merge of sorted runs (okm_merge.hip) behind
-okm_add_sorted_pairs_device: the multi-GPU owner's merge of per-rank slices
-(SURVEY.md §8(e)), set unions (compare.rs:51-66, db_types.rs:43-53) and
-folded batch tables (count.rs:52-89).  Exact against numpy, for u64 and
-128-bit keys, weighted and unweighted runs, many runs, dense key ranges, and
-against the hashing count kernel (OKM_NO_MERGE_KERNEL=1)."""
+"""Counting of sorted runs behind okm_add_sorted_pairs_device: the multi-GPU
+owner's merge of per-rank slices, set unions
+(compare.rs:51-66, db_types.rs:43-53) and folded batch tables
+(count.rs:52-89).  The runs are split into key-range items by binary search
+(no key moves) and counted by the count kernel (default) or the k-way LDS
+merge kernel of okm_merge.hip (OKM_MERGE_KERNEL=1).  Exact against numpy, for
+u64 and 128-bit keys, weighted and unweighted runs, many runs, dense key
+ranges, both kernels."""
 
 import numpy as np
 import pytest
@@ -49,7 +51,10 @@ def _runs(rng, nruns, n, span, k):
     (64, 20_000, 1 << 22, True),        # the most runs one merge item tracks
     (70, 10_000, 1 << 22, True),        # more: the hashing count kernel takes over
 ])
-def test_merge_runs_vs_numpy(nruns, n, span, weighted):
+@pytest.mark.parametrize("merge_kernel", [False, True])
+def test_merge_runs_vs_numpy(nruns, n, span, weighted, merge_kernel, monkeypatch):
+    if merge_kernel:
+        monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
     rng = np.random.default_rng(nruns * 7 + n)
     k = 31
     runs = _runs(rng, nruns, n, span, k)
@@ -75,7 +80,7 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
     out = []
     for env in (None, "1"):
         if env:
-            monkeypatch.setenv("OKM_NO_MERGE_KERNEL", "1")
+            monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
         bufs = []
         with okm.KmerCounter(31) as m:
             m.set_timing(True)
@@ -85,11 +90,14 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
                 m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
             out.append(m.result(1))
             names = set(m.kernel_stats())
-        assert ("merge_write" in names) == (env is None)
+        assert ("merge_write" in names) == (env is not None)
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
-def test_merge_wide_keys():
+@pytest.mark.parametrize("merge_kernel", [False, True])
+def test_merge_wide_keys(merge_kernel, monkeypatch):
+    if merge_kernel:
+        monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
     rng = np.random.default_rng(11)
     k = 45
     runs = []
