@@ -491,6 +491,20 @@ static void invalidate_result(okm_ctx *c) {
     c->counted = false;
 }
 
+// Device memory this context may still use: free + its pool's cached blocks,
+// and no more than the room under the pools' soft cap (OKM_HBM_CAP).
+static double device_room(okm_ctx *c) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        free_b = 0;
+    }
+    const double cached = (double)c->pool.cached();
+    double room = (double)free_b + cached;
+    if (total_b) room = std::min(room, hbm_cap_frac() * (double)total_b - (double)(total_b - free_b) + cached);
+    return std::max(room, 0.0);
+}
+
 static okm_status sync(okm_ctx *c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipGetLastError());
@@ -1420,12 +1434,21 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     c->info.max_partition = hf[1];
     // k-way LDS merge of the runs' sorted slices; the hashing count kernel
     // only for more runs than one merge workgroup tracks
-    // The k-way merge kernel only on request (OKM_MERGE_KERNEL=1): the count
-    // kernel over the same multi-segment items measured faster at every run
-    // count (C3 owner slices, tools/merge8_cost.py: 2 runs 3.9 vs 4.3 ms, 4
-    // runs 7.2 vs 13.1, 8 runs 27.0 vs 53.4 ms)
+    // The count kernel over these multi-segment items measured faster than the
+    // k-way merge kernel at every run count (C3 owner slices,
+    // tools/merge8_cost.py: 2 runs 3.9 vs 4.3 ms, 4 runs 7.2 vs 13.1, 8 runs
+    // 27.0 vs 53.4 ms), but it needs instance-bound slots and result (~2 x 16 B
+    // per pair) where the merge kernel writes the table once at its exact size:
+    // the merge kernel when that does not fit (the last folds of C3 on one GPU),
+    // or on request (OKM_MERGE_KERNEL=1)
+    // (and always for a context's own folded tables: a fold runs at the memory
+    // limit by design, C3 on one GPU folds up to ~2.5 G pairs at once)
+    bool folded = false;
+    for (auto &r : c->runs) folded |= r.folded;
     const bool use_merge = getenv("OKM_MERGE_KERNEL") != nullptr && getenv("OKM_NO_MERGE_KERNEL") == nullptr;
-    const bool merge = use_merge && R <= merge_max_runs() && item_max <= merge_item_capacity();
+    const double need = 2.0 * (8.0 * c->kw + 8.0) * (double)in_total;
+    const bool tight = getenv("OKM_NO_MERGE_KERNEL") == nullptr && (folded || need > 0.75 * device_room(c));
+    const bool merge = (use_merge || tight) && R <= merge_max_runs() && item_max <= merge_item_capacity();
     if (merge) return merge_sorted_items(c, d_items, d_segs, nitems, in_total, weighted, bufs);
     return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
 }
@@ -1776,18 +1799,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     // per instance: level + fan-out copy + staged keys (+ slack) + staged counts (+ weights of both levels)
     const double ws_key = 8.0 * c->kw * 4 + 8.0 + (weighted ? 16.0 : 0.0);
     const double res_key = 8.0 * c->kw + 8.0;     // result entry (instance bound)
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-        (void)hipGetLastError();
-        free_b = 0;
-    }
     // 3/4 of what is free: sampled capacities, line padding and the pool's size
     // classes make a pass hold more than its keys
-    // ... and no more than the room under the pool's soft cap (OKM_HBM_CAP)
-    const double cached = (double)c->pool.cached();
-    double room = (double)free_b + cached;
-    if (total_b) room = std::min(room, hbm_cap_frac() * (double)total_b - (double)(total_b - free_b) + cached);
-    const double avail = 0.75 * std::max(room, 0.0);
+    const double room = device_room(c);
+    const double avail = 0.75 * room;
     uint64_t group_keys = total;
     int mode = 0;  // 0: one group (no grouping)
     const char *ge = getenv("OKM_GROUP_KEYS");
@@ -1796,9 +1811,11 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         group_keys = (uint64_t)atoll(ge);
         mode = (gm && gm[0] == 'B') ? 2 : 1;
     } else if ((double)total * (ws_key + res_key) > avail) {
-        // beside a bound-sized table (its size is exact: the 3/4 margin is for
-        // the groups' working sets only)
-        const double room_a = 0.75 * (std::max(room, 0.0) - (double)total * res_key);
+        // beside a bound-sized table: the 3/4 margin over both (room_a), or —
+        // the last resort below, when per-group tables could not be joined —
+        // over the groups' working sets only (room_l: the table's size is exact)
+        const double room_a = avail - (double)total * res_key;
+        const double room_l = 0.75 * (std::max(room, 0.0) - (double)total * res_key);
         // a bound-sized table is only worth it when it is a small share of HBM
         // (dense inputs such as k=63 long reads); with duplicated keys (a fold
         // of covered reads) exact per-group tables hold a fraction of it
@@ -1807,10 +1824,13 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         // (then even at up to 256 groups: slower, but the join is what fails)
         const double bound = (double)total * res_key;
         const bool a_fits = room_a >= (double)total * ws_key / 64.0;
-        const bool a_last = 2.0 * bound > avail && room_a >= (double)total * ws_key / 256.0;
-        if ((a_fits && (bound <= 0.5 * avail || 2.0 * bound > avail)) || a_last) {
+        const bool a_last = 2.0 * bound > avail && room_l >= (double)total * ws_key / 256.0;
+        if (a_fits && (bound <= 0.5 * avail || 2.0 * bound > avail)) {
             mode = 1;
             group_keys = (uint64_t)(room_a / ws_key);
+        } else if (a_last) {
+            mode = 1;
+            group_keys = (uint64_t)(room_l / ws_key);
         } else {
             mode = 2;  // a bound-sized table per group, plus the finished groups' exact tables
             group_keys = (uint64_t)(avail * 0.6 / (ws_key + res_key));

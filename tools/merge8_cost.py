@@ -63,7 +63,14 @@ for R in merge_counts:
         nd = owner.count()
         owner.synchronize()
         times.append((time.perf_counter() - t0) * 1e3)
+    owner.set_timing(True)  # one more rep for the per-kernel split
+    owner.reset()
+    for kp, cp, m in slices[:R]:
+        owner.add_sorted_pairs_device(kp, cp, m)
+    owner.count()
+    kstats = {k: round(v["total_ms"], 2) for k, v in owner.kernel_stats().items()}
+    owner.set_timing(False)
     pairs = sum(s[2] for s in slices[:R])
     print(json.dumps({"what": f"owner merge of {R} of the 8 slices rank 0 receives at P=8 (C3)", "runs": R,
                       "pairs_in": pairs, "distinct_out": nd, "merge_ms": round(statistics.median(times[1:]), 2),
-                      "all_ms": [round(t, 2) for t in times[1:]]}))
+                      "all_ms": [round(t, 2) for t in times[1:]], "kernels_ms": kstats}))
