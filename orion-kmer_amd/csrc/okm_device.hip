@@ -468,28 +468,52 @@ void launch_bin_bounds(void *stream, const uint64_t *keys, uint64_t n, uint32_t 
 
 // One thread per item: item i is child c of part parts[p] (split by `bits`);
 // its segment in run r is the child's key range within rbins[p * nruns + r].
-template <typename KT>
-__global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t nparts, uint32_t nitems,
-                               const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1, uint32_t kw,
-                               DevItem *__restrict__ items, DevSeg *__restrict__ segs, ull *__restrict__ itemtot,
-                               uint64_t item_max, uint32_t capbits, ull *__restrict__ flags) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nitems) return;
+// The part of item i (parts sorted by item_base).
+__device__ __forceinline__ uint32_t sorted_part_of(const DevSortedPart *__restrict__ parts, uint32_t nparts,
+                                                   uint32_t i) {
     uint32_t lo = 0, hi = nparts;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (parts[mid].item_base <= i) lo = mid; else hi = mid;
     }
-    const DevSortedPart P = parts[lo];
+    return lo;
+}
+
+// bounds[i * nruns + r] = where item i's key range starts in run r: one
+// thread per (item, run), so the binary searches over the runs run side by
+// side instead of 2 x nruns of them back to back in one thread per item.
+template <typename KT>
+__global__ void k_sorted_bounds(const DevSortedPart *__restrict__ parts, uint32_t nparts, uint32_t nitems,
+                                const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1,
+                                ull *__restrict__ bounds) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= (uint64_t)nitems * nruns) return;
+    const uint32_t i = (uint32_t)(x / nruns), r = (uint32_t)(x % nruns);
+    const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
+    const uint32_t c = i - P.item_base;
+    const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
+    bounds[x] = P.bits && c ? lower_bound_bin(reinterpret_cast<const KT *>(rb.keys), 0, rb.len, shift1 - P.bits,
+                                              (uint64_t)P.bin << P.bits, c)
+                            : 0;
+}
+
+template <typename KT>
+__global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t nparts, uint32_t nitems,
+                               const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1, uint32_t kw,
+                               DevItem *__restrict__ items, DevSeg *__restrict__ segs, ull *__restrict__ itemtot,
+                               uint64_t item_max, uint32_t capbits, ull *__restrict__ flags,
+                               const ull *__restrict__ bounds) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems) return;
+    const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
     const uint32_t c = i - P.item_base;
     const uint32_t shift = shift1 - P.bits;                 // child = next `bits` key bits
-    const uint64_t base = (uint64_t)P.bin << P.bits;       // (key >> shift) - base = child index
+    const bool last = !P.bits || c + 1 == (1u << P.bits);  // the part's last child ends where its range does
     ull tot = 0;
     for (uint32_t r = 0; r < nruns; ++r) {
         const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
-        const KT *k = reinterpret_cast<const KT *>(rb.keys);
-        const uint64_t s0 = P.bits ? lower_bound_bin(k, 0, rb.len, shift, base, c) : 0;
-        const uint64_t s1 = P.bits && c + 1 < (1u << P.bits) ? lower_bound_bin(k, s0, rb.len, shift, base, c + 1) : rb.len;
+        const uint64_t s0 = bounds[(uint64_t)i * nruns + r];
+        const uint64_t s1 = last ? rb.len : bounds[(uint64_t)(i + 1) * nruns + r];
         DevSeg sg;
         sg.keys = rb.keys + s0 * kw;
         sg.counts = rb.counts ? rb.counts + s0 : nullptr;
@@ -525,15 +549,20 @@ __global__ void k_set_out_off(DevItem *__restrict__ items, uint32_t nitems, cons
 void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
                          const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
                          unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
-                         bool wide) {
+                         bool wide, unsigned long long *bounds) {
     if (!nitems) return;
     const dim3 g((nitems + 255) / 256), b(256);
-    if (wide)
-        hipLaunchKernelGGL(k_sorted_items<K128>, g, b, 0, (hipStream_t)stream, parts, nparts, nitems, rbins, nruns,
-                           shift1, 2u, items, segs, itemtot, item_max, capbits, flags);
-    else
-        hipLaunchKernelGGL(k_sorted_items<ull>, g, b, 0, (hipStream_t)stream, parts, nparts, nitems, rbins, nruns,
-                           shift1, 1u, items, segs, itemtot, item_max, capbits, flags);
+    const dim3 gb((uint32_t)(((uint64_t)nitems * nruns + 255) / 256));
+    hipStream_t s = (hipStream_t)stream;
+    if (wide) {
+        hipLaunchKernelGGL(k_sorted_bounds<K128>, gb, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, bounds);
+        hipLaunchKernelGGL(k_sorted_items<K128>, g, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, 2u, items,
+                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds);
+    } else {
+        hipLaunchKernelGGL(k_sorted_bounds<ull>, gb, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, bounds);
+        hipLaunchKernelGGL(k_sorted_items<ull>, g, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, 1u, items,
+                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds);
+    }
 }
 
 void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off) {

@@ -1391,7 +1391,10 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &offs));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &tmp));
     OKM_TRY(pool_get(c->pool, 2, &flags));
-    for (void *p : {(void *)d_parts, (void *)d_rbins, (void *)itemtot, (void *)offs, (void *)tmp, (void *)flags})
+    unsigned long long *bounds;
+    OKM_TRY(pool_get(c->pool, std::max<size_t>((size_t)nitems * R, 1), &bounds));
+    for (void *p : {(void *)d_parts, (void *)d_rbins, (void *)itemtot, (void *)offs, (void *)tmp, (void *)flags,
+                    (void *)bounds})
         bufs.push_back(p);
     OKM_TRY(h2d(c, d_parts, parts.data(), parts.size() * sizeof(DevSortedPart)));
     OKM_TRY(h2d(c, d_rbins, rbins.data(), rbins.size() * sizeof(DevSeg)));
@@ -1399,7 +1402,7 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     HIP_TRY(hipMemsetAsync(itemtot + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     launch_sorted_items(c->stream, d_parts, (uint32_t)parts.size(), nitems, d_rbins, R, c->shift1, d_items, d_segs,
-                        itemtot, item_max, capbits, flags, c->wide);
+                        itemtot, item_max, capbits, flags, c->wide, bounds);
     launch_exclusive_scan(c->stream, itemtot, offs, (uint64_t)nitems + 1, tmp);
     launch_set_out_off(c->stream, d_items, nitems, offs);
     c->timer.end(c->stream, "sorted_items", 0.0);

@@ -213,13 +213,14 @@ struct DevSortedPart {
     uint32_t item_base;  // first item of its children
     uint32_t slot;       // row of the part in the rbins table
 };
-// One multi-segment item per child: segs[i * nruns + r] = the child's key range
+// One multi-segment item per child (bounds: nitems * nruns words of scratch):
+// segs[i * nruns + r] = the child's key range
 // in run r (rbins[slot * nruns + r] = the part's range in run r); itemtot[i]
 // = its instances; flags[0] += children still too big, flags[1] = max.
 void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
                          const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
                          unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
-                         bool wide);
+                         bool wide, unsigned long long *bounds);
 void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off);
 
 // Gather the per-item results into dense arrays given exclusive offsets
