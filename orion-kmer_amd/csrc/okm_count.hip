@@ -271,7 +271,8 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 template <bool W, typename KT>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
                                               const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
-                                              uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts) {
+                                              uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
+                                              bool nowrite) {
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
@@ -396,7 +397,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     }
     __syncthreads();
     PMARK(14);
-    for (uint32_t p = t; p < D; p += kCB) {
+    for (uint32_t p = t; p < (nowrite ? 0u : D); p += kCB) {
         const uint32_t b = first[p], e = first[p + 1];
         out_keys[out_off + p] = sk[b];
         ull c = 0;
@@ -416,7 +417,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
 
 constexpr uint32_t kDeferred = ~0u;
 
-template <bool W>
+template <bool W, bool NW = false>
 __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
                                              const ull (&kk)[kPer], const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
                                              uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts) {
@@ -560,7 +561,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         }
 #pragma unroll
         for (int q = 0; q < kHomesPer; ++q) {
-            if (tg[q] != kEmptyKey) {
+            if (!NW && tg[q] != kEmptyKey) {
                 const uint64_t o = out_off + ho[q] + lq[q];
                 out_keys[o] = tg[q];
                 store_count<W>(out_counts, o, W ? (uint64_t)tc64[kHomesPer * t + q] : (uint64_t)nq[q]);
@@ -570,7 +571,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     // 6b. rest keys: rank = home offset + rest distinct keys below + [tag below]
 #pragma unroll
     for (int k = 0; k < L::kRestIters; ++k) {
-        if ((uint32_t)k * kCB >= rtot) break;
+        if (NW || (uint32_t)k * kCB >= rtot) break;
         if (prange[k]) {
             const ull x = px[k];
             const uint32_t hs = prange[k] >> 16, he = prange[k] & 0xFFFFu;
@@ -608,7 +609,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 template <bool W, typename KT>
 __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *__restrict__ segs,
                                                uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
-                                               ull *lds, uint32_t *wsum) {
+                                               ull *lds, uint32_t *wsum, bool nowrite) {
     typedef typename CountType<W>::T CT;
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
@@ -652,7 +653,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
     uint64_t o = it.out_off + block_excl_scan32(d, wsum, &D);
     for (uint32_t q = 0; q < kHomesPer; ++q) {
         const uint32_t j = t * kHomesPer + q;
-        if (j < nslots && cnt[j] != 0) {
+        if (!nowrite && j < nslots && cnt[j] != 0) {
             out_keys[o] = slot_key[j];
             store_count<W>(out_counts, o, (uint64_t)cnt[j]);
             ++o;
@@ -664,7 +665,9 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
 // Tag-mode kernel.  Items it cannot take (dense-mode items, rest overflow)
 // go to the deferred list defer[ctl[1]++] for k_count_slow, which runs right
 // after it: separate kernels keep the rare paths' registers out of this one.
-template <bool W>
+// NW (weighted launches only): count each item's distinct keys into n_out and
+// write nothing -- the first pass of an exact-size two-pass count.
+template <bool W, bool NW = false>
 __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM_COUNT_WPE)))
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
@@ -705,7 +708,7 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
                 load_item<W>(it, segs, kk, ww);
             PMARK(1);
             const uint32_t nrows = (uint32_t)((total + kCB - 1) / kCB);  // rows of kk in use (block-uniform)
-            written = tag_item<W>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);
+            written = tag_item<W, NW>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);
         }
         if (t == 0) {
             if (written == kDeferred)
@@ -726,7 +729,8 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
                                                     uint64_t *__restrict__ out_keys,
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                                                     ull *__restrict__ ctl, const uint32_t *__restrict__ defer,
-                                                    const ull *__restrict__ guard, const ull *__restrict__ d_nitems) {
+                                                    const ull *__restrict__ guard, const ull *__restrict__ d_nitems,
+                                                    bool nowrite) {
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2 + (kCapI + 16) * 2;
@@ -791,10 +795,10 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
             continue;
         }
         if (it.rem_bits <= (uint32_t)kDenseBits) {
-            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum);
+            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite);
         } else if (total <= (uint64_t)kCapI) {
             written = full_item<W, KT>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
-                                       out_counts);
+                                       out_counts, nowrite);
         } else if (threadIdx.x == 0) {
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
         }
@@ -813,31 +817,35 @@ void count_prof_read(unsigned long long *out16) {
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
-                        const unsigned long long *guard, const unsigned long long *d_nitems) {
+                        const unsigned long long *guard, const unsigned long long *d_nitems, bool nowrite) {
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
     if (wide) {  // every item through the full / dense modes
         const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems);
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
         else
             hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems);
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
         return;
     }
     const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
     const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
-        hipLaunchKernelGGL(k_count_items<true>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer, guard, d_nitems);
+        if (nowrite)
+            hipLaunchKernelGGL((k_count_items<true, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
+        else
+            hipLaunchKernelGGL((k_count_items<true, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     }
 }
 

@@ -1315,6 +1315,65 @@ static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_seg
     return OKM_OK;
 }
 
+// Weighted sorted runs at the memory limit (a context's own folded tables,
+// C3 on one GPU): the count kernels in two passes -- each item's distinct
+// keys (nothing written), an exclusive scan, then the same items counted
+// again straight into the exact-size result table at their scanned offsets.
+// Same memory as the k-way merge kernel (no instance-bound staging, no
+// compaction) at the count kernels' speed.  Releases bufs, d_items, d_segs.
+static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems,
+                                        uint64_t in_total, std::vector<void *> &bufs) {
+    unsigned long long *n_out, *dense_off, *scan_tmp;
+    uint32_t *defer;
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &n_out));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &dense_off));
+    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    OKM_TRY(pool_get(c->pool, (size_t)nitems, &defer));
+    for (void *p : {(void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer, (void *)d_items, (void *)d_segs})
+        bufs.push_back(p);
+    auto release = [&]() {
+        for (void *p : bufs) c->pool.put(p);
+        bufs.clear();
+    };
+    const double in_bytes = (8.0 * c->kw + 8.0) * (double)in_total;
+    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_count_items(c->stream, d_items, nitems, d_segs, nullptr, nullptr, n_out, c->flag, defer, true, c->wide,
+                       nullptr, nullptr, true);
+    c->timer.end(c->stream, "count_distinct", in_bytes);
+    HIP_TRY(hipGetLastError());
+    launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
+    HIP_TRY(hipGetLastError());
+    unsigned long long *hv = c->hres + kHresCount;
+    HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));
+    if (hv[1]) {
+        release();
+        return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    }
+    const uint64_t nd = hv[0];
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    launch_set_out_off(c->stream, d_items, nitems, dense_off);
+    HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
+    c->timer.begin(c->stream);
+    launch_count_items(c->stream, d_items, nitems, d_segs, c->res_keys, c->res_counts, n_out, c->flag, defer, true,
+                       c->wide);
+    c->timer.end(c->stream, "count_write", in_bytes + (8.0 * c->kw + 8.0) * (double)nd);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    OKM_TRY(sync(c));  // borrowed runs (okm_add_sorted_pairs_device) may be freed once okm_count returns
+    release();
+    if (hv[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
+    c->n_res = nd;
+    c->info.distinct = nd;
+    c->counted = true;
+    c->hprof.mark("count_two_pass");
+    return OKM_OK;
+}
+
 // All runs sorted (okm_add_sorted_pairs_device, e.g. the per-rank slices an
 // owner receives in the multi-GPU merge): every L1 part is split into
 // key-range children by binary search in each run — no key moves — and each
@@ -1448,10 +1507,19 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     // limit by design, C3 on one GPU folds up to ~2.5 G pairs at once)
     bool folded = false;
     for (auto &r : c->runs) folded |= r.folded;
-    const bool use_merge = getenv("OKM_MERGE_KERNEL") != nullptr && getenv("OKM_NO_MERGE_KERNEL") == nullptr;
+    // OKM_MERGE_KERNEL=1: the merge kernel, =2: the two-pass count (tests and
+    // A/B timing); OKM_NO_MERGE_KERNEL: the staged count path always
+    const char *mk = getenv("OKM_MERGE_KERNEL");
+    const int mkv = mk ? atoi(mk) : 0;
+    const bool staged_only = getenv("OKM_NO_MERGE_KERNEL") != nullptr;
     const double need = 2.0 * (8.0 * c->kw + 8.0) * (double)in_total;
-    const bool tight = getenv("OKM_NO_MERGE_KERNEL") == nullptr && (folded || need > 0.75 * device_room(c));
-    const bool merge = (use_merge || tight) && R <= merge_max_runs() && item_max <= merge_item_capacity();
+    const bool tight = !staged_only && (folded || need > 0.75 * device_room(c));
+    // weighted runs at the limit: the count kernels in two passes
+    // (tools/merge8_cost.py, 8 runs: see DESIGN.md §8)
+    if (!staged_only && weighted && (mkv == 2 || (tight && mkv != 1)))
+        return count_sorted_two_pass(c, d_items, d_segs, nitems, in_total, bufs);
+    const bool merge = !staged_only && (mkv == 1 || tight) && R <= merge_max_runs() &&
+                       item_max <= merge_item_capacity();
     if (merge) return merge_sorted_items(c, d_items, d_segs, nitems, in_total, weighted, bufs);
     return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
 }

@@ -143,7 +143,8 @@ uint32_t count_dense_bits();
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
-                        const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr);
+                        const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr,
+                        bool nowrite = false);  // nowrite: n_out only (weighted or wide launches)
 
 // k-way merge of sorted runs (okm_merge.hip): items as built by
 // launch_sorted_items (each segment of an item a sorted unique run of keys),

@@ -2,10 +2,12 @@
 owner's merge of per-rank slices, set unions
 (compare.rs:51-66, db_types.rs:43-53) and folded batch tables
 (count.rs:52-89).  The runs are split into key-range items by binary search
-(no key moves) and counted by the count kernel (default) or the k-way LDS
-merge kernel of okm_merge.hip (OKM_MERGE_KERNEL=1).  Exact against numpy, for
-u64 and 128-bit keys, weighted and unweighted runs, many runs, dense key
-ranges, both kernels."""
+(no key moves) and counted by the count kernel (staged slots + compaction,
+the default), the k-way LDS merge kernel of okm_merge.hip
+(OKM_MERGE_KERNEL=1), or the count kernel in two passes straight into the
+exact-size table (OKM_MERGE_KERNEL=2; weighted runs at the memory limit, the
+default for folded tables).  Exact against numpy, for u64 and 128-bit keys,
+weighted and unweighted runs, many runs, dense key ranges, all three."""
 
 import numpy as np
 import pytest
@@ -51,10 +53,10 @@ def _runs(rng, nruns, n, span, k):
     (64, 20_000, 1 << 22, True),        # the most runs one merge item tracks
     (70, 10_000, 1 << 22, True),        # more: the hashing count kernel takes over
 ])
-@pytest.mark.parametrize("merge_kernel", [False, True])
+@pytest.mark.parametrize("merge_kernel", ["", "1", "2"])
 def test_merge_runs_vs_numpy(nruns, n, span, weighted, merge_kernel, monkeypatch):
     if merge_kernel:
-        monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
+        monkeypatch.setenv("OKM_MERGE_KERNEL", merge_kernel)
     rng = np.random.default_rng(nruns * 7 + n)
     k = 31
     runs = _runs(rng, nruns, n, span, k)
@@ -78,9 +80,9 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
     rng = np.random.default_rng(5)
     runs = _runs(rng, 6, 400_000, 1 << 62, 31)
     out = []
-    for env in (None, "1"):
+    for env in (None, "1", "2"):
         if env:
-            monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
+            monkeypatch.setenv("OKM_MERGE_KERNEL", env)
         bufs = []
         with okm.KmerCounter(31) as m:
             m.set_timing(True)
@@ -90,14 +92,16 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
                 m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
             out.append(m.result(1))
             names = set(m.kernel_stats())
-        assert ("merge_write" in names) == (env is not None)
-    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+        assert ("merge_write" in names) == (env == "1")
+        assert ("count_write" in names) == (env == "2")
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
 
 
-@pytest.mark.parametrize("merge_kernel", [False, True])
+@pytest.mark.parametrize("merge_kernel", ["", "1", "2"])
 def test_merge_wide_keys(merge_kernel, monkeypatch):
     if merge_kernel:
-        monkeypatch.setenv("OKM_MERGE_KERNEL", "1")
+        monkeypatch.setenv("OKM_MERGE_KERNEL", merge_kernel)
     rng = np.random.default_rng(11)
     k = 45
     runs = []
