@@ -737,10 +737,13 @@ static okm_status fold(okm_ctx *c) {
     }
     c->hprof.mark("fold");
     if (c->hprof.on) {
-        uint64_t tb = 0;
-        for (auto &r : c->runs) tb += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
-        fprintf(stderr, "[okm fold] #%u: %zu runs holding %.1f GB; pool held %.1f GB, cached %.1f GB\n", c->folds,
-                c->runs.size(), tb / 1e9, c->pool.held / 1e9, c->pool.cached() / 1e9);
+        uint64_t tb = 0, tn = 0;
+        for (auto &r : c->runs) {
+            tb += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
+            tn += r.n;
+        }
+        fprintf(stderr, "[okm fold] #%u: %zu runs of %.3f G keys holding %.1f GB; pool held %.1f GB, cached %.1f GB\n",
+                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held / 1e9, c->pool.cached() / 1e9);
     }
     return OKM_OK;
 }
