@@ -227,6 +227,11 @@ void okm_classifier_destroy(okm_classifier *c);
 okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, const uint64_t *ref_offsets,
                                    uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
                                    uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth);
+/* Same with the database keys in DEVICE memory (d_keys[ref_offsets[0] ..
+ * ref_offsets[n_refs])); ref_offsets and the outputs stay on the host. */
+okm_status okm_classifier_probe_db_device(okm_classifier *c, const uint64_t *d_keys, const uint64_t *ref_offsets,
+                                          uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
+                                          uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU — replaces nothing in the reference (its count

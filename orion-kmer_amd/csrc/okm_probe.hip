@@ -24,8 +24,10 @@
 // needed and a device batch is consumed in place.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "okm_internal.h"
@@ -266,28 +268,38 @@ constexpr int kCPer = 8;  // reference keys per thread
 // it holds, sum of their counts} (classify.rs:228-236); tot = {|union|,
 // |input ∩ union|, sum of counts over it} (classify.rs:237, :268-272,
 // db_types.rs:50-53).
+__device__ __forceinline__ uint64_t ref_of(const ull *__restrict__ ref_off, uint64_t nrefs, uint64_t i) {
+    uint64_t lo = 0, hi = nrefs;  // last r with ref_off[r] <= i
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (ref_off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(kProbeBlock) void k_classify(const ull *__restrict__ keys, uint64_t nkeys,
                                                           const ull *__restrict__ ref_off, uint64_t nrefs,
                                                           MapTab m, SetTab u, ulonglong2 *__restrict__ per_ref,
                                                           ull *__restrict__ tot) {
-    __shared__ ull red[3];
-    if (threadIdx.x < 3) red[threadIdx.x] = 0;
+    __shared__ ull red[5];
+    if (threadIdx.x < 5) red[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = ((uint64_t)blockIdx.x * kProbeBlock + threadIdx.x) * kCPer;
-    ull un = 0, um = 0, us = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * kProbeBlock * kCPer;
+    const uint64_t base = b0 + (uint64_t)threadIdx.x * kCPer;
+    // a block's keys usually all belong to one reference (references hold
+    // millions): its per-reference sums then leave as ONE pair of atomics
+    // instead of one pair per thread on the same 32 counters
+    const uint64_t blast = min(b0 + (uint64_t)kProbeBlock * kCPer, nkeys) - 1;
+    const uint64_t rb = ref_of(ref_off, nrefs, b0);
+    const bool one_ref = ref_off[rb + 1] > blast;  // block-uniform
+    ull un = 0, um = 0, us = 0, hm = 0, hs = 0;
     if (base < nkeys) {
-        uint64_t lo = 0, hi = nrefs;  // last r with ref_off[r] <= base
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (ref_off[mid] <= base) lo = mid;
-            else hi = mid;
-        }
-        uint64_t r = lo, rend = ref_off[r + 1];
-        ull hm = 0, hs = 0;
+        uint64_t r = one_ref ? rb : ref_of(ref_off, nrefs, base), rend = ref_off[r + 1];
         for (int j = 0; j < kCPer; ++j) {
             const uint64_t i = base + j;
             if (i >= nkeys) break;
-            while (i >= rend) {  // next reference (skipping empty ones)
+            while (i >= rend) {  // next reference (skipping empty ones); never in a one-reference block
                 if (hm) {
                     atomicAdd(&per_ref[r].x, hm);
                     atomicAdd(&per_ref[r].y, hs);
@@ -310,16 +322,33 @@ __global__ __launch_bounds__(kProbeBlock) void k_classify(const ull *__restrict_
                 }
             }
         }
-        if (hm) {
+        if (hm && !one_ref) {
             atomicAdd(&per_ref[r].x, hm);
             atomicAdd(&per_ref[r].y, hs);
         }
     }
-    if (un) atomicAdd(&red[0], un);
-    if (um) atomicAdd(&red[1], um);
-    if (us) atomicAdd(&red[2], us);
+    if (!one_ref) hm = hs = 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {  // wave sums, then one LDS add per wave
+        un += __shfl_xor(un, d, 64);
+        um += __shfl_xor(um, d, 64);
+        us += __shfl_xor(us, d, 64);
+        hm += __shfl_xor(hm, d, 64);
+        hs += __shfl_xor(hs, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (un) atomicAdd(&red[0], un);
+        if (um) atomicAdd(&red[1], um);
+        if (us) atomicAdd(&red[2], us);
+        if (hm) atomicAdd(&red[3], hm);
+        if (hs) atomicAdd(&red[4], hs);
+    }
     __syncthreads();
     if (threadIdx.x < 3 && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
+    if (one_ref && threadIdx.x == 0 && red[3]) {
+        atomicAdd(&per_ref[rb].x, red[3]);
+        atomicAdd(&per_ref[rb].y, red[4]);
+    }
 }
 
 static uint32_t grid_for(uint64_t n) {
@@ -422,6 +451,8 @@ struct okm_classifier {
     uint64_t n_input = 0;
     ull *d_ctr = nullptr;
     Scratch keys, offs, uset, per_ref;
+    uint8_t *stage[2] = {nullptr, nullptr};  // pinned host staging of the database keys (okm_classifier_probe_db)
+    hipEvent_t staged[2] = {nullptr, nullptr};
 
     MapTab tab() const { return MapTab{slots, cap - 1, 64u - log2_exact(cap)}; }
 };
@@ -704,34 +735,63 @@ void okm_classifier_destroy(okm_classifier *c) {
     c->offs.release();
     c->uset.release();
     c->per_ref.release();
+    for (int i = 0; i < 2; ++i) {
+        if (c->stage[i]) (void)hipHostFree(c->stage[i]);
+        if (c->staged[i]) (void)hipEventDestroy(c->staged[i]);
+    }
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
 
-okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, const uint64_t *ref_offsets,
-                                   uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
-                                   uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth) {
-    if (!c || !db_union || !db_matched || !db_sum_depth) return fail(OKM_E_ARG, "null argument");
-    *db_union = *db_matched = *db_sum_depth = 0;
-    if (n_refs == 0) return OKM_OK;
-    if (!ref_offsets || !ref_matched || !ref_sum_depth) return fail(OKM_E_ARG, "null argument");
-    const uint64_t nkeys = ref_offsets[n_refs] - ref_offsets[0];
-    for (uint64_t r = 0; r < n_refs; ++r) {
-        if (ref_offsets[r + 1] < ref_offsets[r]) return fail(OKM_E_ARG, "ref_offsets not ascending");
-        ref_matched[r] = ref_sum_depth[r] = 0;
+}  // extern "C"
+
+namespace {
+
+constexpr size_t kStageBytes = size_t(64) << 20;  // per pinned staging buffer
+
+// Database keys (pageable host memory) to the device: 64 MiB pieces copied
+// into two pinned buffers by host threads in parallel, each piece's DMA
+// overlapping the copy of the next (a single pageable hipMemcpy moves the
+// 880 MB of 110 M keys at a few GB/s).
+okm_status stage_keys(okm_classifier *c, const uint64_t *keys, uint64_t nkeys, uint64_t *d_keys) {
+    for (int i = 0; i < 2; ++i) {
+        if (!c->stage[i]) PHIP(hipHostMalloc(reinterpret_cast<void **>(&c->stage[i]), kStageBytes, hipHostMallocDefault));
+        if (!c->staged[i]) PHIP(hipEventCreateWithFlags(&c->staged[i], hipEventDisableTiming));
     }
-    if (nkeys == 0) return OKM_OK;
-    if (!keys) return fail(OKM_E_ARG, "null keys");
-    PHIP(hipSetDevice(c->device));
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(keys);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(d_keys);
+    const size_t bytes = nkeys * sizeof(uint64_t);
+    const unsigned nthr = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (size_t off = 0, piece = 0; off < bytes; off += kStageBytes, ++piece) {
+        const int b = (int)(piece & 1);
+        const size_t len = std::min(kStageBytes, bytes - off);
+        PHIP(hipEventSynchronize(c->staged[b]));  // the DMA that last read this buffer is done
+        const size_t part = (len + nthr - 1) / nthr;
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nthr && (size_t)t * part < len; ++t) {
+            const size_t o = (size_t)t * part, l = std::min(part, len - o);
+            th.emplace_back([=] { memcpy(c->stage[b] + o, src + off + o, l); });
+        }
+        for (auto &x : th) x.join();
+        PHIP(hipMemcpyAsync(dst + off, c->stage[b], len, hipMemcpyHostToDevice, c->st));
+        PHIP(hipEventRecord(c->staged[b], c->st));
+    }
+    return OKM_OK;
+}
+
+// classify.rs:215-308 over device-resident database keys (ref_offsets and
+// the outputs on the host).
+okm_status probe_db(okm_classifier *c, const ull *d_keys, const uint64_t *ref_offsets, uint64_t n_refs,
+                    uint64_t *ref_matched, uint64_t *ref_sum_depth, uint64_t *db_union, uint64_t *db_matched,
+                    uint64_t *db_sum_depth) {
+    const uint64_t nkeys = ref_offsets[n_refs] - ref_offsets[0];
     const uint64_t ucap = pow2_at_least(2 * nkeys);
-    PTRY(c->keys.ensure(nkeys * sizeof(uint64_t)));
     PTRY(c->offs.ensure((n_refs + 1) * sizeof(uint64_t)));
     PTRY(c->uset.ensure((ucap + 1) * sizeof(ull)));
     PTRY(c->per_ref.ensure(n_refs * sizeof(ulonglong2)));
     std::vector<uint64_t> off(ref_offsets, ref_offsets + n_refs + 1);
     for (auto &v : off) v -= ref_offsets[0];
     ull *uslots = (ull *)c->uset.p;
-    PHIP(hipMemcpyAsync(c->keys.p, keys + ref_offsets[0], nkeys * sizeof(uint64_t), hipMemcpyHostToDevice, c->st));
     PHIP(hipMemcpyAsync(c->offs.p, off.data(), off.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c->st));
     PHIP(hipMemsetAsync(uslots, 0xFF, ucap * sizeof(ull), c->st));
     PHIP(hipMemsetAsync(uslots + ucap, 0, sizeof(ull), c->st));
@@ -741,7 +801,7 @@ okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, cons
     const uint64_t threads = (nkeys + kCPer - 1) / kCPer;
     const uint64_t blocks = (threads + kProbeBlock - 1) / kProbeBlock;
     if (blocks > 0x7FFFFFFFull) return fail(OKM_E_ARG, "okm_classifier_probe_db: too many keys");
-    hipLaunchKernelGGL(k_classify, dim3((uint32_t)blocks), dim3(kProbeBlock), 0, c->st, (const ull *)c->keys.p, nkeys,
+    hipLaunchKernelGGL(k_classify, dim3((uint32_t)blocks), dim3(kProbeBlock), 0, c->st, d_keys, nkeys,
                        (const ull *)c->offs.p, n_refs, c->tab(), u, (ulonglong2 *)c->per_ref.p, c->d_ctr);
     PHIP(hipGetLastError());
     std::vector<ulonglong2> pr(n_refs);
@@ -757,6 +817,53 @@ okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, cons
     *db_matched = tot[1];
     *db_sum_depth = tot[2];
     return OKM_OK;
+}
+
+// Argument checks shared by both entry points; *nkeys = the database's keys.
+okm_status probe_args(okm_classifier *c, const uint64_t *ref_offsets, uint64_t n_refs, uint64_t *ref_matched,
+                      uint64_t *ref_sum_depth, uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth,
+                      uint64_t *nkeys) {
+    *nkeys = 0;
+    if (!c || !db_union || !db_matched || !db_sum_depth) return fail(OKM_E_ARG, "null argument");
+    *db_union = *db_matched = *db_sum_depth = 0;
+    if (n_refs == 0) return OKM_OK;
+    if (!ref_offsets || !ref_matched || !ref_sum_depth) return fail(OKM_E_ARG, "null argument");
+    for (uint64_t r = 0; r < n_refs; ++r) {
+        if (ref_offsets[r + 1] < ref_offsets[r]) return fail(OKM_E_ARG, "ref_offsets not ascending");
+        ref_matched[r] = ref_sum_depth[r] = 0;
+    }
+    *nkeys = ref_offsets[n_refs] - ref_offsets[0];
+    return OKM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+okm_status okm_classifier_probe_db(okm_classifier *c, const uint64_t *keys, const uint64_t *ref_offsets,
+                                   uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
+                                   uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth) {
+    uint64_t nkeys = 0;
+    PTRY(probe_args(c, ref_offsets, n_refs, ref_matched, ref_sum_depth, db_union, db_matched, db_sum_depth, &nkeys));
+    if (nkeys == 0) return OKM_OK;
+    if (!keys) return fail(OKM_E_ARG, "null keys");
+    PHIP(hipSetDevice(c->device));
+    PTRY(c->keys.ensure(nkeys * sizeof(uint64_t)));
+    PTRY(stage_keys(c, keys + ref_offsets[0], nkeys, (uint64_t *)c->keys.p));
+    return probe_db(c, (const ull *)c->keys.p, ref_offsets, n_refs, ref_matched, ref_sum_depth, db_union, db_matched,
+                    db_sum_depth);
+}
+
+okm_status okm_classifier_probe_db_device(okm_classifier *c, const uint64_t *d_keys, const uint64_t *ref_offsets,
+                                          uint64_t n_refs, uint64_t *ref_matched, uint64_t *ref_sum_depth,
+                                          uint64_t *db_union, uint64_t *db_matched, uint64_t *db_sum_depth) {
+    uint64_t nkeys = 0;
+    PTRY(probe_args(c, ref_offsets, n_refs, ref_matched, ref_sum_depth, db_union, db_matched, db_sum_depth, &nkeys));
+    if (nkeys == 0) return OKM_OK;
+    if (!d_keys) return fail(OKM_E_ARG, "null keys");
+    PHIP(hipSetDevice(c->device));
+    return probe_db(c, (const ull *)d_keys + ref_offsets[0], ref_offsets, n_refs, ref_matched, ref_sum_depth,
+                    db_union, db_matched, db_sum_depth);
 }
 
 }  // extern "C"

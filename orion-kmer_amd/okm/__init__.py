@@ -677,18 +677,34 @@ class Classifier:
         except Exception:
             pass
 
-    def probe_db(self, refs: Sequence[np.ndarray]) -> Dict[str, object]:
+    @staticmethod
+    def pack_db(refs: Sequence[np.ndarray]):
+        """(keys, ref_offsets): the references' keys back to back, as
+        okm_classifier_probe_db[_device] take them."""
         offs = np.zeros(len(refs) + 1, dtype=np.uint64)
         if refs:
             offs[1:] = np.cumsum([len(r) for r in refs])
         keys = np.concatenate([np.asarray(r, dtype=np.uint64) for r in refs]) if refs else np.zeros(0, np.uint64)
-        keys = np.ascontiguousarray(keys)
-        rm = np.zeros(len(refs), dtype=np.uint64)
-        rs = np.zeros(len(refs), dtype=np.uint64)
+        return np.ascontiguousarray(keys), offs
+
+    def probe_db(self, refs: Sequence[np.ndarray] = None, packed=None, d_keys: int = None) -> Dict[str, object]:
+        """refs: one key array per reference; or packed = pack_db(refs) (keys
+        on the host), or d_keys = a device address holding pack_db's keys with
+        packed = (None, ref_offsets) (okm_classifier_probe_db_device)."""
+        keys, offs = packed if packed is not None else self.pack_db(refs)
+        nrefs = len(offs) - 1
+        rm = np.zeros(nrefs, dtype=np.uint64)
+        rs = np.zeros(nrefs, dtype=np.uint64)
         du, dm, ds = c_uint64(), c_uint64(), c_uint64()
-        check(lib().okm_classifier_probe_db(self.h, keys.ctypes.data, offs.ctypes.data, len(refs), rm.ctypes.data,
-                                            rs.ctypes.data, byref(du), byref(dm), byref(ds)),
-              "okm_classifier_probe_db")
+        if d_keys is not None:
+            check(lib().okm_classifier_probe_db_device(self.h, c_void_p(d_keys), offs.ctypes.data, nrefs,
+                                                       rm.ctypes.data, rs.ctypes.data, byref(du), byref(dm),
+                                                       byref(ds)),
+                  "okm_classifier_probe_db_device")
+        else:
+            check(lib().okm_classifier_probe_db(self.h, keys.ctypes.data, offs.ctypes.data, nrefs, rm.ctypes.data,
+                                                rs.ctypes.data, byref(du), byref(dm), byref(ds)),
+                  "okm_classifier_probe_db")
         return {"ref_matched": rm, "ref_sum_depth": rs, "union": du.value, "matched": dm.value,
                 "sum_depth": ds.value}
 

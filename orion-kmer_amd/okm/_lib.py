@@ -136,6 +136,8 @@ PROTOTYPES = {
     "okm_classifier_destroy": (None, [c_void_p]),
     "okm_classifier_probe_db": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, _P64, _P64,
                                         _P64]),
+    "okm_classifier_probe_db_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, _P64,
+                                               _P64, _P64]),
     "okm_synth_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                 c_double, c_void_p, c_int]),
     "okm_comm_unique_id": (c_int, [c_void_p]),

@@ -226,6 +226,14 @@ def test_classifier_vs_oracle(min_freq):
         with okm.Classifier(c, min_freq) as cl:
             assert cl.n_input == len(ik)
             got = cl.probe_db(refs)
+            keys_all, offs = okm.Classifier.pack_db(refs)
+            dk = okm.DeviceBuffer(max(8, keys_all.nbytes))
+            dk.upload(keys_all)
+            got_d = cl.probe_db(packed=(None, offs), d_keys=dk.address)  # okm_classifier_probe_db_device
+            dk.free()
+    for f in ("ref_matched", "ref_sum_depth"):
+        assert np.array_equal(got[f], got_d[f])
+    assert (got["union"], got["matched"], got["sum_depth"]) == (got_d["union"], got_d["matched"], got_d["sum_depth"])
     for r, keys in enumerate(refs):
         m = np.isin(keys, ik)
         pos = np.searchsorted(ik, keys[m])
@@ -236,6 +244,37 @@ def test_classifier_vs_oracle(min_freq):
     assert got["union"] == len(uni)
     assert got["matched"] == m.sum()
     assert got["sum_depth"] == ic[np.searchsorted(ik, uni[m])].sum()
+
+
+def test_classifier_staged_database_pieces():
+    # a database past one 64 MiB pinned staging piece (okm_probe.hip
+    # stage_keys: 2 buffers, host threads + overlapped DMA): host and device
+    # entry points agree, and the union / matches equal numpy
+    k = 31
+    rng = np.random.default_rng(3)
+    reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), size=150).tobytes() for _ in range(20_000)]
+    oc = OracleCounter(k)
+    oc.add_records(reads)
+    ik, ic = oc.result(1)
+    foreign = rng.integers(0, 1 << 62, size=21_000_000, dtype=np.uint64)  # 168 MB: three pieces
+    refs = [np.unique(np.concatenate([ik[: len(ik) // 2], foreign[:11_000_000]])),
+            np.unique(np.concatenate([ik[len(ik) // 3:], foreign[10_000_000:]]))]
+    with okm.KmerCounter(k, "count") as c:
+        c.add_records(reads)
+        with okm.Classifier(c, 1) as cl:
+            got = cl.probe_db(refs)
+            keys_all, offs = okm.Classifier.pack_db(refs)
+            dk = okm.DeviceBuffer(keys_all.nbytes)
+            dk.upload(keys_all)
+            got_d = cl.probe_db(packed=(None, offs), d_keys=dk.address)
+            dk.free()
+    uni = np.unique(keys_all)
+    m = np.isin(uni, ik)
+    for g in (got, got_d):
+        assert g["union"] == len(uni) and g["matched"] == m.sum()
+        assert g["sum_depth"] == ic[np.searchsorted(ik, uni[m])].sum()
+        for r, keys in enumerate(refs):
+            assert g["ref_matched"][r] == np.isin(keys, ik).sum()
 
 
 # ---------------------------------------------------------------------------
