@@ -157,6 +157,15 @@ struct DevPool {
             }
             if (e != hipSuccess) {
                 (void)hipGetLastError();
+                if (pool_trace()) {  // what holds the device: every block, in use or cached
+                    std::lock_guard<std::mutex> g(mu);
+                    for (auto &kv : size_) {
+                        bool cached_blk = false;
+                        for (auto &f : free_) cached_blk |= f.second == kv.first;
+                        fprintf(stderr, "[pool] block %p %.2f GB %s\n", kv.first, kv.second / 1e9,
+                                cached_blk ? "cached" : "in use");
+                    }
+                }
                 size_t fr = 0, tot = 0;
                 (void)hipMemGetInfo(&fr, &tot);
                 (void)hipGetLastError();
