@@ -1342,18 +1342,23 @@ static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_seg
 // compaction) at the count kernels' speed.  Releases bufs, d_items, d_segs.
 static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems,
                                         uint64_t in_total, std::vector<void *> &bufs) {
-    unsigned long long *n_out, *dense_off, *scan_tmp;
-    uint32_t *defer;
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &n_out));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &dense_off));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems, &defer));
-    for (void *p : {(void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer, (void *)d_items, (void *)d_segs})
-        bufs.push_back(p);
+    bufs.push_back(d_items);
+    bufs.push_back(d_segs);
     auto release = [&]() {
         for (void *p : bufs) c->pool.put(p);
         bufs.clear();
     };
+    unsigned long long *n_out = nullptr, *dense_off = nullptr, *scan_tmp = nullptr;
+    uint32_t *defer = nullptr;
+    okm_status st = pool_get(c->pool, (size_t)nitems + 1, &n_out);
+    if (st == OKM_OK) bufs.push_back(n_out), st = pool_get(c->pool, (size_t)nitems + 1, &dense_off);
+    if (st == OKM_OK) bufs.push_back(dense_off), st = pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp);
+    if (st == OKM_OK) bufs.push_back(scan_tmp), st = pool_get(c->pool, (size_t)nitems, &defer);
+    if (st != OKM_OK) {
+        release();
+        return st;
+    }
+    bufs.push_back(defer);
     const double in_bytes = (8.0 * c->kw + 8.0) * (double)in_total;
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(n_out + nitems, 0, sizeof(unsigned long long), c->stream));
@@ -1373,8 +1378,13 @@ static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_
         return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     }
     const uint64_t nd = hv[0];
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    st = pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys);
+    if (st == OKM_OK) st = pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts);
+    if (st != OKM_OK) {
+        release();
+        invalidate_result(c);
+        return st;
+    }
     launch_set_out_off(c->stream, d_items, nitems, dense_off);
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
