@@ -216,6 +216,12 @@ __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__
 
 constexpr int kSegW = 16;                       // scatter windows per thread
 constexpr int kTileW = kExtractBlock * kSegW;   // 4096 windows: 64 KiB stage
+#ifndef OKM_WIDE_SCAT_BLOCK  // single-sweep wide scatter: threads per workgroup (tile = 16 windows each)
+#define OKM_WIDE_SCAT_BLOCK 512
+#endif
+constexpr int kScatBlockW = OKM_WIDE_SCAT_BLOCK;
+constexpr int kTileW1 = kScatBlockW * kSegW;     // 256 threads: 64 KiB stage; 512: 128 KiB (one per CU)
+static_assert(kScatBlockW >= kMaxL1BinsW && (16384 % kTileW1) == 0, "wide scatter tile must divide the hist tile");
 
 // Windows [w0, w0 + SEG) with 2k-bit keys (direct extraction, okm_scan.h):
 // the forward key is the 2k code bits from base j (MSB-first) and the reverse
@@ -318,7 +324,9 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
     }
 }
 
-// Single sweep (OKM_WIDE_SWEEP1, default): the 16 keys of a thread and their
+// Single sweep (OKM_WIDE_SWEEP1, default; OKM_WIDE_SCAT_BLOCK = 512 threads, so an
+// 8192-window tile: 128 KiB of staged keys, 512-B runs per bin; 256 threads
+// measured 7.09 vs 6.29 ms at 1 Gbases, k=63): the 16 keys of a thread and their
 // within-bin ranks (returned by the histogram atomic) stay in registers, as
 // in k_extract_scatter, so each window is extracted once and the second LDS
 // atomic pass of the two-sweep kernel above is gone; the next tile's bytes
@@ -326,19 +334,19 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
 #ifndef OKM_WIDE_SWEEP1
 #define OKM_WIDE_SWEEP1 1
 #endif
-__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const uint8_t *__restrict__ seq,
+__global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uint8_t *__restrict__ seq,
                                                                          ExtractGeom g,
                                                                          const uint32_t *__restrict__ HC,
                                                                          ull *__restrict__ cursor,
                                                                          K128 *__restrict__ out,
                                                                          const ull *__restrict__ cap_end,
                                                                          ull *__restrict__ ovf) {
-    __shared__ K128 stage[kTileW + 64];  // + one dummy slot per lane for invalid windows
+    __shared__ K128 stage[kTileW1 + 64];  // + one dummy slot per lane for invalid windows
     __shared__ ull gcur[kMaxL1BinsW];
     __shared__ uint32_t hist[kMaxL1BinsW + 1];
     __shared__ uint32_t lofs[kMaxL1BinsW];
     __shared__ uint32_t lcur[kMaxL1BinsW];
-    __shared__ ull wsum[kExtractBlock / 64];
+    __shared__ ull wsum[kScatBlockW / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     if (t < nb && HC) {
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const u
     WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead
     if (beg + (uint64_t)t * kSegW < end) load_windows<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
-    for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
+    for (uint64_t t0 = beg; t0 < end; t0 += kTileW1) {
         if (t <= nb) hist[t] = 0;
         __syncthreads();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
@@ -375,9 +383,9 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const u
                     rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
                 }
             }
-            if (w0 + kTileW < end) load_windows<kSegW, 64>(seq, g.n, w0 + kTileW, ww);  // next tile, in flight
+            if (w0 + kTileW1 < end) load_windows<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);  // next tile, in flight
             __syncthreads();
-            tile_n = tile_offsets<kExtractBlock>(t, nb, hist, lofs, lcur, wsum);
+            tile_n = tile_offsets<kScatBlockW>(t, nb, hist, lofs, lcur, wsum);
             uint32_t ch = 0;
             ull cp = 0;
             if (!HC && t < nb) {
@@ -388,7 +396,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const u
 #pragma unroll
             for (int j = 0; j < kSegW; ++j) {
                 const uint32_t b = rk[j] >> 16;
-                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTileW + (t & 63u);
+                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTileW1 + (t & 63u);
                 stage[dst] = kk[j];
             }
             if (!HC && t < nb) {
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide1(const u
             }
         }
         __syncthreads();
-        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
+        for (uint32_t j = t; j < tile_n; j += kScatBlockW) {
             const K128 key = stage[j];
             const uint32_t b = bin_of_wide(key, shift);
             const ull gb = gcur[b];
@@ -446,7 +454,7 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
     hipStream_t s = (hipStream_t)stream;
     if (g.k > 32) {
         if (OKM_WIDE_SWEEP1)
-            hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC,
+            hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kScatBlockW), 0, s, seq, g, HC,
                                cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
         else
             hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC,
