@@ -14,7 +14,7 @@
 // contiguous slice per bin (claimed with one returning atomic per (block,
 // bin)), and every 16384-window tile (1024-thread workgroups, 128 KiB of staged keys; 8192
 // windows: 1.62 vs 1.48 ms on C2) is counting-sorted by bin in LDS first so
-// that each bin's keys leave the CU as one contiguous run (~512 B at 256 bins)
+// that each bin's keys leave the CU as one contiguous run (~256 B at 512 bins)
 // instead of 8-byte scattered stores (which cost 3.5x the bytes in HBM
 // writes).
 //
@@ -54,7 +54,7 @@ static_assert(kSegS % 16 == 0, "scan_windows loads whole 16-B words");
 constexpr int kSegH = 64;                      // hist: window starts per thread
 constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
 #ifndef OKM_L1_BITS  // first-level key-range bins of the k <= 32 extraction (2^bits <= kScatBlock)
-#define OKM_L1_BITS 8
+#define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
 #endif
 constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
 constexpr int kMaxL1BinsW = 256;              // k in 33..64 kernels (256-thread blocks)
