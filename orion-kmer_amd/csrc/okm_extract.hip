@@ -57,7 +57,10 @@ constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
 #define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
 #endif
 constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
-constexpr int kMaxL1BinsW = 256;              // k in 33..64 kernels (256-thread blocks)
+#ifndef OKM_L1_BITS_W  // first-level bins of the k in 33..64 extraction (2^bits <= OKM_WIDE_SCAT_BLOCK)
+#define OKM_L1_BITS_W 9  // 8: k=63 1 Gbases 39.3 vs 34.8 ms (children past one fan-out job), C4 248 vs 237 ms
+#endif
+constexpr int kMaxL1BinsW = 1 << OKM_L1_BITS_W;  // k in 33..64 kernels
 static_assert(kMaxL1Bins <= kScatBlock, "one bin per scatter thread");
 
 uint32_t extract_tile() { return (uint32_t)kHTile; }  // chunks are multiples of both tiles
@@ -454,7 +457,7 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
                             const unsigned long long *cap_end, unsigned long long *ovf) {
     hipStream_t s = (hipStream_t)stream;
     if (g.k > 32) {
-        if (OKM_WIDE_SWEEP1)
+        if (OKM_WIDE_SWEEP1 || kMaxL1BinsW > kExtractBlock)  // the two-sweep kernel holds <= 256 bins
             hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kScatBlockW), 0, s, seq, g, HC,
                                cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
         else

@@ -493,7 +493,9 @@ def test_fan_out_split(k, wide, monkeypatch):
     # instead of a host-planned second round (levels stays 1).  The weighted
     # variant: the same table re-added as (key, count) pairs.
     from oracle import OracleCounterWide
-    monkeypatch.setenv("OKM_PART_MAXB", "3")
+    # (wide: 9 L1 bits hold children of this batch below one item with 3-bit
+    # passes, so the cap is 2 bits there)
+    monkeypatch.setenv("OKM_PART_MAXB", "2" if wide else "3")
     batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=7, seed=k, sub_rate=0.01,
                             n_rate=0.001)
     gk, gc, stats, info = _count_device(batch, k, wide=wide)
@@ -537,12 +539,13 @@ def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
 
 
 @pytest.mark.parametrize("k,wide,mode,maxb", [(31, False, "A", None), (31, False, "B", None), (27, False, "A", "3"),
-                                              (63, True, "A", "3"), (45, True, "B", None)])
+                                              (63, True, "A", "2"), (45, True, "B", None)])
 def test_grouped_count(k, wide, mode, maxb, monkeypatch):
     # memory-bounded counting: the L1 parts are counted in key-range groups
     # (OKM_GROUP_KEYS forces ~1.5 M instances per group), compacted straight
     # into one instance-bound table (A) or into exact per-group tables joined
     # at the end (B); with OKM_PART_MAXB the groups also take the fan-out path
+    # (2 bits for k=63: its 9 L1 bits keep 3-bit children below one item)
     from oracle import OracleCounterWide
     monkeypatch.setenv("OKM_GROUP_KEYS", "1500000")
     monkeypatch.setenv("OKM_GROUP_MODE", mode)
