@@ -384,8 +384,8 @@ struct Run {
 using namespace okm;
 
 static const size_t kHpinBytes = size_t(4) << 20;
-static const size_t kHresWords = 4096;  // [0, 2048): L1 readback; [2048, 2064): count readback
-static const size_t kHresCount = 2048;
+static const size_t kHresWords = 8192;  // [0, 4096): L1 readback (3 nb + 2 words, nb <= 1024); [4096, 4112): count readback
+static const size_t kHresCount = 4096;
 
 struct okm_ctx {
     int device = 0;
