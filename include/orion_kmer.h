@@ -254,6 +254,15 @@ okm_status okm_comm_init_rank(okm_comm **out, int nranks, int rank, const uint8_
  * (ncclCommInitAll); out has n entries.  Each rank's calls then run on a host
  * thread of its own. */
 okm_status okm_comm_init_all(okm_comm **out, int n, const int *devices);
+/* n virtual ranks in THIS process on ONE device, without RCCL: the same owner
+ * plan, pack / widen / escape kernels, message pieces and owner merge as an
+ * RCCL communicator, with every collective done by device copies between the
+ * ranks' buffers (host threads meet at a barrier; a rank missing for
+ * OKM_LOOPBACK_TIMEOUT_S seconds, default 300, aborts it).  RCCL refuses two
+ * ranks on one GPU: this is how the P > 1 merge runs on one device (tests,
+ * rehearsals).  out has n entries; each rank's okm_merge_owned runs on a host
+ * thread of its own. */
+okm_status okm_comm_init_loopback(okm_comm **out, int n, int device);
 void okm_comm_destroy(okm_comm *comm);
 int okm_comm_rank(const okm_comm *comm);
 int okm_comm_size(const okm_comm *comm);
@@ -262,11 +271,27 @@ int okm_comm_size(const okm_comm *comm);
  * of the union of all ranks' tables, counted and sorted, and *n_owned its
  * distinct keys.  local, owner and comm share one device; k <= 32; owner may
  * be local itself (its table is only read until the exchange completes).
- * Set-mode contexts exchange keys only (build.rs / compare.rs sets). */
+ * Set-mode contexts exchange keys only (build.rs / compare.rs sets).  The
+ * owner keeps no pointer into local or the communicator afterwards: it may
+ * take more input, and local may be reset.  A rank that fails between the
+ * collectives (e.g. out of memory) reports it to its peers, so every rank
+ * returns an error; a failure inside a send/recv aborts the communicator
+ * (later calls: OKM_E_COMM). */
 okm_status okm_merge_owned(okm_ctx *local, okm_comm *comm, okm_ctx *owner, uint64_t *n_owned);
+/* okm_merge_owned for n tables under ONE owner split (balanced over the sum of
+ * their histograms), so equal keys of different tables meet on one rank: the
+ * distributed compare (compare.rs:51-66) intersects owners[0] and owners[1]
+ * per rank and sums with okm_comm_allreduce_u64.  n_owned has n entries. */
+okm_status okm_merge_owned_n(okm_ctx *const *locals, okm_comm *comm, okm_ctx *const *owners, int n,
+                             uint64_t *n_owned);
+/* Collective sum of n u64 (host memory; out may equal in). */
+okm_status okm_comm_allreduce_u64(okm_comm *comm, const uint64_t *in, uint64_t *out, uint32_t n);
 /* Host wall ms of the last okm_merge_owned: [0] plan (histogram, all-reduce,
  * sizes), [1] exchange (pack + send/recv + unpack), [2] reserved, [3] owner merge. */
 okm_status okm_comm_last_times(const okm_comm *comm, double *ms4);
+/* Bytes this rank sent to / received from OTHER ranks in the last
+ * okm_merge_owned (keys, count bytes and escapes; the self slice excluded). */
+okm_status okm_comm_last_bytes(const okm_comm *comm, uint64_t *sent, uint64_t *received);
 /* The owner split (host, no device): bounds[0] = 0 <= ... <= bounds[world] =
  * nbins, rank r owns histogram bins [bounds[r], bounds[r+1]), cut where the
  * running total first reaches r/world of the whole. */

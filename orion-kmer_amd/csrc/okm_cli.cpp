@@ -19,6 +19,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <algorithm>
 
 #include "orion_kmer.h"
 
@@ -276,8 +277,10 @@ struct AsyncGroup {
     bool joined = false;
     void start(uint8_t k, okm_mode mode) {
         th = std::thread([this, k, mode] {
-            const int one = g_device;  // --device picks the GPU of a one-GPU count
-            st = okm_group_create(&g, k, mode, g_gpus, g_gpus == 1 ? &one : nullptr, 0);
+            // --device is the first ordinal: --gpus N counts on devices D .. D+N-1
+            std::vector<int> devs;
+            for (int i = 0; i < std::max(g_gpus, 1); ++i) devs.push_back(g_device + i);
+            st = okm_group_create(&g, k, mode, g_gpus, g_gpus >= 1 ? devs.data() : nullptr, 0);
             if (st != OKM_OK) err = okm_last_error();
         });
     }
@@ -979,6 +982,8 @@ int main(int argc, char **argv) {
         uint64_t v;
         if (!parse_u64(gp, v) || v > 64) return usage_error("invalid value '" + gp + "' for '--gpus <GPUS>'");
         g_gpus = (int)v;
+        if (g_gpus == 0 && g_device != 0)
+            return usage_error("the argument '--device <DEVICE>' cannot be used with '--gpus 0' (every visible GPU)");
     }
     if (cmd == "count") return run_count(a);
     if (cmd == "build") return run_build(a);

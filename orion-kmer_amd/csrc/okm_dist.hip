@@ -8,30 +8,48 @@
 //
 //   1. 2^16-bin histogram of the top key bits of the local SORTED table: one
 //      binary search per bin start (k_bin_bounds), no pass over the keys;
-//   2. ncclAllReduce of the histogram; the host cuts it into count-balanced
+//   2. all-reduce of the histogram; the host cuts it into count-balanced
 //      contiguous key ranges, one per rank (okm_owner_bounds: value-range
 //      ownership, so the global table is the concatenation of the owners'
 //      ranges in rank order and needs no final merge; canonical k-mers are
 //      skewed ~7:5:3:1 by first base, so equal-width ranges would not balance);
 //   3. the local table splits at the range starts (binary search again) and
-//      moves with grouped ncclSend/ncclRecv: keys as u64, counts as ONE byte
-//      (k_pack_counts: the low byte; a count > 255 also travels as an escape
-//      (position, value) that overwrites the byte on arrival, k_apply_escapes):
-//      9 B per pair on a point-to-point xGMI link instead of 16;
+//      moves with grouped point-to-point sends: keys as u64, counts as ONE
+//      byte (k_pack_counts: the low byte; a count > 255 also travels as an
+//      escape (position, value) that overwrites the byte on arrival,
+//      k_apply_escapes): 9 B per pair on a point-to-point xGMI link instead of
+//      16;
 //   4. the owner adds every rank's slice — each one sorted — without copying
 //      (okm_add_sorted_pairs_device) and counts them as key-range items split
 //      out of every slice by binary search: counts add, the fetch_add of
 //      count.rs:31-34.
 //
-// RCCL is loaded at run time (dlopen), so the library still loads where no
-// RCCL is installed; only the okm_comm_* calls then fail, with OKM_E_COMM.
+// The collectives go through a Transport with two implementations that share
+// everything above (plan, pack / widen / escape kernels, piece cutting, owner
+// merge):
+//   - RcclTransport: RCCL (loaded at run time with dlopen, so the library
+//     still loads where no RCCL is installed; only the okm_comm_* calls then
+//     fail, with OKM_E_COMM), one rank per GPU;
+//   - LoopTransport: P virtual ranks in one process on one device, exchanging
+//     by device copies between the ranks' buffers (host threads meet at a
+//     barrier per collective).  RCCL refuses two ranks on one GPU, so this is
+//     how the P > 1 code paths run on a one-GPU box (tests, rehearsals).
+//
+// Failure agreement: a rank that fails between collectives (e.g. out of
+// memory while sizing its receive buffers) still takes part in the next
+// collective with a status word set, so every rank leaves okm_merge_owned
+// with an error instead of its peers blocking forever; only a failure inside
+// a grouped send/recv aborts the communicator (ncclCommAbort / the loopback
+// hub's abort), after which it is unusable.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -49,6 +67,7 @@ struct Rccl {
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
     ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
     ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -87,6 +106,7 @@ static Rccl load_rccl() {
     sym(r.CommInitRank, "ncclCommInitRank");
     sym(r.CommInitAll, "ncclCommInitAll");
     sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.CommAbort, "ncclCommAbort");
     sym(r.AllReduce, "ncclAllReduce");
     sym(r.AllGather, "ncclAllGather");
     sym(r.Send, "ncclSend");
@@ -136,9 +156,10 @@ static void owner_bounds(const uint64_t *hist, uint32_t nbins, int world, uint32
 // Kernels
 // ---------------------------------------------------------------------------
 
+// hist[b] += instances of bin b (several tables add into one histogram)
 __global__ void k_hist_from_starts(const ull *__restrict__ starts, uint32_t nb, ull *__restrict__ hist) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) hist[b] = starts[b + 1] - starts[b];
+    if (b < nb) hist[b] += starts[b + 1] - starts[b];
 }
 
 __device__ __forceinline__ uint32_t dest_of(const ull *cut, uint32_t P, uint64_t i) {
@@ -222,6 +243,215 @@ __global__ void k_apply_escapes(const uint64_t *__restrict__ esc, uint64_t nesc,
     counts[roff[s] + esc[2 * j]] = esc[2 * j + 1];
 }
 
+// dst[i] += src[i] (the loopback all-reduce)
+__global__ void k_add_u64(ull *__restrict__ dst, const ull *__restrict__ src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
+// ---------------------------------------------------------------------------
+// Transports
+// ---------------------------------------------------------------------------
+
+// One point-to-point operation of a grouped exchange (esize: 1 = u8, 8 = u64).
+struct P2POp {
+    bool send;
+    void *buf;
+    uint64_t count;
+    int esize;
+    int peer;
+};
+
+class Transport {
+  public:
+    virtual ~Transport() = default;
+    // recv[i] = sum over ranks of send[i]; send and recv are device u64 arrays
+    virtual okm_status all_reduce_sum(const ull *send, ull *recv, size_t n, hipStream_t s) = 0;
+    // recv[r * n + i] = rank r's send[i]
+    virtual okm_status all_gather(const ull *send, ull *recv, size_t n, hipStream_t s) = 0;
+    // one group of sends and receives; the i-th send from a to b matches b's
+    // i-th receive from a (both sides issue their operations in one order)
+    virtual okm_status exchange(const std::vector<P2POp> &ops, hipStream_t s) = 0;
+    // after a failure inside a collective: peers blocked in one return an error
+    virtual void abort() = 0;
+    virtual const char *name() const = 0;
+};
+
+class RcclTransport final : public Transport {
+  public:
+    explicit RcclTransport(ncclComm_t nc) : nc_(nc) {}
+    ~RcclTransport() override {
+        if (nc_) (void)rccl().CommDestroy(nc_);
+    }
+    okm_status all_reduce_sum(const ull *send, ull *recv, size_t n, hipStream_t s) override {
+        NCCL_TRY(rccl().AllReduce(send, recv, n, ncclUint64, ncclSum, nc_, s));
+        return OKM_OK;
+    }
+    okm_status all_gather(const ull *send, ull *recv, size_t n, hipStream_t s) override {
+        NCCL_TRY(rccl().AllGather(send, recv, n, ncclUint64, nc_, s));
+        return OKM_OK;
+    }
+    okm_status exchange(const std::vector<P2POp> &ops, hipStream_t s) override {
+        NCCL_TRY(rccl().GroupStart());
+        ncclResult_t bad = ncclSuccess;
+        for (const P2POp &o : ops) {
+            const ncclDataType_t t = o.esize == 1 ? ncclUint8 : ncclUint64;
+            bad = o.send ? rccl().Send(o.buf, o.count, t, o.peer, nc_, s) : rccl().Recv(o.buf, o.count, t, o.peer, nc_, s);
+            if (bad != ncclSuccess) break;
+        }
+        const ncclResult_t end = rccl().GroupEnd();  // the group is always closed
+        if (bad != ncclSuccess) return fail(OKM_E_COMM, std::string("ncclSend/ncclRecv: ") + rccl().GetErrorString(bad));
+        if (end != ncclSuccess) return fail(OKM_E_COMM, std::string("ncclGroupEnd: ") + rccl().GetErrorString(end));
+        return OKM_OK;
+    }
+    void abort() override {
+        if (nc_) (void)rccl().CommAbort(nc_);
+        nc_ = nullptr;
+    }
+    const char *name() const override { return "rccl"; }
+
+  private:
+    ncclComm_t nc_;
+};
+
+// The meeting point of a loopback communicator's P virtual ranks: a
+// generation barrier (with a timeout, so a rank that never arrives ends the
+// collective with an error instead of a hang) and the buffers each rank posts.
+struct LoopHub {
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;
+    int arrived = 0;
+    bool aborted = false;
+    std::vector<const void *> post;           // all-reduce / all-gather sources
+    std::vector<std::vector<P2POp>> sends;    // each rank's sends of the current group
+    explicit LoopHub(int n) : P(n), post(n, nullptr), sends(n) {}
+
+    static double timeout_s() {
+        const char *e = getenv("OKM_LOOPBACK_TIMEOUT_S");
+        return e && atof(e) > 0 ? atof(e) : 300.0;
+    }
+    // false: aborted (now or while waiting) or timed out (the hub is then aborted)
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return false;
+        const uint64_t g = gen;
+        if (++arrived == P) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s()),
+                                    [&] { return gen != g || aborted; });
+        if (gen != g) return true;
+        if (!ok) {  // timed out: nobody else is coming
+            aborted = true;
+            cv.notify_all();
+        }
+        return false;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+class LoopTransport final : public Transport {
+  public:
+    LoopTransport(std::shared_ptr<LoopHub> hub, int rank) : hub_(std::move(hub)), me_(rank) {}
+    okm_status all_reduce_sum(const ull *send, ull *recv, size_t n, hipStream_t s) override {
+        HIP_TRY(hipStreamSynchronize(s));
+        hub_->post[me_] = send;
+        if (!hub_->barrier()) return lost();
+        okm_status st = OKM_OK;
+        if (n) {
+            if (hipMemcpyAsync(recv, hub_->post[0], n * sizeof(ull), hipMemcpyDeviceToDevice, s) != hipSuccess)
+                st = fail(OKM_E_DEVICE, "loopback all-reduce: copy");
+            for (int r = 1; r < hub_->P && st == OKM_OK; ++r) {
+                hipLaunchKernelGGL(k_add_u64, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, recv,
+                                   static_cast<const ull *>(hub_->post[r]), (uint64_t)n);
+                if (hipGetLastError() != hipSuccess) st = fail(OKM_E_DEVICE, "loopback all-reduce: kernel");
+            }
+            if (hipStreamSynchronize(s) != hipSuccess && st == OKM_OK) st = fail(OKM_E_DEVICE, "loopback all-reduce");
+        }
+        return finish(st);  // sources stay unchanged until every rank has read them
+    }
+    okm_status all_gather(const ull *send, ull *recv, size_t n, hipStream_t s) override {
+        HIP_TRY(hipStreamSynchronize(s));
+        hub_->post[me_] = send;
+        if (!hub_->barrier()) return lost();
+        okm_status st = OKM_OK;
+        for (int r = 0; r < hub_->P && st == OKM_OK && n; ++r)
+            if (hipMemcpyAsync(recv + (size_t)r * n, hub_->post[r], n * sizeof(ull), hipMemcpyDeviceToDevice, s) !=
+                hipSuccess)
+                st = fail(OKM_E_DEVICE, "loopback all-gather: copy");
+        if (hipStreamSynchronize(s) != hipSuccess && st == OKM_OK) st = fail(OKM_E_DEVICE, "loopback all-gather");
+        return finish(st);
+    }
+    okm_status exchange(const std::vector<P2POp> &ops, hipStream_t s) override {
+        HIP_TRY(hipStreamSynchronize(s));  // the sends' bytes are ready
+        std::vector<P2POp> mine;
+        for (const P2POp &o : ops)
+            if (o.send) mine.push_back(o);
+        hub_->sends[me_] = std::move(mine);
+        if (!hub_->barrier()) return lost();
+        // receive: the j-th receive from peer p takes p's j-th send to me
+        std::vector<size_t> taken(hub_->P, 0);
+        okm_status st = OKM_OK;
+        for (const P2POp &o : ops) {
+            if (o.send) continue;
+            const std::vector<P2POp> &ps = hub_->sends[o.peer];
+            size_t j = taken[o.peer], seen = 0, at = ps.size();
+            for (size_t i = 0; i < ps.size(); ++i)
+                if (ps[i].peer == me_ && seen++ == j) {
+                    at = i;
+                    break;
+                }
+            if (at == ps.size()) {
+                st = fail(OKM_E_COMM, "loopback exchange: rank " + std::to_string(o.peer) + " posted no matching send");
+                break;
+            }
+            const P2POp &src = ps[at];
+            if (src.count != o.count || src.esize != o.esize) {
+                st = fail(OKM_E_COMM, "loopback exchange: send/receive size mismatch with rank " + std::to_string(o.peer));
+                break;
+            }
+            taken[o.peer] = j + 1;
+            if (o.count && hipMemcpyAsync(o.buf, src.buf, o.count * (uint64_t)o.esize, hipMemcpyDeviceToDevice, s) !=
+                               hipSuccess) {
+                st = fail(OKM_E_DEVICE, "loopback exchange: copy");
+                break;
+            }
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && st == OKM_OK) st = fail(OKM_E_DEVICE, "loopback exchange");
+        return finish(st);  // senders may reuse their buffers once every rank has copied
+    }
+    void abort() override { hub_->abort(); }
+    const char *name() const override { return "loopback"; }
+
+  private:
+    okm_status lost() { return fail(OKM_E_COMM, "loopback communicator aborted (a peer rank failed or timed out)"); }
+    okm_status finish(okm_status st) {
+        if (st != OKM_OK) {  // peers may wait in the closing barrier: release them
+            hub_->abort();
+            return st;
+        }
+        return hub_->barrier() ? OKM_OK : lost();
+    }
+    std::shared_ptr<LoopHub> hub_;
+    int me_;
+};
+
+// Bytes per point-to-point message piece (OKM_RCCL_PIECE; default 1 GiB).
+static uint64_t piece_bytes() {
+    const char *e = getenv("OKM_RCCL_PIECE");
+    const long long v = e ? atoll(e) : 0;
+    return v >= 8 ? (uint64_t)v & ~uint64_t(7) : (uint64_t(1) << 30);
+}
+
 }  // namespace okm
 
 using namespace okm;
@@ -254,12 +484,14 @@ struct DevBuf {
 
 struct okm_comm {
     int device = 0, rank = 0, size = 1;
-    ncclComm_t nc = nullptr;
+    std::unique_ptr<Transport> tp;
+    bool broken = false;  // aborted after a failure inside a collective
     hipStream_t stream = nullptr;
-    DevBuf starts, hist, hsum, cut, sizes, gsizes, low, esc_cnt, esc_cur, esc, rk, rlow, rc, resc, offs;
+    DevBuf starts, hist, hsum, cut, sizes, gsizes, low, esc_cnt, esc_cur, esc, rk, rlow, rc, resc, offs, flag;
     ull *hpin = nullptr;  // pinned landing area for the small readbacks
     size_t hpin_cap = 0;
     double last_ms[4] = {0, 0, 0, 0};  // plan, exchange, unpack, merge (host wall, last okm_merge_owned)
+    uint64_t last_bytes[2] = {0, 0};   // bytes sent / received by the last okm_merge_owned (excl. self)
 };
 
 namespace {
@@ -281,6 +513,303 @@ okm_status comm_finish_init(okm_comm *m) {
 
 double ms_since(const std::chrono::steady_clock::time_point &t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// A failure inside a collective leaves peers in undefined places: the
+// communicator is aborted and refuses further merges.
+okm_status broke(okm_comm *m, okm_status st) {
+    m->tp->abort();
+    m->broken = true;
+    return st;
+}
+
+// Test hook: OKM_DIST_FAIL_RANK=r makes rank r fail while sizing its receive
+// buffers (after the size exchange, before any send): every rank must return
+// an error and the communicator must stay usable.
+int debug_fail_rank() {
+    const char *e = getenv("OKM_DIST_FAIL_RANK");
+    return e ? atoi(e) : -1;
+}
+
+// One local table taking part in a merge.
+struct Table {
+    okm_ctx *local, *owner;
+    const uint64_t *dk = nullptr, *dc = nullptr;
+    uint64_t n = 0;
+    std::vector<ull> starts;  // first index of every top-bits bin (nb + 1)
+};
+
+// Steps 1-2 (see the file comment) for nt tables at once: their histograms
+// summed, then over ranks; the owner split balances the sum, so equal keys of
+// different tables meet on one rank.  Returns with every rank agreeing on
+// success: the word nb of the all-reduce carries "this rank failed".
+okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32_t shift, std::vector<uint32_t> &bounds) {
+    const uint32_t P = (uint32_t)m->size;
+    const size_t nt = tabs.size();
+    hipStream_t s = m->stream;
+    // The small buffers every collective needs: without them this rank cannot
+    // even report its failure to its peers, so the communicator is aborted.
+    {
+        okm_status a = OKM_OK;
+        for (auto [b, bytes] : {std::pair<DevBuf *, size_t>{&m->starts, nt * (nb + 1) * sizeof(ull)},
+                                {&m->hist, (nb + 1) * sizeof(ull)},
+                                {&m->hsum, (nb + 1) * sizeof(ull)},
+                                {&m->cut, (P + 1) * sizeof(ull)},
+                                {&m->sizes, (2 * P + 1) * sizeof(ull)},
+                                {&m->gsizes, (2 * (size_t)P + 1) * P * sizeof(ull)},
+                                {&m->esc_cnt, P * sizeof(ull)},
+                                {&m->esc_cur, (P + 1) * sizeof(ull)},
+                                {&m->offs, 2 * (P + 1) * sizeof(ull)},
+                                {&m->flag, 2 * sizeof(ull)}})
+            if (a == OKM_OK) a = b->ensure(bytes);
+        if (a == OKM_OK) a = ensure_hpin(m, (nt + 1) * (nb + 1) + (2 * (size_t)P + 1) * P + 64);
+        if (a != OKM_OK) return broke(m, a);
+    }
+    const ull one = 1;  // host source of an async copy: lives until the sync below
+    okm_status st = OKM_OK;
+    for (size_t i = 0; i < nt && st == OKM_OK; ++i)  // counts the local shards if needed (synchronous)
+        st = okm_result_device(tabs[i].local, &tabs[i].dk, &tabs[i].dc, &tabs[i].n);
+    HIP_TRY(hipMemsetAsync(m->hist.p, 0, (nb + 1) * sizeof(ull), s));
+    HIP_TRY(hipMemsetAsync(m->starts.p, 0, nt * (nb + 1) * sizeof(ull), s));
+    if (st == OKM_OK) {
+        for (size_t i = 0; i < nt; ++i) {
+            ull *st_i = m->starts.as<ull>() + i * (nb + 1);
+            launch_bin_bounds(s, tabs[i].dk, tabs[i].n, shift, nb, st_i, false);
+            hipLaunchKernelGGL(k_hist_from_starts, dim3((nb + 255) / 256), dim3(256), 0, s, st_i, nb,
+                               m->hist.as<ull>());
+            HIP_TRY(hipGetLastError());
+        }
+    } else {
+        HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb, &one, sizeof(ull), hipMemcpyHostToDevice, s));
+    }
+    {
+        okm_status c = m->tp->all_reduce_sum(m->hist.as<ull>(), m->hsum.as<ull>(), nb + 1, s);
+        if (c != OKM_OK) return broke(m, c);
+    }
+    ull *h_sum = m->hpin, *h_starts = m->hpin + nb + 1;
+    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_starts, m->starts.p, nt * (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (st != OKM_OK) return st;
+    if (h_sum[nb]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed before the exchange");
+    for (size_t i = 0; i < nt; ++i) tabs[i].starts.assign(h_starts + i * (nb + 1), h_starts + (i + 1) * (nb + 1));
+    bounds.assign(P + 1, 0);
+    owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());
+    return OKM_OK;
+}
+
+// Steps 3-4 for one table under agreed bounds: sizes, escapes, the grouped
+// exchange, then the owner's count of the received slices.
+okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bounds, uint32_t nb,
+                          uint64_t *n_owned, double *ms3, uint64_t *bytes2) {
+    const auto t0 = std::chrono::steady_clock::now();
+    okm_ctx *local = t.local, *owner = t.owner;
+    const bool set = ctx_is_set(local) || ctx_is_set(owner);
+    const uint32_t P = (uint32_t)m->size, me = (uint32_t)m->rank;
+    hipStream_t s = m->stream;
+    Transport &tp = *m->tp;
+    const uint64_t *dk = t.dk, *dc = t.dc;
+    const uint64_t n = t.n;
+    // host sources of async copies live until the stream is synchronised
+    ull bad = 0;
+    std::vector<ull> esc_offs(2 * (P + 1));
+    std::vector<ull> cut(P + 1);
+    for (uint32_t r = 0; r <= P; ++r) cut[r] = bounds[r] >= nb ? n : t.starts[bounds[r]];
+    cut[0] = 0;
+    cut[P] = n;
+
+    // 3. sizes (and escape counts) of every pair of ranks; word 2P = status
+    HIP_TRY(hipMemcpyAsync(m->cut.p, cut.data(), (P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
+    std::vector<ull> hs(2 * P + 1, 0);
+    for (uint32_t r = 0; r < P; ++r) hs[r] = cut[r + 1] - cut[r];
+    // This rank's own slice never crosses the transport when the owner is
+    // another context: the owner borrows it straight from the local table (it
+    // stays unchanged until okm_count(owner) returns below).  owner == local
+    // receives it through a self send/recv, since okm_reset(owner) releases it.
+    const bool self_borrow = owner != local;
+    const uint64_t skip0 = self_borrow ? cut[me] : 0, skip1 = self_borrow ? cut[me + 1] : 0;
+    const uint64_t pblocks = (n + kPackBlock - 1) / kPackBlock;
+    okm_status st = OKM_OK;
+    if (!set) st = m->low.ensure(std::max<uint64_t>(n, 16));
+    hs[2 * P] = st != OKM_OK;
+    HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), (2 * P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, P * sizeof(ull), s));
+    if (!set && st == OKM_OK && pblocks) {
+        hipLaunchKernelGGL(k_pack_counts<false>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
+                           m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr, skip0, skip1);
+        HIP_TRY(hipGetLastError());
+    }
+    {
+        okm_status c = tp.all_gather(m->sizes.as<ull>(), m->gsizes.as<ull>(), 2 * P + 1, s);
+        if (c != OKM_OK) return broke(m, c);
+    }
+    const size_t row = 2 * (size_t)P + 1;
+    std::vector<ull> h_g(row * P);
+    HIP_TRY(hipMemcpyAsync(m->hpin, m->gsizes.p, row * P * sizeof(ull), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::copy(m->hpin, m->hpin + row * P, h_g.begin());
+    if (st != OKM_OK) return st;
+    for (uint32_t r = 0; r < P; ++r)
+        if (h_g[(size_t)r * row + 2 * P]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed while sizing");
+    std::vector<ull> ss(P), rs(P), es(P), er(P), roff(P + 1, 0), reoff(P + 1, 0), eoff(P + 1, 0);
+    for (uint32_t r = 0; r < P; ++r) {
+        ss[r] = h_g[(size_t)me * row + r];
+        es[r] = h_g[(size_t)me * row + P + r];
+        rs[r] = h_g[(size_t)r * row + me];
+        er[r] = h_g[(size_t)r * row + P + me];
+        roff[r + 1] = roff[r] + rs[r];
+        reoff[r + 1] = reoff[r] + er[r];
+        eoff[r + 1] = eoff[r] + es[r];
+    }
+    const uint64_t self_n = ss[me];
+    if (self_borrow) {
+        for (uint32_t r = me + 1; r <= P; ++r) roff[r] -= rs[me], reoff[r] -= er[me];
+        rs[me] = er[me] = 0;
+        ss[me] = es[me] = 0;
+    }
+    const uint64_t nrecv = roff[P], nresc = reoff[P], nesc = eoff[P];
+
+    // receive buffers and the escapes, then one more status word: a rank that
+    // cannot allocate them tells its peers before any send is posted
+    st = m->rk.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
+    if (!set) {
+        if (st == OKM_OK) st = m->rlow.ensure(std::max<uint64_t>(nrecv, 16));
+        if (st == OKM_OK) st = m->rc.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
+        if (st == OKM_OK) st = m->resc.ensure(std::max<uint64_t>(2 * nresc, 2) * sizeof(uint64_t));
+        if (st == OKM_OK && nesc) st = m->esc.ensure(2 * nesc * sizeof(uint64_t));
+    }
+    if (st == OKM_OK && debug_fail_rank() == (int)me) st = fail(OKM_E_NOMEM, "okm_merge_owned: OKM_DIST_FAIL_RANK test hook");
+    if (st == OKM_OK && !set && nesc) {  // escapes grouped by destination
+        HIP_TRY(hipMemcpyAsync(m->esc_cur.p, eoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_pack_counts<true>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
+                           m->low.as<uint8_t>(), nullptr, m->esc_cur.as<ull>(), m->esc.as<uint64_t>(), skip0, skip1);
+        HIP_TRY(hipGetLastError());
+    }
+    if (P > 1) {
+        bad = st != OKM_OK;
+        HIP_TRY(hipMemcpyAsync(m->flag.p, &bad, sizeof(ull), hipMemcpyHostToDevice, s));
+        okm_status c = tp.all_reduce_sum(m->flag.as<ull>(), m->flag.as<ull>() + 1, 1, s);
+        if (c != OKM_OK) return broke(m, c);
+        HIP_TRY(hipMemcpyAsync(m->hpin, m->flag.as<ull>() + 1, sizeof(ull), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (st != OKM_OK) return st;
+        if (m->hpin[0]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed to allocate its receive buffers");
+    } else if (st != OKM_OK) {
+        return st;
+    }
+    const double t_plan = ms_since(t0);
+
+    // 4. move the slices: keys as u64, counts as bytes (+ escapes), in pieces
+    // of at most piece_bytes().  Group j holds piece j of every message, so a
+    // group's sends and receives always match their peers' group j (a group
+    // cut by operation count could pair a send of one group with a receive of
+    // a later one on the peer and deadlock).
+    struct Msg {
+        bool send;
+        uint8_t *buf;
+        uint64_t count;
+        int esize;
+        int peer;
+    };
+    std::vector<Msg> msgs;
+    auto add = [&](bool send, const void *buf, uint64_t count, int esize, uint32_t peer) {
+        if (count) msgs.push_back(Msg{send, (uint8_t *)const_cast<void *>(buf), count, esize, (int)peer});
+    };
+    uint64_t bytes_out = 0, bytes_in = 0;
+    for (uint32_t r = 0; r < P; ++r) {
+        add(true, dk + cut[r], ss[r], 8, r);
+        add(false, m->rk.as<uint64_t>() + roff[r], rs[r], 8, r);
+        if (!set) {
+            add(true, m->low.as<uint8_t>() + cut[r], ss[r], 1, r);
+            add(false, m->rlow.as<uint8_t>() + roff[r], rs[r], 1, r);
+            add(true, m->esc.as<uint64_t>() + 2 * eoff[r], 2 * es[r], 8, r);
+            add(false, m->resc.as<uint64_t>() + 2 * reoff[r], 2 * er[r], 8, r);
+        }
+        if (r != me) {
+            bytes_out += ss[r] * (set ? 8 : 9) + (set ? 0 : 16 * es[r]);
+            bytes_in += rs[r] * (set ? 8 : 9) + (set ? 0 : 16 * er[r]);
+        }
+    }
+    const uint64_t piece = piece_bytes();
+    uint64_t npieces = 0;
+    for (const Msg &g : msgs) npieces = std::max<uint64_t>(npieces, (g.count * g.esize + piece - 1) / piece);
+    std::vector<P2POp> ops;
+    for (uint64_t j = 0; j < npieces; ++j) {
+        ops.clear();
+        for (const Msg &g : msgs) {
+            const uint64_t per = piece / (uint64_t)g.esize, o = j * per;
+            if (o < g.count) ops.push_back(P2POp{g.send, g.buf + o * g.esize, std::min(per, g.count - o), g.esize, g.peer});
+        }
+        okm_status c = tp.exchange(ops, s);
+        if (c != OKM_OK) return broke(m, c);
+    }
+    if (!set && nrecv) {
+        const uint64_t wb = (nrecv + kPackBlock - 1) / kPackBlock;
+        hipLaunchKernelGGL(k_widen_counts, dim3((uint32_t)wb), dim3(256), 0, s, m->rlow.as<uint8_t>(), nrecv,
+                           m->rc.as<uint64_t>());
+        if (nresc) {
+            std::copy(reoff.begin(), reoff.end(), esc_offs.begin());
+            std::copy(roff.begin(), roff.end(), esc_offs.begin() + P + 1);
+            HIP_TRY(hipMemcpyAsync(m->offs.p, esc_offs.data(), esc_offs.size() * sizeof(ull), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_apply_escapes, dim3((uint32_t)((nresc + 255) / 256)), dim3(256), 0, s,
+                               m->resc.as<uint64_t>(), nresc, m->offs.as<ull>(), m->offs.as<ull>() + P + 1, P,
+                               m->rc.as<uint64_t>());
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(s));  // received: the owner's stream may read the slices
+    const double t_x = ms_since(t0);
+
+    // 5. the owner counts the P sorted slices in place (key-range items); no
+    // collective from here on
+    OKM_TRY(okm_reset(owner));
+    for (uint32_t r = 0; r < P; ++r) {
+        if (r == me && self_borrow && self_n) {
+            OKM_TRY(okm_add_sorted_pairs_device(owner, dk + cut[me], set ? nullptr : dc + cut[me], self_n));
+            continue;
+        }
+        if (!rs[r]) continue;
+        OKM_TRY(okm_add_sorted_pairs_device(owner, m->rk.as<uint64_t>() + roff[r],
+                                            set ? nullptr : m->rc.as<uint64_t>() + roff[r], rs[r]));
+    }
+    uint64_t nd = 0;
+    // synchronous; the owner releases the borrowed slices once counted, so the
+    // next add / merge may overwrite them (okm_engine.hip do_count)
+    OKM_TRY(okm_count(owner, &nd));
+    if (n_owned) *n_owned = nd;
+    ms3[0] += t_plan;
+    ms3[1] += t_x - t_plan;
+    ms3[2] += ms_since(t0) - t_x;
+    bytes2[0] += bytes_out;
+    bytes2[1] += bytes_in;
+    return OKM_OK;
+}
+
+// The collective body of okm_merge_owned / okm_merge_owned_n.
+okm_status merge_owned_n(okm_ctx *const *locals, okm_comm *m, okm_ctx *const *owners, int nt, uint64_t *n_owned) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(m->device));
+    const uint32_t k = ctx_k(locals[0]);
+    const uint32_t bits = std::min<uint32_t>(16, 2 * k);
+    const uint32_t nb = 1u << bits, shift = 2 * k - bits;
+    std::vector<Table> tabs(nt);
+    for (int i = 0; i < nt; ++i) {
+        tabs[i].local = locals[i];
+        tabs[i].owner = owners[i];
+    }
+    std::vector<uint32_t> bounds;
+    OKM_TRY(plan_split(m, tabs, nb, shift, bounds));
+    double ms3[3] = {ms_since(t0), 0, 0};
+    uint64_t bytes2[2] = {0, 0};
+    for (int i = 0; i < nt; ++i)
+        OKM_TRY(move_and_merge(m, tabs[i], bounds, nb, n_owned ? n_owned + i : nullptr, ms3, bytes2));
+    m->last_ms[0] = ms3[0];
+    m->last_ms[1] = ms3[1];
+    m->last_ms[2] = 0;
+    m->last_ms[3] = ms3[2];
+    m->last_bytes[0] = bytes2[0];
+    m->last_bytes[1] = bytes2[1];
+    return OKM_OK;
 }
 }  // namespace
 
@@ -309,15 +838,13 @@ okm_status okm_comm_init_rank(okm_comm **out, int nranks, int rank, const uint8_
     HIP_TRY(hipSetDevice(device));
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
+    ncclComm_t nc = nullptr;
+    NCCL_TRY(rccl().CommInitRank(&nc, nranks, u, rank));
     okm_comm *m = new okm_comm();
     m->device = device;
     m->rank = rank;
     m->size = nranks;
-    ncclResult_t r = rccl().CommInitRank(&m->nc, nranks, u, rank);
-    if (r != ncclSuccess) {
-        delete m;
-        return fail(OKM_E_COMM, std::string("ncclCommInitRank: ") + rccl().GetErrorString(r));
-    }
+    m->tp.reset(new RcclTransport(nc));
     okm_status st = comm_finish_init(m);
     if (st != OKM_OK) {
         okm_comm_destroy(m);
@@ -339,7 +866,7 @@ okm_status okm_comm_init_all(okm_comm **out, int n, const int *devices) {
         m->device = devs[i];
         m->rank = i;
         m->size = n;
-        m->nc = ncs[i];
+        m->tp.reset(new RcclTransport(ncs[i]));
         out[i] = m;
         okm_status st = comm_finish_init(m);
         if (st != OKM_OK) {
@@ -351,13 +878,34 @@ okm_status okm_comm_init_all(okm_comm **out, int n, const int *devices) {
     return OKM_OK;
 }
 
+okm_status okm_comm_init_loopback(okm_comm **out, int n, int device) {
+    if (!out || n < 1) return fail(OKM_E_ARG, "okm_comm_init_loopback: bad arguments");
+    auto hub = std::make_shared<LoopHub>(n);
+    for (int i = 0; i < n; ++i) out[i] = nullptr;
+    for (int i = 0; i < n; ++i) {
+        okm_comm *m = new okm_comm();
+        m->device = device;
+        m->rank = i;
+        m->size = n;
+        m->tp.reset(new LoopTransport(hub, i));
+        out[i] = m;
+        okm_status st = comm_finish_init(m);
+        if (st != OKM_OK) {
+            for (int j = 0; j <= i; ++j) okm_comm_destroy(out[j]);
+            for (int j = 0; j < n; ++j) out[j] = nullptr;
+            return st;
+        }
+    }
+    return OKM_OK;
+}
+
 void okm_comm_destroy(okm_comm *m) {
     if (!m) return;
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
-    if (m->nc) (void)rccl().CommDestroy(m->nc);
+    m->tp.reset();
     for (DevBuf *b : {&m->starts, &m->hist, &m->hsum, &m->cut, &m->sizes, &m->gsizes, &m->low, &m->esc_cnt,
-                      &m->esc_cur, &m->esc, &m->rk, &m->rlow, &m->rc, &m->resc, &m->offs})
+                      &m->esc_cur, &m->esc, &m->rk, &m->rlow, &m->rc, &m->resc, &m->offs, &m->flag})
         b->release();
     if (m->hpin) (void)hipHostFree(m->hpin);
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -373,187 +921,55 @@ okm_status okm_comm_last_times(const okm_comm *m, double *ms4) {
     return OKM_OK;
 }
 
+okm_status okm_comm_last_bytes(const okm_comm *m, uint64_t *sent, uint64_t *received) {
+    if (!m) return fail(OKM_E_ARG, "null argument");
+    if (sent) *sent = m->last_bytes[0];
+    if (received) *received = m->last_bytes[1];
+    return OKM_OK;
+}
+
+okm_status okm_merge_owned_n(okm_ctx *const *locals, okm_comm *m, okm_ctx *const *owners, int n,
+                             uint64_t *n_owned) {
+    // argument errors are the caller's and symmetric (every rank passes the
+    // same kind of contexts): they return before any collective
+    if (!locals || !m || !owners || n < 1) return fail(OKM_E_ARG, "okm_merge_owned: null argument");
+    if (m->broken) return fail(OKM_E_COMM, "okm_merge_owned: communicator aborted by an earlier failure");
+    for (int i = 0; i < n; ++i) {
+        okm_ctx *local = locals[i], *owner = owners[i];
+        if (!local || !owner) return fail(OKM_E_ARG, "okm_merge_owned: null context");
+        if (ctx_device(local) != m->device || ctx_device(owner) != m->device)
+            return fail(OKM_E_ARG, "okm_merge_owned: local, owner and communicator must share one device");
+        // owner == local is allowed (and cheapest: one context, one device
+        // pool): the local table is only read until the exchange has completed
+        if (ctx_is_wide(local) || ctx_is_wide(owner) || ctx_k(local) != ctx_k(owner) || ctx_k(local) != ctx_k(locals[0]))
+            return fail(OKM_E_ARG, "okm_merge_owned: k must match and be <= 32");
+        for (int j = 0; j < i; ++j)
+            if (owners[j] == owner || owners[j] == local || locals[j] == owner)
+                return fail(OKM_E_ARG, "okm_merge_owned_n: every table needs its own contexts");
+    }
+    return merge_owned_n(locals, m, owners, n, n_owned);
+}
+
 okm_status okm_merge_owned(okm_ctx *local, okm_comm *m, okm_ctx *owner, uint64_t *n_owned) {
-    if (!local || !m || !owner) return fail(OKM_E_ARG, "okm_merge_owned: null argument");
-    if (ctx_device(local) != m->device || ctx_device(owner) != m->device)
-        return fail(OKM_E_ARG, "okm_merge_owned: local, owner and communicator must share one device");
-    // owner == local is allowed (and cheapest: one context, one device pool):
-    // the local table is only read until the exchange has completed
-    if (ctx_is_wide(local) || ctx_is_wide(owner) || ctx_k(local) != ctx_k(owner))
-        return fail(OKM_E_ARG, "okm_merge_owned: k must match and be <= 32");
-    const auto t0 = std::chrono::steady_clock::now();
+    return okm_merge_owned_n(&local, m, &owner, 1, n_owned);
+}
+
+okm_status okm_comm_allreduce_u64(okm_comm *m, const uint64_t *in, uint64_t *out, uint32_t n) {
+    if (!m || (n && (!in || !out))) return fail(OKM_E_ARG, "okm_comm_allreduce_u64: null argument");
+    if (m->broken) return fail(OKM_E_COMM, "okm_comm_allreduce_u64: communicator aborted by an earlier failure");
+    if (!n) return OKM_OK;
     HIP_TRY(hipSetDevice(m->device));
-    const uint64_t *dk = nullptr, *dc = nullptr;
-    uint64_t n = 0;
-    OKM_TRY(okm_result_device(local, &dk, &dc, &n));  // counts the local shard if needed (synchronous)
-    const bool set = ctx_is_set(local) || ctx_is_set(owner);
-    const uint32_t P = (uint32_t)m->size, me = (uint32_t)m->rank;
-    const uint32_t k = ctx_k(local);
-    const uint32_t bits = std::min<uint32_t>(16, 2 * k);
-    const uint32_t nb = 1u << bits, shift = 2 * k - bits;
+    okm_status st = m->flag.ensure(2 * (size_t)n * sizeof(ull));
+    if (st == OKM_OK) st = ensure_hpin(m, 2 * (size_t)n);
+    if (st != OKM_OK) return broke(m, st);
     hipStream_t s = m->stream;
-
-    // 1-2. histogram of the sorted table's top bits, summed over ranks
-    OKM_TRY(m->starts.ensure((nb + 1) * sizeof(ull)));
-    OKM_TRY(m->hist.ensure(nb * sizeof(ull)));
-    OKM_TRY(m->hsum.ensure(nb * sizeof(ull)));
-    launch_bin_bounds(s, dk, n, shift, nb, m->starts.as<ull>(), false);
-    hipLaunchKernelGGL(k_hist_from_starts, dim3((nb + 255) / 256), dim3(256), 0, s, m->starts.as<ull>(), nb,
-                       m->hist.as<ull>());
-    HIP_TRY(hipGetLastError());
-    NCCL_TRY(rccl().AllReduce(m->hist.p, m->hsum.p, nb, ncclUint64, ncclSum, m->nc, s));
-    OKM_TRY(ensure_hpin(m, 2 * (size_t)nb + 1 + 8 * (size_t)P * P + 64));
-    ull *h_sum = m->hpin, *h_starts = m->hpin + nb;
-    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, nb * sizeof(ull), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h_starts, m->starts.p, (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
+    memcpy(m->hpin, in, n * sizeof(ull));
+    HIP_TRY(hipMemcpyAsync(m->flag.p, m->hpin, n * sizeof(ull), hipMemcpyHostToDevice, s));
+    st = m->tp->all_reduce_sum(m->flag.as<ull>(), m->flag.as<ull>() + n, n, s);
+    if (st != OKM_OK) return broke(m, st);
+    HIP_TRY(hipMemcpyAsync(m->hpin + n, m->flag.as<ull>() + n, n * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    std::vector<uint32_t> bounds(P + 1);
-    owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());
-    std::vector<ull> cut(P + 1);
-    for (uint32_t r = 0; r <= P; ++r) cut[r] = bounds[r] >= nb ? n : h_starts[bounds[r]];
-    cut[0] = 0;
-    cut[P] = n;
-
-    // 3. sizes (and escape counts) of every pair of ranks
-    OKM_TRY(m->cut.ensure((P + 1) * sizeof(ull)));
-    OKM_TRY(m->sizes.ensure(2 * P * sizeof(ull)));
-    OKM_TRY(m->gsizes.ensure(2 * (size_t)P * P * sizeof(ull)));
-    OKM_TRY(m->esc_cnt.ensure(P * sizeof(ull)));
-    OKM_TRY(m->esc_cur.ensure((P + 1) * sizeof(ull)));
-    HIP_TRY(hipMemcpyAsync(m->cut.p, cut.data(), (P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
-    std::vector<ull> hs(2 * P, 0);
-    for (uint32_t r = 0; r < P; ++r) hs[r] = cut[r + 1] - cut[r];
-    HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, P * sizeof(ull), s));
-    const uint64_t pblocks = (n + kPackBlock - 1) / kPackBlock;
-    // This rank's own slice never crosses RCCL when the owner is another
-    // context: the owner borrows it straight from the local table (it stays
-    // unchanged until okm_count(owner) returns below).  owner == local
-    // receives it through a self send/recv, since okm_reset(owner) releases it.
-    const bool self_borrow = owner != local;
-    const uint64_t skip0 = self_borrow ? cut[me] : 0, skip1 = self_borrow ? cut[me + 1] : 0;
-    if (!set) {
-        OKM_TRY(m->low.ensure(std::max<uint64_t>(n, 16)));
-        if (pblocks)
-            hipLaunchKernelGGL(k_pack_counts<false>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(),
-                               P, m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr, skip0, skip1);
-        HIP_TRY(hipGetLastError());
-    }
-    NCCL_TRY(rccl().AllGather(m->sizes.p, m->gsizes.p, 2 * P, ncclUint64, m->nc, s));
-    ull *h_g = m->hpin + 2 * (size_t)nb + 1;
-    HIP_TRY(hipMemcpyAsync(h_g, m->gsizes.p, 2 * (size_t)P * P * sizeof(ull), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    std::vector<ull> ss(P), rs(P), es(P), er(P), roff(P + 1, 0), reoff(P + 1, 0), eoff(P + 1, 0);
-    for (uint32_t r = 0; r < P; ++r) {
-        ss[r] = h_g[(size_t)me * 2 * P + r];
-        es[r] = h_g[(size_t)me * 2 * P + P + r];
-        rs[r] = h_g[(size_t)r * 2 * P + me];
-        er[r] = h_g[(size_t)r * 2 * P + P + me];
-        roff[r + 1] = roff[r] + rs[r];
-        reoff[r + 1] = reoff[r] + er[r];
-        eoff[r + 1] = eoff[r] + es[r];
-    }
-    const uint64_t self_n = ss[me];
-    if (self_borrow) {
-        for (uint32_t r = me + 1; r <= P; ++r) roff[r] -= rs[me], reoff[r] -= er[me];
-        rs[me] = er[me] = 0;
-        ss[me] = es[me] = 0;
-    }
-    const uint64_t nrecv = roff[P], nresc = reoff[P], nesc = eoff[P];
-    if (!set && nesc) {  // escapes grouped by destination
-        OKM_TRY(m->esc.ensure(2 * nesc * sizeof(uint64_t)));
-        HIP_TRY(hipMemcpyAsync(m->esc_cur.p, eoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_pack_counts<true>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
-                           m->low.as<uint8_t>(), nullptr, m->esc_cur.as<ull>(), m->esc.as<uint64_t>(), skip0, skip1);
-        HIP_TRY(hipGetLastError());
-    }
-    const double t_plan = ms_since(t0);
-
-    // 4. move the slices: keys as u64, counts as bytes (+ escapes)
-    OKM_TRY(m->rk.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t)));
-    if (!set) {
-        OKM_TRY(m->rlow.ensure(std::max<uint64_t>(nrecv, 16)));
-        OKM_TRY(m->rc.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t)));
-        OKM_TRY(m->resc.ensure(std::max<uint64_t>(2 * nresc, 2) * sizeof(uint64_t)));
-    }
-    // Messages go in pieces of at most kPiece bytes: a single 7.9 GB self
-    // send/recv (a C3 shard's table at one rank) arrived corrupted; both sides
-    // cut a slice the same way, and a group holds at most kGroupOps operations.
-    constexpr uint64_t kPiece = uint64_t(1) << 30;
-    struct Op {
-        bool send;
-        void *buf;
-        uint64_t count;
-        ncclDataType_t type;
-        int peer;
-    };
-    std::vector<Op> ops;
-    auto add = [&](bool send, const void *buf, uint64_t count, ncclDataType_t type, size_t esize, int peer) {
-        const uint64_t per = kPiece / esize;
-        for (uint64_t o = 0; o < count; o += per)
-            ops.push_back(Op{send, (uint8_t *)const_cast<void *>(buf) + o * esize, std::min(per, count - o), type, peer});
-    };
-    for (uint32_t r = 0; r < P; ++r) {
-        if (ss[r]) add(true, dk + cut[r], ss[r], ncclUint64, 8, (int)r);
-        if (rs[r]) add(false, m->rk.as<uint64_t>() + roff[r], rs[r], ncclUint64, 8, (int)r);
-        if (set) continue;
-        if (ss[r]) add(true, m->low.as<uint8_t>() + cut[r], ss[r], ncclUint8, 1, (int)r);
-        if (rs[r]) add(false, m->rlow.as<uint8_t>() + roff[r], rs[r], ncclUint8, 1, (int)r);
-        if (es[r]) add(true, m->esc.as<uint64_t>() + 2 * eoff[r], 2 * es[r], ncclUint64, 8, (int)r);
-        if (er[r]) add(false, m->resc.as<uint64_t>() + 2 * reoff[r], 2 * er[r], ncclUint64, 8, (int)r);
-    }
-    // every peer issues its pieces in the same order, so the i-th send to a
-    // peer matches that peer's i-th receive from us
-    constexpr size_t kGroupOps = 4096;  // one group in practice (P <= 64 peers x a few pieces)
-    for (size_t g0 = 0; g0 < ops.size(); g0 += kGroupOps) {
-        NCCL_TRY(rccl().GroupStart());
-        for (size_t i = g0; i < std::min(ops.size(), g0 + kGroupOps); ++i) {
-            const Op &o = ops[i];
-            if (o.send)
-                NCCL_TRY(rccl().Send(o.buf, o.count, o.type, o.peer, m->nc, s));
-            else
-                NCCL_TRY(rccl().Recv(o.buf, o.count, o.type, o.peer, m->nc, s));
-        }
-        NCCL_TRY(rccl().GroupEnd());
-    }
-    if (!set && nrecv) {
-        const uint64_t wb = (nrecv + kPackBlock - 1) / kPackBlock;
-        hipLaunchKernelGGL(k_widen_counts, dim3((uint32_t)wb), dim3(256), 0, s, m->rlow.as<uint8_t>(), nrecv,
-                           m->rc.as<uint64_t>());
-        if (nresc) {
-            OKM_TRY(m->offs.ensure(2 * (P + 1) * sizeof(ull)));
-            std::vector<ull> o(2 * (P + 1));
-            std::copy(reoff.begin(), reoff.end(), o.begin());
-            std::copy(roff.begin(), roff.end(), o.begin() + P + 1);
-            HIP_TRY(hipMemcpyAsync(m->offs.p, o.data(), o.size() * sizeof(ull), hipMemcpyHostToDevice, s));
-            hipLaunchKernelGGL(k_apply_escapes, dim3((uint32_t)((nresc + 255) / 256)), dim3(256), 0, s,
-                               m->resc.as<uint64_t>(), nresc, m->offs.as<ull>(), m->offs.as<ull>() + P + 1, P,
-                               m->rc.as<uint64_t>());
-        }
-        HIP_TRY(hipGetLastError());
-    }
-    HIP_TRY(hipStreamSynchronize(s));  // received: the owner's stream may read the slices
-    const double t_x = ms_since(t0);
-
-    // 5. the owner counts the P sorted slices in place (key-range items)
-    OKM_TRY(okm_reset(owner));
-    for (uint32_t r = 0; r < P; ++r) {
-        if (r == me && self_borrow && self_n) {
-            OKM_TRY(okm_add_sorted_pairs_device(owner, dk + cut[me], set ? nullptr : dc + cut[me], self_n));
-            continue;
-        }
-        if (!rs[r]) continue;
-        OKM_TRY(okm_add_sorted_pairs_device(owner, m->rk.as<uint64_t>() + roff[r],
-                                            set ? nullptr : m->rc.as<uint64_t>() + roff[r], rs[r]));
-    }
-    uint64_t nd = 0;
-    OKM_TRY(okm_count(owner, &nd));  // synchronous: the slices may be overwritten by the next call
-    if (n_owned) *n_owned = nd;
-    const double t_all = ms_since(t0);
-    m->last_ms[0] = t_plan;
-    m->last_ms[1] = t_x - t_plan;
-    m->last_ms[2] = 0;
-    m->last_ms[3] = t_all - t_x;
+    memcpy(out, m->hpin + n, n * sizeof(ull));
     return OKM_OK;
 }
 

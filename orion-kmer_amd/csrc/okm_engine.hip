@@ -425,6 +425,10 @@ struct okm_ctx {
 
     // result
     bool counted = false;
+    // the result stands for every input added so far: the runs it was
+    // counted from are gone (borrowed runs are dropped once counted, since
+    // their memory belongs to the caller); the next add keeps it as a table
+    bool res_is_input = false;
     uint64_t *res_keys = nullptr, *res_counts = nullptr;
     uint64_t n_res = 0;
     okm_engine_info info{};
@@ -448,6 +452,12 @@ void *host_pinned_alloc(size_t bytes) {
 
 void host_pinned_free(void *p) {
     if (p) (void)hipHostFree(p);
+}
+
+okm_status memcpy_d2h_on(int device, void *dst, const void *src, size_t bytes) {
+    HIP_TRY(hipSetDevice(device));
+    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return OKM_OK;
 }
 
 static okm_status ensure_hc(okm_ctx *c, size_t n_u32) {
@@ -498,6 +508,7 @@ static void invalidate_result(okm_ctx *c) {
     c->res_keys = c->res_counts = nullptr;
     c->n_res = 0;
     c->counted = false;
+    c->res_is_input = false;
 }
 
 // Device memory this context may still use: free + its pool's cached blocks,
@@ -683,6 +694,27 @@ static okm_status result_to_folded_run(okm_ctx *c, Run *out) {
     c->counted = false;
     if (run.n) OKM_TRY(sorted_run_bins(c, run));
     *out = std::move(run);
+    return OKM_OK;
+}
+
+// Before new input: drop the result, unless it is the only record of the
+// input so far (res_is_input: its borrowed runs were released once counted),
+// in which case it stays as a folded run that the next count merges with the
+// new input (count.rs:48: one map across every add).
+static okm_status before_add(okm_ctx *c) {
+    if (!(c->counted && c->res_is_input)) {
+        invalidate_result(c);
+        return OKM_OK;
+    }
+    c->res_is_input = false;
+    Run t;
+    OKM_TRY(result_to_folded_run(c, &t));
+    if (t.n) {
+        c->runs.push_back(std::move(t));
+    } else {
+        c->pool.put(t.keys);
+        c->pool.put(t.counts);
+    }
     return OKM_OK;
 }
 
@@ -1568,8 +1600,24 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
 static okm_status count_general(okm_ctx *c);
 static okm_status count_unsorted_to_table(okm_ctx *c);
 
+static okm_status do_count_runs(okm_ctx *c);
+
+// Count the runs; afterwards no run may still point at caller memory: the
+// caller may free a borrowed run (okm_add_sorted_pairs_device) once okm_count
+// returns, so those runs are released and the result stands for the input.
 static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
+    OKM_TRY(do_count_runs(c));
+    bool borrowed = false;
+    for (auto &r : c->runs) borrowed |= r.borrowed;
+    if (borrowed && c->counted) {
+        release_runs(c, c->runs);
+        c->res_is_input = true;
+    }
+    return OKM_OK;
+}
+
+static okm_status do_count_runs(okm_ctx *c) {
     invalidate_result(c);
     if (c->runs.size() == 1 && c->runs[0].folded) {  // nothing added since the fold: its table is the result
         Run &r = c->runs[0];
@@ -1579,6 +1627,7 @@ static okm_status do_count(okm_ctx *c) {
         c->info.distinct = r.n;
         c->runs.clear();
         c->counted = true;
+        c->res_is_input = true;  // the fold's table was the input: kept on the next add
         return OKM_OK;
     }
     bool any_sorted = false, all_sorted = !c->runs.empty();
@@ -1619,6 +1668,7 @@ static okm_status do_count(okm_ctx *c) {
         c->info.levels = 0;
         c->info.work_items = 0;
         c->counted = true;
+        c->res_is_input = true;  // its run is gone: the copy is kept on the next add
         return OKM_OK;
     }
     if (all_sorted) {
@@ -1940,14 +1990,31 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     if (mode == 0 || group_keys >= total) return count_parts(c, segtab, parts, weighted, cp, nullptr);
 
     ResDst d{nullptr, nullptr, 0};
-    if (mode == 1) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &d.counts));
-    }
     struct Tab {
         uint64_t *keys, *counts, n;
     };
     std::vector<Tab> tabs;
+    // every table block goes back to the pool on any error path (a stranded
+    // block would make the caller's retry run out of memory sooner)
+    struct Guard {
+        okm_ctx *c;
+        ResDst *d;
+        std::vector<Tab> *tabs;
+        bool armed = true;
+        ~Guard() {
+            if (!armed) return;
+            c->pool.put(d->keys);
+            c->pool.put(d->counts);
+            for (auto &t : *tabs) {
+                c->pool.put(t.keys);
+                c->pool.put(t.counts);
+            }
+        }
+    } guard{c, &d, &tabs};
+    if (mode == 1) {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &d.counts));
+    }
     okm_engine_info agg = c->info;
     agg.work_items = 0;
     agg.max_partition = 0;
@@ -1978,6 +2045,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     }
     uint64_t nd = d.off;
     if (mode == 1) {
+        guard.armed = false;
         c->res_keys = d.keys;
         c->res_counts = d.counts;
     } else {
@@ -1995,11 +2063,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
             }
             o += t.n;
         }
-        OKM_TRY(sync(c));
-        for (auto &t : tabs) {
-            c->pool.put(t.keys);
-            c->pool.put(t.counts);
-        }
+        OKM_TRY(sync(c));  // the guard returns the groups' tables (and only them: d is unused in mode 2)
     }
     agg.distinct = nd;
     agg.groups = ngroups;
@@ -2217,7 +2281,7 @@ okm_status okm_add_batch(okm_ctx *c, const uint8_t *seq, const uint64_t *offsets
     }
     OKM_TRY(ensure_staging(c, o));
     HIP_TRY(hipMemcpyAsync(c->staging, dst, o, hipMemcpyHostToDevice, c->stream));
-    invalidate_result(c);
+    OKM_TRY(before_add(c));
     return l1_batch(c, c->staging, o);
 }
 
@@ -2226,7 +2290,7 @@ okm_status okm_add_batch_device(okm_ctx *c, const uint8_t *d_seq, uint64_t n_byt
     if (n_bytes == 0) return OKM_OK;
     if (!d_seq) return fail(OKM_E_ARG, "okm_add_batch_device: null pointer");
     HIP_TRY(hipSetDevice(c->device));
-    invalidate_result(c);
+    OKM_TRY(before_add(c));
     if ((reinterpret_cast<uintptr_t>(d_seq) & 15u) != 0) {
         OKM_TRY(ensure_staging(c, n_bytes));
         HIP_TRY(hipMemcpyAsync(c->staging, d_seq, n_bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -2240,7 +2304,7 @@ okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64
     if (n == 0) return OKM_OK;
     if (!d_keys) return fail(OKM_E_ARG, "okm_add_pairs_device: null keys");
     HIP_TRY(hipSetDevice(c->device));
-    invalidate_result(c);
+    OKM_TRY(before_add(c));
     Run run;
     OKM_TRY(partition_pairs(c, d_keys, d_counts, n, run));
     c->runs.push_back(std::move(run));
@@ -2252,7 +2316,7 @@ okm_status okm_add_sorted_pairs_device(okm_ctx *c, const uint64_t *d_keys, const
     if (n == 0) return OKM_OK;
     if (!d_keys) return fail(OKM_E_ARG, "okm_add_sorted_pairs_device: null keys");
     HIP_TRY(hipSetDevice(c->device));
-    invalidate_result(c);
+    OKM_TRY(before_add(c));
     Run run;
     run.keys = const_cast<uint64_t *>(d_keys);
     run.counts = const_cast<uint64_t *>(d_counts);

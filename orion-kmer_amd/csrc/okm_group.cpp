@@ -296,6 +296,7 @@ okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t m
     struct Chunk {
         const uint64_t *k, *c;
         uint64_t n;
+        int device;  // the owning GPU: the copy runs on its device, not device 0's
     };
     std::vector<Chunk> chunks;
     uint64_t per = uint64_t(1) << 24;  // entries per chunk (256 MB of keys + counts at k <= 32)
@@ -304,7 +305,8 @@ okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t m
         const uint64_t *dk = nullptr, *dc = nullptr;
         uint64_t n = 0;
         if ((s = okm_result_device(W.ctx, &dk, &dc, &n)) != OKM_OK) return s;
-        for (uint64_t o = 0; o < n; o += per) chunks.push_back({dk + o * kw, dc + o, std::min(per, n - o)});
+        for (uint64_t o = 0; o < n; o += per)
+            chunks.push_back({dk + o * kw, dc + o, std::min(per, n - o), okm::ctx_device(W.ctx)});
     }
     uint64_t cap = 0;
     for (auto &c : chunks) cap = std::max(cap, c.n);
@@ -341,8 +343,8 @@ okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t m
                 cv.wait(lk, [&] { return stop || i < consumed + 2; });
                 if (stop) return;
             }
-            okm_status st = okm_memcpy_d2h(sl.k, chunks[i].k, chunks[i].n * kw * 8);
-            if (st == OKM_OK) st = okm_memcpy_d2h(sl.c, chunks[i].c, chunks[i].n * 8);
+            okm_status st = okm::memcpy_d2h_on(chunks[i].device, sl.k, chunks[i].k, chunks[i].n * kw * 8);
+            if (st == OKM_OK) st = okm::memcpy_d2h_on(chunks[i].device, sl.c, chunks[i].c, chunks[i].n * 8);
             std::lock_guard<std::mutex> lk(mu);
             if (st != OKM_OK) {
                 copy_st = st;

@@ -21,6 +21,9 @@ constexpr uint64_t kEmptyKey = ~0ull;
 // (okm_group.cpp's device-to-file stream); nullptr on failure.
 void *host_pinned_alloc(size_t bytes);
 void host_pinned_free(void *p);
+// Device-to-host copy issued on `device` (this thread's current device is set
+// to it first, so the copy does not queue behind device 0's null stream).
+okm_status memcpy_d2h_on(int device, void *dst, const void *src, size_t bytes);
 
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);

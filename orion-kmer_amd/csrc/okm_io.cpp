@@ -793,19 +793,42 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
     if (k == 0 || k > 64) return fail(OKM_E_INVALID_K, "Invalid K-mer size");
     const int kw = k > 32 ? 2 : 1;
     const std::string ext = lower_extension(path);
-    const bool plain = ext != "gz" && ext != "xz" && ext != "zst" && ext != "zstd";
+    bool plain = ext != "gz" && ext != "xz" && ext != "zst" && ext != "zstd";
     int fd = -1;
     OutWriter w;
     if (plain) {
-        // no O_TRUNC: a rerun over an existing output overwrites its page-cache
-        // pages in place (truncating a multi-GB file first costs ~0.8 s); the
-        // length is set once at the end
-        fd = ::open(path, O_WRONLY | O_CREAT, 0644);
-        if (fd < 0) return fail(OKM_E_IO, std::string("cannot create ") + path);
-    } else {
+        // A regular file is written in place by offset (pwrite) and cut to
+        // length at the end: no O_TRUNC, so a rerun over an existing output
+        // overwrites its page-cache pages instead of first truncating a
+        // multi-GB file (~0.8 s).  Anything else (a pipe, FIFO, tty,
+        // /dev/stdout) cannot seek: it takes the sequential writer below, like
+        // the reference's File::create (utils.rs:168).
+        struct stat st;
+        if (::stat(path, &st) == 0 && !S_ISREG(st.st_mode)) {
+            plain = false;
+        } else {
+            fd = ::open(path, O_WRONLY | O_CREAT, 0644);
+            if (fd < 0) return fail(OKM_E_IO, std::string("cannot create ") + path);
+            if (::fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+                ::close(fd);
+                fd = -1;
+                plain = false;
+            }
+        }
+    }
+    if (!plain) {
         okm_status s = w.open(path);
         if (s != OKM_OK) return s;
     }
+    // on failure a plain output keeps only the complete chunks written so far
+    // (never a new prefix over an old file's tail)
+    auto abandon = [&](uint64_t keep) {
+        if (fd >= 0) {
+            if (::ftruncate(fd, (off_t)keep) != 0) (void)::unlink(path);
+            ::close(fd);
+            fd = -1;
+        }
+    };
     const uint64_t step = plain ? (1 << 16) : (1 << 17);
     uint64_t at_byte = 0, lines = 0;
     std::atomic<int> bad{0};
@@ -814,7 +837,7 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
         uint64_t n = 0;
         okm_status s = get(ci, &keys, &counts, &n);
         if (s != OKM_OK) {
-            if (fd >= 0) ::close(fd);
+            abandon(at_byte);
             return s;
         }
         if (!n) continue;
@@ -829,6 +852,7 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
                 off[b + 1] += off[b];
                 lines += cnt[b];
             }
+            const uint64_t chunk_start = at_byte;
             const size_t nt = std::min<size_t>(nb, (size_t)host_threads());
             parallel_for(nt, [&](size_t t) {
                 std::string buf;
@@ -850,6 +874,10 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
                     }
                 }
             });
+            if (bad) {
+                abandon(chunk_start);
+                break;
+            }
             at_byte += off[nb];
         } else {
             const size_t per_round = 2 * (size_t)host_threads();
@@ -875,10 +903,13 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
     }
     if (n_lines) *n_lines = lines;
     if (plain) {
-        if (!bad && ::ftruncate(fd, (off_t)at_byte) != 0) bad = 1;
-        if (::close(fd) != 0 && !bad) bad = 1;
         if (bad == 2) return fail(OKM_E_IO, "TSV block length mismatch");
         if (bad) return fail(OKM_E_IO, std::string("write failed: ") + path);
+        if (::ftruncate(fd, (off_t)at_byte) != 0) {
+            abandon(0);
+            return fail(OKM_E_IO, std::string("write failed: ") + path);
+        }
+        if (::close(fd) != 0) return fail(OKM_E_IO, std::string("write failed: ") + path);
         return OKM_OK;
     }
     return w.close();

@@ -27,7 +27,7 @@ __all__ = [
     "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads", "synth_reads_device",
     "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
     "KmerSet", "Classifier", "run_query", "run_classify", "read_fastx_records",
-    "Comm", "comm_unique_id", "owner_bounds", "synth_reads_device",
+    "Comm", "comm_unique_id", "owner_bounds", "synth_reads_device", "distributed_compare",
 ]
 
 
@@ -249,6 +249,7 @@ class KmerCounter:
     def __init__(self, k: int, mode: str = "count", device: int = 0, distinct_hint: int = 0,
                  wide: bool = False):
         self.k = k
+        self.device = device
         self.wide = bool(wide) and k > 32
         self.ctx = c_void_p()
         m = OKM_MODE_SET if mode == "set" else OKM_MODE_COUNT
@@ -400,6 +401,14 @@ class Comm:
         check(lib().okm_comm_init_all(arr, n, devs), "okm_comm_init_all")
         return [cls(n, i, b"", devices[i], _handle=c_void_p(arr[i])) for i in range(n)]
 
+    @classmethod
+    def init_loopback(cls, n: int, device: int = 0) -> List["Comm"]:
+        """n virtual ranks on one device (okm_comm_init_loopback): the P > 1
+        merge without RCCL; drive each rank's merge_owned from its own thread."""
+        arr = (c_void_p * n)()
+        check(lib().okm_comm_init_loopback(arr, n, device), "okm_comm_init_loopback")
+        return [cls(n, i, b"", device, _handle=c_void_p(arr[i])) for i in range(n)]
+
     @property
     def rank(self) -> int:
         return int(lib().okm_comm_rank(self.h))
@@ -414,10 +423,34 @@ class Comm:
         check(lib().okm_merge_owned(local.ctx, self.h, owner.ctx, byref(n)), "okm_merge_owned")
         return n.value
 
+    def merge_owned_n(self, locals_: Sequence["KmerCounter"], owners: Sequence["KmerCounter"]) -> List[int]:
+        """Collective: owners[i] <- this rank's key range of every rank's
+        locals_[i], all tables under one owner split (okm_merge_owned_n)."""
+        n = len(locals_)
+        la = (c_void_p * n)(*[c.ctx for c in locals_])
+        oa = (c_void_p * n)(*[c.ctx for c in owners])
+        out = (c_uint64 * n)()
+        check(lib().okm_merge_owned_n(la, self.h, oa, n, out), "okm_merge_owned_n")
+        return [int(x) for x in out]
+
+    def allreduce(self, values: Sequence[int]) -> List[int]:
+        """Collective sum of u64 values (okm_comm_allreduce_u64)."""
+        n = len(values)
+        a = (c_uint64 * n)(*[int(v) for v in values])
+        out = (c_uint64 * n)()
+        check(lib().okm_comm_allreduce_u64(self.h, a, out, n), "okm_comm_allreduce_u64")
+        return [int(x) for x in out]
+
     def last_times(self) -> Dict[str, float]:
         v = (ctypes.c_double * 4)()
         check(lib().okm_comm_last_times(self.h, v), "okm_comm_last_times")
         return {"plan_ms": v[0], "exchange_ms": v[1], "merge_ms": v[3]}
+
+    def last_bytes(self) -> Tuple[int, int]:
+        """(sent, received) bytes to / from other ranks in the last merge_owned."""
+        a, b = c_uint64(), c_uint64()
+        check(lib().okm_comm_last_bytes(self.h, byref(a), byref(b)), "okm_comm_last_bytes")
+        return a.value, b.value
 
     def close(self) -> None:
         if self.h:
@@ -429,6 +462,25 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def distributed_compare(comm: "Comm", a: "KmerCounter", b: "KmerCounter", owner_a: "KmerCounter",
+                        owner_b: "KmerCounter") -> Tuple[int, int, int]:
+    """compare.rs:51-66 over the ranks of `comm` (collective): a / b hold this
+    rank's share of DB1's / DB2's k-mers (set contexts).  Both go to key-range
+    owners under ONE split (okm_merge_owned_n), so a key of A and the same key
+    of B meet on one rank; each owner intersects its two ranges on its GPU
+    (compare.rs:58) and |A|, |B|, |A ∩ B| are summed over the ranks.  Every
+    rank returns the global (|A|, |B|, |A ∩ B|); union and Jaccard follow on
+    the host (compare.rs:60-66)."""
+    na, nb = comm.merge_owned_n([a, b], [owner_a, owner_b])
+    inter = 0
+    if na and nb:
+        pa, _, _ = owner_a.result_device()
+        pb, _, _ = owner_b.result_device()
+        inter = set_intersection_size_device(pa, na, pb, nb, owner_a.device)
+    ta, tb, ti = comm.allreduce([na, nb, inter])
+    return ta, tb, ti
 
 
 def set_intersection_size(a: np.ndarray, b: np.ndarray, device: int = 0) -> int:

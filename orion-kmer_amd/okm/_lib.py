@@ -143,11 +143,15 @@ PROTOTYPES = {
     "okm_comm_unique_id": (c_int, [c_void_p]),
     "okm_comm_init_rank": (c_int, [POINTER(c_void_p), c_int, c_int, c_void_p, c_int]),
     "okm_comm_init_all": (c_int, [c_void_p, c_int, c_void_p]),
+    "okm_comm_init_loopback": (c_int, [c_void_p, c_int, c_int]),
     "okm_comm_destroy": (None, [c_void_p]),
     "okm_comm_rank": (c_int, [c_void_p]),
     "okm_comm_size": (c_int, [c_void_p]),
     "okm_merge_owned": (c_int, [c_void_p, c_void_p, c_void_p, _P64]),
+    "okm_merge_owned_n": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "okm_comm_allreduce_u64": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
     "okm_comm_last_times": (c_int, [c_void_p, POINTER(c_double)]),
+    "okm_comm_last_bytes": (c_int, [c_void_p, _P64, _P64]),
     "okm_owner_bounds": (c_int, [c_void_p, c_uint32, c_int, c_void_p]),
     "okm_group_create": (c_int, [POINTER(c_void_p), c_uint8, c_int, c_int, c_void_p, c_uint64]),
     "okm_group_destroy": (None, [c_void_p]),

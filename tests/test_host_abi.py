@@ -143,6 +143,33 @@ def test_empty_tsv(tmp_path):
     assert open(p, "rb").read() == b""
 
 
+def test_tsv_to_fifo(tmp_path):
+    """`count -o <pipe>`: a plain output that cannot seek is written
+    sequentially (utils.rs:168 File::create works on any path), not by offset."""
+    import threading
+    k = 13
+    rng = np.random.default_rng(3)
+    keys = np.sort(rng.integers(0, 1 << 26, 200_000, dtype=np.uint64))
+    counts = rng.integers(1, 1000, 200_000, dtype=np.uint64)
+    fifo = str(tmp_path / "out.tsv")
+    os.mkfifo(fifo)
+    got = []
+    reader = threading.Thread(target=lambda: got.append(open(fifo, "rb").read()))
+    reader.start()
+    okm.write_counts_tsv(fifo, k, keys, counts)
+    reader.join(timeout=60)
+    exp = "".join(f"{R.u64_to_seq(int(a), k).decode()}\t{int(b)}\n" for a, b in zip(keys, counts))
+    assert got and got[0].decode() == exp
+
+
+def test_tsv_overwrites_longer_file(tmp_path):
+    """A rerun over a longer existing output leaves exactly the new table."""
+    p = tmp_path / "o.tsv"
+    p.write_bytes(b"Z" * 100_000)
+    okm.write_counts_tsv(str(p), 3, np.array([1, 6], np.uint64), np.array([2, 9], np.uint64))
+    assert p.read_bytes() == b"AAC\t2\nACG\t9\n"
+
+
 def test_kmerdb_roundtrip_and_bincode_layout(tmp_path):
     db = okm.KmerDb(4)
     db.add_reference("a.fa", np.array([1, 5, 9], np.uint64))
