@@ -1,25 +1,19 @@
 """Set mode (build.rs:46-58) and compare (compare.rs:51-66) on the device at
-sample scale, and the two-rank table merge / compare driven through the HIP
-engine (gloo moves the runs between two processes sharing the one MI355X of
-the box; RCCL refuses two ranks on one device, so the library communicator is
-covered at one rank in test_gpu_dist.py).
+sample scale.  The multi-rank table merge and the distributed compare run
+through the library's own exchange (okm_merge_owned / okm_merge_owned_n) at
+P = 2, 3 and 8 virtual ranks on the one device in test_gpu_loopback.py.
 
 Oracles: the C restatement's sets (oracle/okm_oracle.c: every canonical key of
 build.rs:46-58's DashSet) and numpy's union1d / intersect1d for
 db_types.rs:43-53 get_all_kmers_unified and compare.rs:58's intersection."""
 
 import os
-import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import okm
-from okm import dist as okm_dist
-from oracle import OracleCounter, count_separated_mt
+from oracle import count_separated_mt
 
 pytestmark = pytest.mark.gpu
 
@@ -113,138 +107,3 @@ def test_set_union_of_sorted_runs_and_intersection_device(k):
         assert okm.set_intersection_size(runs[x], runs[y]) == e
     for b in bufs:
         b.free()
-
-
-# ---------------------------------------------------------------------------
-# two ranks (gloo between processes) driving the HIP engine end to end
-# ---------------------------------------------------------------------------
-
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _count_worker(rank, world, port, k, out_path):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        batch = okm.synth_reads(60_000, 150, genome_len=300_000, genome_seed=31, seed=32)
-        recs = batch.reshape(60_000, 151)
-        recs[::40, :150] = ord("A")  # a hot key: counts past the one-byte escape
-        shard = np.ascontiguousarray(np.array_split(recs, world)[rank]).reshape(-1)
-        buf = okm.DeviceBuffer(len(shard))
-        buf.upload(shard)
-        with okm.KmerCounter(k) as local, okm.KmerCounter(k) as owner:
-            local.add_device_batch(buf.address, len(shard))
-            lk, lc = local.result(1)
-            rk, rc, _, rs = okm_dist.exchange_runs(torch.from_numpy(lk.view(np.int64).copy()),
-                                                   torch.from_numpy(lc.view(np.int64).copy()), k)
-            dk, dc = _upload(rk.numpy().view(np.uint64)), _upload(rc.numpy().view(np.uint64))
-            off = 0
-            for sz in rs:  # every rank's slice is sorted: merged in place by the k-way LDS merge
-                if sz:
-                    owner.add_sorted_pairs_device(dk.address + 8 * off, dc.address + 8 * off, sz)
-                off += sz
-            owner.count()
-            mk, mc = owner.result(1)
-            dk.free()
-            dc.free()
-        buf.free()
-        gk, gc = okm_dist.gather_global(torch.from_numpy(mk.view(np.int64).copy()),
-                                        torch.from_numpy(mc.view(np.int64).copy()))
-        if rank == 0:
-            np.savez(out_path, keys=gk, counts=gc)
-    finally:
-        dist.destroy_process_group()
-
-
-def test_two_ranks_hip_count_exchange_merge(tmp_path):
-    k, world = 31, 2
-    out = os.path.join(str(tmp_path), "merged.npz")
-    mp.spawn(_count_worker, args=(world, _free_port(), k, out), nprocs=world, join=True)
-    got = np.load(out)
-    batch = okm.synth_reads(60_000, 150, genome_len=300_000, genome_seed=31, seed=32)
-    batch.reshape(60_000, 151)[::40, :150] = ord("A")
-    oc = OracleCounter(k)
-    oc.add_separated(batch)
-    ek, ec = oc.result(1)
-    assert ec.max() > 255
-    assert np.array_equal(got["keys"], ek) and np.array_equal(got["counts"], ec)
-
-
-def _c5_samples():
-    return [_sample(8_000, 150, 40 + s, [(900 + (s % 4), 400_000), (904 + (s % 3), 300_000)]) for s in range(8)]
-
-
-def _compare_worker(rank, world, port, k, out_path):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        samples = _c5_samples()
-        half = len(samples) // 2
-        local = {0: [], 1: []}
-        for s in range(rank, len(samples), world):  # samples dealt round-robin
-            local[0 if s < half else 1].append(_device_set(samples[s], k))
-
-        def local_union(sets):  # this rank's share of a DB's references, unioned on the device
-            bufs = [_upload(x) for x in sets]
-            with okm.KmerCounter(k, "set") as u:
-                for x, b in zip(sets, bufs):
-                    if len(x):
-                        u.add_sorted_pairs_device(b.address, None, len(x))
-                u.count()
-                keys, _ = u.result(1)
-            for b in bufs:
-                b.free()
-            return torch.from_numpy(keys.view(np.int64).copy())
-
-        held = []
-
-        def union(rk, sizes):  # the owner's union of the received sorted runs (set mode, HIP)
-            arr = rk.numpy().view(np.uint64)
-            d = _upload(arr)
-            u = okm.KmerCounter(k, "set")
-            off = 0
-            for sz in sizes:
-                if sz:
-                    u.add_sorted_pairs_device(d.address + 8 * off, None, sz)
-                off += sz
-            n = u.count()
-            d.free()
-            held.append(u)
-            return n, u
-
-        def intersect(ha, na, hb, nb):  # |A ∩ B| of the two owned ranges, on the device
-            pa, _, _ = ha.result_device()
-            pb, _, _ = hb.result_device()
-            return okm.set_intersection_size_device(pa, na, pb, nb)
-
-        res = okm_dist.distributed_compare(local_union(local[0]), local_union(local[1]), k, union, intersect)
-        for u in held:
-            u.close()
-        if rank == 0:
-            np.savez(out_path, res=np.array(res, np.int64))
-    finally:
-        dist.destroy_process_group()
-
-
-def test_two_ranks_hip_distributed_compare(tmp_path):
-    k, world = 31, 2
-    out = os.path.join(str(tmp_path), "c5.npz")
-    mp.spawn(_compare_worker, args=(world, _free_port(), k, out), nprocs=world, join=True)
-    na, nb, inter = (int(x) for x in np.load(out)["res"])
-    samples = _c5_samples()
-    half = len(samples) // 2
-    sets = []
-    for s in samples:
-        oc = OracleCounter(k)
-        oc.add_separated(s)
-        sets.append(oc.result(1)[0])
-    a = np.unique(np.concatenate(sets[:half]))
-    b = np.unique(np.concatenate(sets[half:]))
-    assert (na, nb) == (len(a), len(b))
-    assert inter == len(np.intersect1d(a, b, assume_unique=True))
-    assert 0 < inter < min(na, nb)
