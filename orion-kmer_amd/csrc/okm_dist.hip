@@ -445,11 +445,17 @@ class LoopTransport final : public Transport {
     int me_;
 };
 
-// Bytes per point-to-point message piece (OKM_RCCL_PIECE; default 1 GiB).
+// Bytes per point-to-point message piece (OKM_RCCL_PIECE, default and
+// maximum 512 MiB).  RCCL 2.27.7 (ROCm 7.2) delivers only the FIRST HALF of a
+// self send/recv above 1 GiB -- every byte from size/2 on is left unwritten,
+// for u8 and u64 messages alike (1.5 GiB, 2 GiB, 4 GiB, 7.9 GB all lose their
+// second half; 1 GiB arrives intact: tools/rccl_big_p2p.hip,
+// profiles/r03_rccl_self_p2p_sizes.txt) -- so pieces stay well below 1 GiB.
 static uint64_t piece_bytes() {
+    constexpr uint64_t kMax = uint64_t(1) << 29;
     const char *e = getenv("OKM_RCCL_PIECE");
     const long long v = e ? atoll(e) : 0;
-    return v >= 8 ? (uint64_t)v & ~uint64_t(7) : (uint64_t(1) << 30);
+    return v >= 8 ? std::min<uint64_t>((uint64_t)v & ~uint64_t(7), kMax) : kMax;
 }
 
 }  // namespace okm

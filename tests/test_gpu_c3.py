@@ -176,9 +176,17 @@ def test_c3_shard_full_size(monkeypatch):
         assert bool((kk <= torch_revcomp(kk, k)).all().item()), "canonical (kmer.rs:99-106)"
     # a 1/P shard of a 1 Gbp genome at ~3.1x coverage: ~1e9 distinct
     assert 0.7e9 < info["distinct"] < 1.3e9
+    # the library's RCCL merge at one rank over this 7.9 GB table: the self
+    # send/recv goes in 1 GiB pieces (RCCL delivers half of a >= 2 GiB message)
+    want = _table_digest(keys, counts)
     del keys, counts, fk, fc, results
-    for c in ctrs:
-        c.close()
+    ctrs[0].close()
+    comm = okm.Comm(1, 0, okm.comm_unique_id(), 0)
+    assert comm.merge_owned(ctrs[1], ctrs[1]) == info["distinct"]
+    kp, cp, nn = ctrs[1].result_device()
+    assert _table_digest(dev_tensor(kp, nn), dev_tensor(cp, nn)) == want
+    comm.close()
+    ctrs[1].close()
     # exact parity on the first 1,000,000 reads of the shard (sharded restatement)
     m = 1_000_000
     host = np.empty(m * stride, dtype=np.uint8)
@@ -189,4 +197,112 @@ def test_c3_shard_full_size(monkeypatch):
         ctr.add_device_batch(buf.address, m * stride)
         gk, gc = ctr.result(1)
     buf.free()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def _table_digest(keys, counts, chunk=1 << 26):
+    """Order-sensitive 64-bit digests of a device table (int64 wraps), in
+    chunks: the engine's pool holds most of the device."""
+    d = [int(keys.numel()), 0, 0, 0]
+    for o in range(0, keys.numel(), chunk):
+        kk, cc = keys[o:o + chunk], counts[o:o + chunk]
+        pos = torch.arange(o, o + kk.numel(), dtype=torch.int64, device=kk.device)
+        mix = kk * 0x1E3779B97F4A7C15 - 0x61C8864680B583EB  # wraps: an odd multiplier is a bijection
+        d[1] += int(cc.sum().item())
+        d[2] += int((mix ^ cc).sum().item())
+        d[3] += int(((mix + pos) * (cc | 1)).sum().item())
+        del pos, mix
+    return (d[0], d[1], d[2] % (1 << 64), d[3] % (1 << 64))
+
+
+def _count_c3_p1(buf, spans, k):
+    ctr = okm.KmerCounter(k)
+    for off, nb in spans:
+        ctr.add_device_batch(buf.address + off, nb)
+    nd = ctr.count()
+    return ctr, nd
+
+
+def test_c3_p1_full_size(monkeypatch):
+    """BASELINE configs[2] on ONE GPU at full size (bench.py --workload c3
+    --gpus 1): 167,772,160 reads = 25,165,824,000 bases of a 1 Gbp genome,
+    generated on the device, counted batch by batch into ONE table
+    (count.rs:52-89), with folding and key-range groups active.  Checked on
+    the device: sum of counts == valid windows, strictly increasing canonical
+    keys, fold invariance (digests of the table at the default fold threshold
+    and at half of it); exact parity on the first 1,000,000 reads."""
+    k, read_len = 31, 150
+    n = C3_READS
+    stride = read_len + 1
+    buf = okm.DeviceBuffer(n * stride)
+    okm.synth_reads_device(buf.address, n, read_len, genome_len=C3_GENOME, genome_seed=C3_SEED, seed=C3_SEED,
+                           first_read=0, sub_rate=0.001, n_rate=0.0001)
+    vw = device_valid_windows(dev_tensor(buf.address, n * stride, "|u1"), read_len, k)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the engine's pool gets the device
+    batch_reads = 4_194_304
+    spans = [(b0 * stride, (min(n, b0 + batch_reads) - b0) * stride) for b0 in range(0, n, batch_reads)]
+    assert len(spans) == 40
+    monkeypatch.delenv("OKM_FOLD_BYTES", raising=False)
+    ctr, nd = _count_c3_p1(buf, spans, k)
+    info = ctr.engine_info()
+    assert info["folds"] >= 4, info  # memory bounded by distinct keys, not input
+    kp, cp, nn = ctr.result_device()
+    assert nn == nd
+    keys, counts = dev_tensor(kp, nd), dev_tensor(cp, nd)
+    assert int(counts.sum().item()) == vw == info["kmers"]
+    step = 1 << 26  # chunks: the engine's pool holds most of the device
+    for o in range(0, nd, step):
+        kk = keys[o:o + step + 1]
+        assert bool((kk[1:] > kk[:-1]).all().item()), "strictly increasing (count.rs:119)"
+        kk = kk[:step]
+        assert bool((kk <= torch_revcomp(kk, k)).all().item()), "canonical (kmer.rs:99-106)"
+        assert bool((kk >= 0).all().item()) and bool((kk < (1 << 62)).all().item())
+        assert bool((counts[o:o + step] >= 1).all().item())
+        del kk
+    # ~1.0e9 genomic + ~0.6e9 error k-mers (SURVEY §8(d): ~1.8e9 expected; measured 1.61e9)
+    assert 1.4e9 < nd < 1.9e9
+    d1 = _table_digest(keys, counts)
+    del keys, counts
+    ctr.close()
+    # the same input folded twice as often: the same table
+    total = torch.cuda.get_device_properties(0).total_memory
+    monkeypatch.setenv("OKM_FOLD_BYTES", str(int(0.04 * total)))
+    ctr2, nd2 = _count_c3_p1(buf, spans, k)
+    info2 = ctr2.engine_info()
+    assert info2["folds"] > info["folds"]
+    kp, cp, _ = ctr2.result_device()
+    d2 = _table_digest(dev_tensor(kp, nd2), dev_tensor(cp, nd2))
+    ctr2.close()
+    assert d1 == d2, "fold invariance"
+    # exact parity on the first 1,000,000 reads (sharded restatement)
+    m = 1_000_000
+    host = np.empty(m * stride, dtype=np.uint8)
+    buf.download(host)
+    thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+    ek, ec = count_separated_mt(host, k, thr)
+    with okm.KmerCounter(k) as c:
+        c.add_device_batch(buf.address, m * stride)
+        gk, gc = c.result(1)
+    buf.free()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_count_add_count_after_fold(monkeypatch):
+    """okm_count, more input, okm_count again: the folded table that became the
+    result is kept as input (one map across every add, count.rs:48)."""
+    monkeypatch.setenv("OKM_FOLD_BYTES", "1")
+    k = 25
+    b = okm.synth_reads(40_000, 150, genome_len=400_000, seed=19)
+    recs = [bytes(r) for r in b.tobytes().split(b"\n") if r]
+    ref = OracleCounter(k)
+    for _ in range(3):
+        ref.add_separated(b)
+    ek, ec = ref.result(1)
+    with okm.KmerCounter(k) as ctr:
+        ctr.add_records(recs, normalized=True)
+        ctr.add_records(recs, normalized=True)
+        ctr.count()
+        ctr.add_records(recs, normalized=True)
+        gk, gc = ctr.result(1)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)

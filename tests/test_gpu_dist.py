@@ -57,6 +57,28 @@ def test_merge_owned_single_rank_equals_local(comm1, genome):
     assert t["plan_ms"] >= 0 and t["exchange_ms"] >= 0 and t["merge_ms"] >= 0
 
 
+@pytest.mark.parametrize("piece", [4096, 1 << 20])
+def test_merge_owned_rccl_multi_piece(comm1, monkeypatch, piece):
+    """Real RCCL at one rank with every message cut into many pieces
+    (OKM_RCCL_PIECE): keys, count bytes and escapes of the self slice."""
+    monkeypatch.setenv("OKM_RCCL_PIECE", str(piece))
+    k = 31
+    b = _batch(200_000, 3_000_000, 8)
+    b.reshape(200_000, 151)[::50, :150] = ord("A")  # a hot key: counts past the one-byte escape
+    ref = OracleCounter(k)
+    ref.add_separated(b)
+    ek, ec = ref.result(1)
+    assert (ec > 255).any() and len(ek) * 8 > 16 * piece
+    buf = okm.DeviceBuffer(len(b))
+    buf.upload(b)
+    with okm.KmerCounter(k) as ctx:
+        ctx.add_device_batch(buf.address, len(b))
+        assert comm1.merge_owned(ctx, ctx) == len(ek)
+        gk, gc = ctx.result(1)
+    buf.free()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
 def test_merge_owned_set_mode(comm1):
     k = 21
     b = _batch(50_000, 300_000, 3)
