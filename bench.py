@@ -353,6 +353,16 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # one job alone (one context, one stream, one host thread): the latency of
+    # a single batch, beside the throughput of S batches in flight above
+    single_ms = None
+    if not dist_on and S > 1:
+        barrier_sync()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            count_batch(ctr)
+        ctr.synchronize()
+        single_ms = (time.perf_counter() - t1) / args.steps * 1e3
     # per-kernel HIP-event timing: a separate single-stream pass of the same K
     # steps (kernels of the timed region overlap across streams, so their
     # durations there would not be any one kernel's)
@@ -411,6 +421,9 @@ def main():
                             "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
                             "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
                             "input_stream_frac": round(bases * args.steps / dt / 8e12, 5)},
+        "single_job": ({"ms_per_step": round(single_ms, 3), "value": round(bases / (single_ms * 1e-3), 1),
+                        "note": "one context, one stream, one host thread: a batch's latency; `value` above "
+                                f"is {S} batches in flight"} if single_ms else None),
         "kernels": kernels,
         "engine": info,
     }
@@ -645,7 +658,13 @@ def cpu_baselines(host, m, m_mt, device, what):
     cpu_mt = None
     if m_mt > 0:
         nproc = os.cpu_count() or 1
-        thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or nproc), nproc))
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            avail = nproc
+        # the GPU box grants one GPU's job 16 host threads (OMP_NUM_THREADS=16);
+        # nproc / os.cpu_count() report the whole node's CPUs there
+        thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS") or avail), avail))
         sample = host[:m_mt * stride]
         tc = time.perf_counter()
         mk, mc = count_separated_mt(sample, K, thr)
@@ -657,6 +676,9 @@ def cpu_baselines(host, m, m_mt, device, what):
             gk, gc = chk.result(1)
             sb.free()
         cpu_mt = {"value": m_mt * READ_LEN / tmt, "unit": "bases/s", "threads": thr, "nproc": nproc,
+                  "affinity_cpus": avail,
+                  "threads_note": "OMP_NUM_THREADS: the host-thread share the GPU box grants one GPU's job "
+                                  "(nproc counts the whole node)",
                   "kind": "restatement-MT (not reference behaviour: count.rs is single-threaded)",
                   "sample": f"first {m_mt} reads ({m_mt * READ_LEN} bases) of {what}, k=31, {thr} shards "
                             f"counted by oracle/okm_oracle.c on {thr} threads + key-range merge, {tmt:.1f} s",

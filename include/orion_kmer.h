@@ -461,6 +461,19 @@ okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t s
 okm_status okm_synth_reads_device(uint64_t genome_seed, uint64_t genome_len, uint64_t seed,
                                   uint64_t first_read, uint64_t n_reads, uint32_t read_len,
                                   double sub_rate, double n_rate, uint8_t *d_out, int device);
+/* ONT-like long reads (BASELINE configs[3] shape): read
+ * r's length is lognormal (median_len, sigma) clipped to [min_len, max_len];
+ * its bases come from the genome (genome_seed, genome_len >= 2 max_len + 1)
+ * with per-base errors: substitution (sub_rate), insertion of a random base
+ * after the source base (ins_rate), deletion of the source base (del_rate);
+ * strand 50/50 (reverse complement).  Reads [first_read, first_read +
+ * n_reads), each followed by OKM_RECORD_SEPARATOR, into library-allocated
+ * *out (okm_free_result); *n_bytes = bytes; lens (optional, n_reads entries) =
+ * read lengths.  out == NULL: lengths and *n_bytes only. */
+okm_status okm_synth_long_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t seed, uint64_t first_read,
+                                uint64_t n_reads, double median_len, double sigma, uint32_t min_len,
+                                uint32_t max_len, double sub_rate, double ins_rate, double del_rate,
+                                uint8_t **out, uint64_t *n_bytes, uint32_t *lens, int threads);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,10 @@
 // 50/50, substitution errors, N bases).  Counter-based: every read is a pure
 // function of (seed, read index), so any thread count, any shard of read
 // indices and any machine produce identical bytes.
+#include <stdlib.h>
 #include <string.h>
+
+#include <cmath>
 
 #include <algorithm>
 #include <mutex>
@@ -101,5 +104,97 @@ extern "C" okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len,
         ts.emplace_back(work, a, b);
     }
     for (auto &t : ts) t.join();
+    return OKM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ONT-like long reads: lognormal lengths, either strand,
+// substitutions, insertions and deletions.  Counter-based like the reads above.
+// ---------------------------------------------------------------------------
+
+namespace okm {
+
+static inline double unit_open(uint64_t x) { return ((double)(x >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+
+// Read r's length: exp(ln(median) + sigma * z), z standard normal (Box-Muller
+// over two splitmix64 draws), clipped to [min_len, max_len].
+static uint32_t long_read_len(uint64_t seed, uint64_t r, double median, double sigma, uint32_t lo, uint32_t hi) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(r ^ 0x5851F42D4C957F2Dull));
+    const double u1 = unit_open(h), u2 = unit_open(splitmix64(h));
+    const double z = std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    const double L = std::exp(std::log(median) + sigma * z);
+    return (uint32_t)std::min<double>(hi, std::max<double>(lo, std::floor(L)));
+}
+
+}  // namespace okm
+
+extern "C" okm_status okm_synth_long_reads(uint64_t genome_seed, uint64_t genome_len, uint64_t seed,
+                                           uint64_t first_read, uint64_t n_reads, double median_len, double sigma,
+                                           uint32_t min_len, uint32_t max_len, double sub_rate, double ins_rate,
+                                           double del_rate, uint8_t **out, uint64_t *n_bytes, uint32_t *lens,
+                                           int threads) {
+    if (!n_bytes || min_len == 0 || max_len < min_len || median_len <= 0 || sigma < 0 ||
+        genome_len < 2ull * max_len + 1 || sub_rate < 0 || ins_rate < 0 || del_rate < 0 ||
+        sub_rate + ins_rate + del_rate >= 1.0)
+        return fail(OKM_E_ARG, "okm_synth_long_reads: bad arguments");
+    if (out) *out = nullptr;
+    std::vector<uint64_t> off(n_reads + 1, 0);
+    for (uint64_t i = 0; i < n_reads; ++i) {
+        const uint32_t L = long_read_len(seed, first_read + i, median_len, sigma, min_len, max_len);
+        if (lens) lens[i] = L;
+        off[i + 1] = off[i] + L + 1;
+    }
+    *n_bytes = off[n_reads];
+    if (!out) return OKM_OK;  // lengths only
+    uint8_t *buf = (uint8_t *)malloc(std::max<uint64_t>(off[n_reads], 1));
+    if (!buf) return fail(OKM_E_NOMEM, "okm_synth_long_reads: host allocation");
+    const Genome &G = genome(genome_seed, genome_len);
+    const uint8_t *g = G.codes.data();
+    const uint64_t npos = genome_len - 2ull * max_len;  // a read consumes < 2 L source bases
+    // per-base draw u (32 bits): [0, t1) substitution, [t1, t2) insertion after
+    // the base, [t2, t3) deletion of the base, else the base as it is
+    const uint64_t t1 = (uint64_t)(sub_rate * 4294967296.0);
+    const uint64_t t2 = t1 + (uint64_t)(ins_rate * 4294967296.0);
+    const uint64_t t3 = t2 + (uint64_t)(del_rate * 4294967296.0);
+    auto work = [&](uint64_t a, uint64_t b) {
+        for (uint64_t i = a; i < b; ++i) {
+            const uint64_t r = first_read + i;
+            const uint64_t h = splitmix64(seed ^ splitmix64(r));
+            const uint64_t pos = h % npos;
+            const bool rev = (splitmix64(h) >> 63) != 0;
+            uint8_t *o = buf + off[i];
+            const uint64_t L = off[i + 1] - off[i] - 1;
+            uint64_t j = 0, src = pos, d = 0;
+            while (j < L) {
+                const uint64_t draw = splitmix64(h + 0x632BE59BD9B4E019ull * (++d));
+                const uint64_t u = draw & 0xFFFFFFFFull;
+                const uint32_t code = g[src++];
+                if (u < t1) {
+                    o[j++] = (uint8_t)((code + 1 + (uint32_t)((draw >> 32) % 3)) & 3u);
+                } else if (u < t2) {
+                    o[j++] = (uint8_t)code;
+                    if (j < L) o[j++] = (uint8_t)((draw >> 32) & 3u);
+                } else if (u >= t3) {
+                    o[j++] = (uint8_t)code;
+                }  // else: deleted
+            }
+            if (rev) {  // the other strand: reverse complement of the read
+                std::reverse(o, o + L);
+                for (uint64_t q = 0; q < L; ++q) o[q] = (uint8_t)(3u - o[q]);
+            }
+            for (uint64_t q = 0; q < L; ++q) o[q] = (uint8_t)"ACGT"[o[q]];
+            o[L] = OKM_RECORD_SEPARATOR;
+        }
+    };
+    int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::min<uint64_t>((uint64_t)nt, std::max<uint64_t>(1, n_reads / 64));
+    std::vector<std::thread> ts;
+    const uint64_t per = (n_reads + nt - 1) / std::max(nt, 1);
+    for (int t = 0; t < nt; ++t) {
+        const uint64_t a = std::min<uint64_t>(n_reads, t * per), b = std::min<uint64_t>(n_reads, a + per);
+        if (a < b) ts.emplace_back(work, a, b);
+    }
+    for (auto &t : ts) t.join();
+    *out = buf;
     return OKM_OK;
 }

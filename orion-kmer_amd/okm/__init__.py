@@ -24,7 +24,7 @@ from ._lib import (OKM_E_DEVICE, OKM_E_INVALID_K, OKM_E_IO, OKM_E_PARSE, OKM_E_R
 __all__ = [
     "seq_to_u64", "u64_to_seq", "reverse_complement_u64", "canonical_u64",
     "KmerCounter", "DeviceBuffer", "device_count", "device_arch", "pack_records",
-    "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads", "synth_reads_device",
+    "parse_fastx", "read_fastx_file", "write_counts_tsv", "synth_reads", "synth_reads_device", "synth_long_reads",
     "run_count", "run_build", "run_compare", "KmerDb", "OkmError",
     "KmerSet", "Classifier", "run_query", "run_classify", "read_fastx_records",
     "Comm", "comm_unique_id", "owner_bounds", "synth_reads_device", "distributed_compare",
@@ -234,6 +234,40 @@ def synth_reads_device(d_out: int, n_reads: int, read_len: int = 150, genome_len
     check(lib().okm_synth_reads_device(genome_seed, genome_len, seed, first_read, n_reads, read_len, sub_rate,
                                        n_rate, c_void_p(d_out), device), "okm_synth_reads_device")
     return n_reads * (read_len + 1)
+
+
+def synth_long_reads(gbases: float, genome_len: int, genome_seed: int = 4, seed: int = 4,
+                     median_len: float = 2891.0, sigma: float = 1.085, min_len: int = 200, max_len: int = 100_000,
+                     sub_rate: float = 0.025, ins_rate: float = 0.0125, del_rate: float = 0.0125,
+                     threads: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """ONT-like reads of at least `gbases` bases in the device batch layout
+    (okm_synth_long_reads; BASELINE configs[3] / SURVEY §8(d) C4: lognormal
+    lengths, median 2,891, sigma 1.085, 200..100k; 5 % errors split into
+    substitutions 2.5 %, insertions 1.25 %, deletions 1.25 %).  Returns
+    (batch, read lengths)."""
+    target = int(gbases * 1e9)
+    n_guess = max(16, int(target / (median_len * np.exp(sigma * sigma / 2))) + 1)
+    while True:  # enough reads for the target (lengths only, cheap)
+        lens = np.zeros(n_guess, np.uint32)
+        nb = c_uint64()
+        check(lib().okm_synth_long_reads(genome_seed, genome_len, seed, 0, n_guess, median_len, sigma, min_len,
+                                         max_len, sub_rate, ins_rate, del_rate, None, byref(nb),
+                                         lens.ctypes.data, threads), "okm_synth_long_reads")
+        csum = np.cumsum(lens, dtype=np.uint64)
+        if int(csum[-1]) >= target:
+            n = int(np.searchsorted(csum, target)) + 1
+            break
+        n_guess *= 2
+    ptr = c_void_p()
+    nb = c_uint64()
+    check(lib().okm_synth_long_reads(genome_seed, genome_len, seed, 0, n, median_len, sigma, min_len, max_len,
+                                     sub_rate, ins_rate, del_rate, byref(ptr), byref(nb), None, threads),
+          "okm_synth_long_reads")
+    try:
+        out = np.ctypeslib.as_array(ctypes.cast(ptr, POINTER(ctypes.c_uint8)), shape=(nb.value,)).copy()
+    finally:
+        lib().okm_free_result(ptr)
+    return out, lens[:n].astype(np.int64)
 
 
 # ---------------------------------------------------------------------------

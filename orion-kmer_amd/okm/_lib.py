@@ -163,6 +163,9 @@ PROTOTYPES = {
     "okm_group_write_counts_tsv": (c_int, [c_void_p, c_char_p, c_uint64, _P64]),
     "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                        c_double, c_void_p, c_int]),
+    "okm_synth_long_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_double, c_double, c_uint32,
+                                     c_uint32, c_double, c_double, c_double, POINTER(c_void_p), _P64, c_void_p,
+                                     c_int]),
 }
 
 _lib = None

@@ -30,35 +30,12 @@ def _threads():
 
 
 def ont_batch(gbases: float, seed: int, genome_len: int = 200_000_000):
-    """ONT-like reads in the device batch layout (records + '\\n'): lognormal
-    lengths (median 2,891, sigma 1.085, clipped 200..100k), either strand,
-    5 % substitutions, from a seeded random genome.  Returns (batch, lengths)."""
-    rng = np.random.default_rng(seed)
-    genome = rng.integers(0, 4, genome_len, dtype=np.uint8)
-    target = int(gbases * 1e9)
-    lens = []
-    tot = 0
-    while tot < target:
-        L = np.clip(np.exp(np.log(2891.0) + 1.085 * rng.standard_normal(65536)), 200, 100_000).astype(np.int64)
-        lens.append(L)
-        tot += int(L.sum())
-    lens = np.concatenate(lens)
-    lens = lens[:int(np.searchsorted(np.cumsum(lens), target)) + 1]
-    starts = rng.integers(0, genome_len - 100_001, size=len(lens))
-    flip = rng.random(len(lens)) < 0.5
-    out = np.empty(int(lens.sum()) + len(lens), np.uint8)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    o = 0
-    for i in range(len(lens)):
-        L = int(lens[i])
-        c = genome[starts[i]:starts[i] + L]
-        c = (3 - c)[::-1] if flip[i] else c.copy()
-        m = rng.random(L) < 0.05
-        c[m] = (c[m] + rng.integers(1, 4, int(m.sum()), dtype=np.uint8)) % 4
-        out[o:o + L] = acgt[c]
-        out[o + L] = ord("\n")
-        o += L + 1
-    return out, lens
+    """ONT-like reads in the device batch layout (records + '\\n'), SURVEY
+    §8(d) C4: lognormal lengths (median 2,891, sigma 1.085, clipped
+    200..100k), either strand, 5 % errors (2.5 % substitutions, 1.25 %
+    insertions, 1.25 % deletions; okm_synth_long_reads), from a seeded random
+    genome.  Returns (batch, lengths)."""
+    return okm.synth_long_reads(gbases, genome_len, genome_seed=seed, seed=seed)
 
 
 def _bins_of(keys):

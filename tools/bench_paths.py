@@ -11,13 +11,15 @@ input, warmup then timed steps bracketed by device syncs).
                      batch (okm_add_batch_device + okm_count in OKM_MODE_SET).
   --workload wide    BASELINE configs[3] shape — k=63 (two-u64 keys) over
                      ONT-like lognormal reads (median 2,891 bp, sigma 1.085,
-                     clipped 200..100k, 5 % substitutions); --gbases sets the
+                     clipped 200..100k, 5 % substitution + indel errors); --gbases sets the
                      size (configs[3] is ~5.36 Gbases).
   --workload c5      BASELINE configs[4] shape: build.rs per-sample sets of 64
                      WGS-shaped synthetic samples (tools/c5_runs.json) into two
                      databases, then compare.rs (unions, |A ∩ B|, Jaccard).
-                     Under torchrun (WORLD_SIZE > 1) the samples shard over the
-                     ranks and the unions are owner-partitioned (wl_c5_dist).
+                     Under torchrun (WORLD_SIZE > 1, RCCL) or with --loopback P
+                     (P virtual ranks on one GPU) the samples shard over the
+                     ranks and the unions are owner-partitioned by the
+                     library's exchange (wl_c5_dist, okm_merge_owned_n).
   --workload classify classify.rs:215-308 — probe a 32-reference database
                      (the genome split in 32 slices, ~100 M keys) against the
                      counted table of the batch (okm_classifier_probe_db).
@@ -40,6 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 
 import okm  # noqa: E402
+from okm import workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
 READS, READ_LEN, GENOME_BP = 3_355_443, 150, 100_000_000
@@ -141,32 +144,12 @@ def wl_build(args):
 
 
 def ont_batch(gbases: float, seed: int = 4):
-    """ONT-like reads: lognormal lengths, 5 % substitutions."""
-    rng = np.random.default_rng(seed)
-    target = int(gbases * 1e9)
-    genome = rng.integers(0, 4, size=min(target // 4 + 200_000, 1_000_000_000), dtype=np.uint8)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    lens = []
-    tot = 0
-    while tot < target:
-        L = rng.lognormal(np.log(2891.0), 1.085, size=65536).clip(200, 100_000).astype(np.int64)
-        lens.append(L)
-        tot += int(L.sum())
-    lens = np.concatenate(lens)
-    lens = lens[:np.searchsorted(np.cumsum(lens), target) + 1]
-    n = len(lens)
-    starts = rng.integers(0, len(genome) - 100_001, size=n)
-    out = np.empty(int(lens.sum()) + n, np.uint8)
-    o = 0
-    for i in range(n):
-        L = int(lens[i])
-        r = genome[starts[i]:starts[i] + L].copy()
-        m = rng.random(L) < 0.05
-        r[m] = rng.integers(0, 4, size=int(m.sum()), dtype=np.uint8)
-        out[o:o + L] = acgt[r]
-        out[o + L] = ord("\n")
-        o += L + 1
-    return out, n
+    """ONT-like reads (okm.workloads.c4_reads): lognormal
+    lengths (median 2,891, sigma 1.085, 200..100k), either strand, 5 %
+    substitution + indel errors (2.5 % substitutions, 1.25 % insertions, 1.25 %
+    deletions), seed 4, from a genome of a quarter of the bases."""
+    batch, lens = workloads.c4_reads(gbases, seed)
+    return batch, len(lens)
 
 
 def wl_wide(args):
@@ -196,36 +179,16 @@ def wl_wide(args):
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
             "dtype": "u128 (two u64)", "data": "synthetic ONT-like (device-resident)",
             "config": {"workload": f"BASELINE configs[3] shape at {args.gbases} Gbases: lognormal read "
-                                   "lengths (median 2891, sigma 1.085, 200..100k), 5 % substitutions",
+                                   "lengths (median 2891, sigma 1.085, 200..100k), 5 % substitution + indel errors",
                        "k": k, "reads": n, "bases": bases, "kmers": int(info["kmers"]),
                        "distinct": int(info["distinct"])},
             "kernels": kern, "engine": info}
 
 
 def c5_samples(cap_bases: float, which=None):
-    """64 synthetic samples shaped by 64 WGS runs of
-    data_metagenome.json.gz (tools/c5_runs.json: mean read length, base count
-    capped at cap_bases), each drawn from 3 of a pool of 48 seeded genomes
-    (2-8 Mbp); samples 0-31 (DB1) use genomes 0-35, samples 32-63 (DB2)
-    genomes 12-47, so the two halves share half of their genomes."""
-    runs = json.load(open(os.path.join(ROOT, "tools", "c5_runs.json")))["runs"]
-    glen = [2_000_000 + g * 6_000_000 // 47 for g in range(48)]
-    out = []
-    for s_, r in enumerate(runs):
-        if which is not None and s_ not in which:
-            continue
-        rng = np.random.default_rng(5_000 + s_)
-        lo = 0 if s_ < 32 else 12
-        gs = rng.choice(np.arange(lo, lo + 36), size=3, replace=False)
-        L = int(min(max(r["mean_read_len"], 100), 30_000))
-        bases = int(min(r["base_count"], cap_bases))
-        parts = []
-        for j, g in enumerate(gs):
-            nr = max(1, bases // 3 // L)
-            parts.append(okm.synth_reads(nr, L, genome_len=glen[g], genome_seed=9_000 + int(g),
-                                         seed=s_ * 16 + j, sub_rate=0.001, n_rate=0.0001))
-        out.append(np.concatenate(parts))
-    return out
+    """SURVEY §8(d) C5 (okm.workloads.c5_samples): 64 synthetic samples shaped
+    by 64 WGS runs of data_metagenome.json.gz (tools/c5_runs.json)."""
+    return workloads.c5_samples(cap_bases, which)
 
 
 def wl_c5(args):
@@ -363,38 +326,24 @@ def wl_c5(args):
                                        f"1 thread), {tcpu:.1f} s; engine set identical"}}
 
 
-def wl_c5_dist(args):
-    """C5 over WORLD_SIZE ranks, one GPU each (SURVEY.md §8(e) "C5"): the 64
-    samples are dealt round-robin (sample s -> rank s mod N), every rank builds
-    its samples' sets (build.rs:46-116) and unions its share of each DB's
-    references; okm.dist.distributed_compare then moves both unions to
-    value-range owners under one set of bounds, each owner unions and
-    intersects its ranges on its GPU and one all_reduce sums |A|, |B|, |A ∩ B|
-    (compare.rs:51-66).  Strong scaling: the 64-sample workload is fixed."""
-    import torch
-    import torch.distributed as tdist
-    from okm import dist as okm_dist
+def _c5_rank(rank, world, comm, device, args, steps, warmup, gate=None):
+    """One rank of the distributed C5 (SURVEY.md §8(e) "C5"): the 64 samples
+    dealt round-robin (sample s -> rank s mod N); this rank builds its
+    samples' sets (build.rs:46-116), unions its share of each DB's references
+    (sorted runs, set mode), and okm.distributed_compare moves both unions to
+    key-range owners under one split (okm_merge_owned_n), intersects each
+    owner's two ranges on its GPU and sums |A|, |B|, |A ∩ B| over the ranks
+    (compare.rs:51-66).  gate: a barrier shared by in-process ranks."""
     k = 31
-    world = int(os.environ["WORLD_SIZE"])
-    rank = int(os.environ["RANK"])
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(device)
-    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
-    if backend == "nccl":
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
-    else:
-        tdist.init_process_group(backend)
     mine = list(range(rank, 64, world))
-    t = time.time()
     samples = dict(zip(mine, c5_samples(args.c5_cap, set(mine))))
     my_bases = sum(int(len(b)) - int((b == 10).sum()) for b in samples.values())
-    log(f"[rank {rank}] C5: {len(mine)} samples, {my_bases / 1e9:.2f} Gbases ({time.time() - t:.1f}s)")
     dev = {}
     for s_, b in samples.items():
         d = okm.DeviceBuffer(len(b), device)
         d.upload(b)
         dev[s_] = (d, len(b))
+    del samples
     sample_ctx = okm.KmerCounter(k, "set", device)
     locals_ = [okm.KmerCounter(k, "set", device), okm.KmerCounter(k, "set", device)]
     owners = [okm.KmerCounter(k, "set", device), okm.KmerCounter(k, "set", device)]
@@ -404,12 +353,6 @@ def wl_c5_dist(args):
         sample_ctx.add_device_batch(d.address, n)
         tot += sample_ctx.count()
     store = okm.DeviceBuffer(max(8, 8 * tot), device)
-
-    def as_tensor(ptr, n):
-        if n == 0:
-            return torch.empty(0, dtype=torch.int64, device="cuda")
-        t_ = torch.as_tensor(okm_dist.DeviceView(ptr, n), device="cuda")
-        return t_ if backend == "nccl" else t_.cpu()
 
     def step():
         sizes = {}
@@ -421,73 +364,114 @@ def wl_c5_dist(args):
             sample_ctx.fetch_into_device(store.address + 8 * off, 0, m)
             sizes[s_] = (off, m)
             off += m
-        tabs = []
         for h in (0, 1):
             u = locals_[h]
             u.reset()
             for s_, (o, m) in sizes.items():
                 if (s_ < 32) == (h == 0) and m:
                     u.add_sorted_pairs_device(store.address + 8 * o, 0, m)
-            n = u.count()
-            tabs.append(as_tensor(u.result_device()[0], n))
-        torch.cuda.synchronize()
-        which = [0]
+            u.count()
+        return okm.distributed_compare(comm, locals_[0], locals_[1], owners[0], owners[1])
 
-        def union(rk, rs):
-            o_ = owners[which[0]]
-            which[0] += 1
-            if backend != "nccl":
-                rk = rk.cuda()
-            o_.reset()
-            pos = 0
-            for sz in rs:
-                if sz:
-                    o_.add_sorted_pairs_device(rk.data_ptr() + 8 * pos, 0, sz)
-                pos += sz
-            n = o_.count()
-            keep.append(rk)  # borrowed until count(); kept alive for the step
-            return n, o_.result_device()[0]
-
-        def intersect(ha, na, hb, nb):
-            return okm.set_intersection_size_device(ha, na, hb, nb, device) if na and nb else 0
-
-        keep = []
-        return okm_dist.distributed_compare(tabs[0], tabs[1], k, union, intersect)
-
-    def barrier_sync():
-        torch.cuda.synchronize()
-        tdist.barrier()
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    barrier_sync()
+    if gate:
+        gate.wait()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         res = step()
-    barrier_sync()
-    dt = (time.perf_counter() - t0) / args.steps
-    tt = torch.tensor([dt, float(my_bases), float(tot)], dtype=torch.float64,
-                      device="cuda" if backend == "nccl" else "cpu")
-    mx = tt.clone()
-    tdist.all_reduce(mx, op=tdist.ReduceOp.MAX)
-    tdist.all_reduce(tt, op=tdist.ReduceOp.SUM)
-    dt = float(mx[0])
-    bases, set_total = int(tt[1]), int(tt[2])
+    for c in [sample_ctx] + locals_ + owners:
+        c.synchronize()
+    if gate:
+        gate.wait()
+    dt = (time.perf_counter() - t0) / steps
+    ta, tb = comm.last_bytes()
+    for c in [sample_ctx] + locals_ + owners:
+        c.close()
+    store.free()
+    for d, _ in dev.values():
+        d.free()
+    return {"dt": dt, "bases": my_bases, "sets": tot, "res": res, "bytes_sent": ta}
+
+
+def wl_c5_dist(args):
+    """C5 over N ranks through the library's exchange (okm_merge_owned_n).
+    Under torchrun: one process per GPU, RCCL communicator (torch gloo only
+    hands out its id and takes the max time).  --loopback P: P virtual ranks in
+    this process on one GPU (okm_comm_init_loopback) -- the same code path at
+    P = 8 on a one-GPU box; its time is all ranks sharing one device, a
+    rehearsal, not a scaling number.  Strong scaling: the 64-sample workload
+    is fixed."""
+    if args.loopback:
+        import threading
+        P = args.loopback
+        comms = okm.Comm.init_loopback(P, 0)
+        gate = threading.Barrier(P)
+        out, err = [None] * P, []
+
+        def body(r):
+            try:
+                out[r] = _c5_rank(r, P, comms[r], 0, args, args.steps, args.warmup, gate)
+            except BaseException as e:  # surfaced below
+                err.append(e)
+                gate.abort()
+
+        th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(P)]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        for c in comms:
+            c.close()
+        if err:
+            raise err[0]
+        world, impl = P, f"okm_merge_owned_n over a loopback communicator ({P} virtual ranks on one MI355X)"
+        dt = max(o["dt"] for o in out)
+        bases = sum(o["bases"] for o in out)
+        set_total = sum(o["sets"] for o in out)
+        sent = sum(o["bytes_sent"] for o in out)
+        res = out[0]["res"]
+        assert all(o["res"] == res for o in out)
+        n_gpus = 1
+    else:
+        import torch
+        import torch.distributed as tdist
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ["RANK"])
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        device = local % max(1, torch.cuda.device_count())
+        tdist.init_process_group("gloo")
+        uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
+        tdist.broadcast(uid, 0)
+        comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
+        tdist.barrier()
+        o = _c5_rank(rank, world, comm, device, args, args.steps, args.warmup)
+        comm.close()
+        tt = torch.tensor([o["dt"], float(o["bases"]), float(o["sets"]), float(o["bytes_sent"])], dtype=torch.float64)
+        mx = tt.clone()
+        tdist.all_reduce(mx, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.SUM)
+        tdist.destroy_process_group()
+        if rank != 0:
+            return None
+        dt, bases, set_total, sent = float(mx[0]), int(tt[1]), int(tt[2]), int(tt[3])
+        res = o["res"]
+        impl, n_gpus = "okm_merge_owned_n over RCCL (one rank per GPU)", world
     na, nb, inter = res
     union_ = na + nb - inter
-    tdist.destroy_process_group()
-    if rank != 0:
-        return None
     return {"metric": f"bases/sec built into per-sample k-mer sets + compared (k=31, build.rs + compare.rs) "
-                      f"on {world} MI355X",
-            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": world, "steps": args.steps,
+                      f"over {world} ranks",
+            "value": round(bases / dt, 1), "unit": "bases/s", "n_gpus": n_gpus, "ranks": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "dtype": "u64",
             "data": "synthetic (64 samples shaped by tools/c5_runs.json, device-resident)",
             "config": {"workload": f"BASELINE configs[4] shape over {world} ranks: 64 WGS-shaped samples "
                                    f"(<= {args.c5_cap / 1e6:.0f} Mbases each) dealt round-robin, DB1 = samples "
-                                   f"0-31, DB2 = 32-63, unions owner-partitioned ({backend})",
-                       "k": k, "bases": bases, "set_sizes_total": set_total,
+                                   f"0-31, DB2 = 32-63, unions owner-partitioned",
+                       "k": 31, "bases": bases, "set_sizes_total": set_total, "exchange": impl,
+                       "bytes_sent_all_ranks": sent,
                        "db1_total_unique_kmers_across_references": na,
                        "db2_total_unique_kmers_across_references": nb, "intersection_size": inter,
                        "union_size": union_, "jaccard_index": inter / union_ if union_ else 0.0}}
@@ -539,8 +523,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gbases", type=float, default=1.0)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="c5: P virtual ranks on one GPU through okm_comm_init_loopback (the distributed compare)")
     args = ap.parse_args()
-    c5 = wl_c5_dist if int(os.environ.get("WORLD_SIZE", "1")) > 1 else wl_c5
+    c5 = wl_c5_dist if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.loopback else wl_c5
     out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify,
            "c5": c5}[args.workload](args)
     if out is not None:
