@@ -209,6 +209,19 @@ struct DevPool {
         auto it = size_.find(const_cast<void *>(p));
         return it == size_.end() ? 0 : it->second;
     }
+    // OKM_POOL_DUMP=1 (tuning): every block, its size and whether it is cached
+    void dump(const char *tag) {
+        std::lock_guard<std::mutex> g(mu);
+        size_t c = 0;
+        for (auto &f : free_) c += f.first;
+        fprintf(stderr, "[okm pool %s] %zu blocks, held %.2f GB, cached %.2f GB:", tag, size_.size(), held / 1e9, c / 1e9);
+        for (auto &kv : size_) {
+            bool cached_blk = false;
+            for (auto &f : free_) cached_blk |= f.second == kv.first;
+            fprintf(stderr, " %.3f%s", kv.second / 1e9, cached_blk ? "c" : "");
+        }
+        fprintf(stderr, "\n");
+    }
     size_t cached() {
         std::lock_guard<std::mutex> g(mu);
         size_t b = 0;
@@ -1148,10 +1161,14 @@ struct ResDst {
 };
 
 // Count the items in LDS (okm_count.hip), then gather their sorted runs into
-// the dense result table.  The table is first sized by the instance bound
-// (in_total), so the distinct total is read back once, at the end; when that
-// much memory is not to be had, the count is read first and the table sized
-// exactly.  Releases level_bufs, d_items and d_segs.
+// the dense result table.  One host sync sits between the two: it reads the
+// distinct total (and the guard words), so the table is allocated at its exact
+// size -- after the level arrays went back to the pool, whose blocks it then
+// reuses (the count's working set: level + staged keys + u32 staged counts;
+// an instance-bound table would hold 16 B per instance instead of per
+// distinct key, 3.6x more at C2).  Into a caller's table (dst: key-range
+// groups) the compaction is launched with the count, before the sync.
+// Releases level_bufs, d_items and d_segs.
 // guard (a speculative launch over round-0 items, make_items' flags): the
 // kernels return at once when guard[0] or guard[1] is set; then *aborted is
 // set, hguard[0..2] receives the flags, and the caller keeps level_bufs,
@@ -1163,8 +1180,10 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr) {
     uint64_t *sk, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
+    // staged counts: u64 for weighted launches, u32 otherwise (okm_count.hip store_count)
+    const uint64_t sc_words = weighted ? std::max<uint64_t>(out_total, 1) : (std::max<uint64_t>(out_total, 1) + 1) / 2;
     OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
+    OKM_TRY(pool_get(c->pool, sc_words, &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
@@ -1173,6 +1192,11 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     auto release_own = [&]() {
         for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer})
             c->pool.put(p);
+    };
+    auto release_level = [&]() {
+        for (void *p : level_bufs) c->pool.put(p);
+        level_bufs.clear();
+        c->pool.put(d_segs);
     };
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     // items past a device-side count (d_nitems) must scan as empty
@@ -1186,34 +1210,20 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
     HIP_TRY(hipGetLastError());
-    // one-pass: the result table sized by the instance bound
-    const uint64_t bound = std::max<uint64_t>(in_total, 1);
-    uint64_t *rk = nullptr, *rc = nullptr;
-    bool one_pass;
     if (dst) {  // a key-range group: straight into the caller's table (sized by the instance bound)
-        rk = dst->keys + dst->off * c->kw;
-        rc = dst->counts + dst->off;
-        one_pass = true;
-    } else {
-        one_pass = c->pool.get(bound * 8 * c->kw, (void **)&rk) == OKM_OK;
-        if (one_pass && c->pool.get(bound * 8, (void **)&rc) != OKM_OK) {
-            c->pool.put(rk);
-            one_pass = false;
-        }
-        if (!one_pass) (void)hipGetLastError();  // the exact-size path below
-    }
-    if (one_pass) {
         c->timer.begin(c->stream);
-        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, rk, rc, c->wide, !weighted, guard,
-                             c->flag, d_nitems);
+        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, dst->keys + dst->off * c->kw,
+                             dst->counts + dst->off, c->wide, !weighted, guard, c->flag, d_nitems);
         c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
         HIP_TRY(hipGetLastError());
     }
-    unsigned long long *hv = c->hres + kHresCount;  // [0] distinct, [1] error word, [2..4] guard words
+    // [0] distinct, [1] error word, [2..4] guard words, [5] items kept (d_nitems)
+    unsigned long long *hv = c->hres + kHresCount;
     HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     if (guard)
         HIP_TRY(hipMemcpyAsync(&hv[2], guard, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    if (d_nitems) HIP_TRY(hipMemcpyAsync(&hv[5], d_nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     c->hprof.mark("count+scan+sync");
     if (guard) {
@@ -1221,49 +1231,36 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         *aborted = (hv[2] | hv[3]) != 0;
         if (*aborted) {
             release_own();
-            if (one_pass && !dst) {
-                c->pool.put(rk);
-                c->pool.put(rc);
-            }
             return OKM_OK;
         }
     }
     if (hv[1]) {  // give every buffer of the step back before failing (long-lived contexts)
         release_own();
-        if (one_pass && !dst) {
-            c->pool.put(rk);
-            c->pool.put(rc);
-        }
-        for (void *p : level_bufs) c->pool.put(p);
-        level_bufs.clear();
-        c->pool.put(d_segs);
+        release_level();
         c->pool.put(d_items);
         return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     }
     const uint64_t nd = hv[0];
+    const uint32_t nkept = d_nitems ? (uint32_t)std::min<unsigned long long>(nitems, hv[5]) : nitems;
     const double staged = 8.0 * c->kw + (weighted ? 8.0 : 4.0);  // per distinct key: staged (key, count)
     const double dense = 8.0 * c->kw + 8.0;                      // ... and its dense result entry
     if (!c->timer.stats.empty()) {
         c->timer.stats[c->timer.id_of("count_items")].alg_bytes += staged * (double)nd;
-        if (one_pass) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
+        if (dst) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
     }
-    if (dst) {
-        OKM_TRY(sync(c));  // the caller reuses this group's buffers for the next
-    } else if (one_pass) {
-        c->res_keys = rk;
-        c->res_counts = rc;
-    } else {
+    // nothing is in flight: the level arrays (and the item flags the kernels
+    // read) are dead, and their blocks may hold the result
+    release_level();
+    if (!dst) {
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         c->timer.begin(c->stream);
-        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, c->res_keys, c->res_counts,
-                             c->wide, !weighted, nullptr, nullptr, d_nitems);
+        launch_compact_items(c->stream, d_items, nkept, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide,
+                             !weighted, nullptr, nullptr, nullptr);
         c->timer.end(c->stream, "compact_items", (staged + dense) * (double)nd);
         HIP_TRY(hipGetLastError());
-        OKM_TRY(sync(c));
     }
-    for (void *p : level_bufs) c->pool.put(p);
-    c->pool.put(d_segs);
+    OKM_TRY(sync(c));  // the result is complete (and a group's buffers may serve the next group)
     c->pool.put(d_items);
     release_own();
     c->n_res = nd;
@@ -1946,9 +1943,13 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
                                 const CountPlan &cp) {
     uint64_t total = 0;
     for (const Part &p : parts) total += p.len;
-    // per instance: level + fan-out copy + staged keys (+ slack) + staged counts (+ weights of both levels)
-    const double ws_key = 8.0 * c->kw * 4 + 8.0 + (weighted ? 16.0 : 0.0);
+    // per instance: level + fan-out copy + staged keys (+ slack) + staged counts
+    // (u32 unweighted) (+ weights of both levels)
+    const double ws_key = 8.0 * c->kw * 4 + (weighted ? 8.0 : 4.0) + (weighted ? 16.0 : 0.0);
     const double res_key = 8.0 * c->kw + 8.0;     // result entry (instance bound)
+    // one group: the exact result is allocated after the level arrays went
+    // back to the pool, beside the staged runs only (count_and_compact)
+    const double one_key = std::max(ws_key, 8.0 * c->kw + (weighted ? 8.0 : 4.0) + res_key);
     // 3/4 of what is free: sampled capacities, line padding and the pool's size
     // classes make a pass hold more than its keys
     const double room = device_room(c);
@@ -1960,7 +1961,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     if (ge && atoll(ge) > 0) {
         group_keys = (uint64_t)atoll(ge);
         mode = (gm && gm[0] == 'B') ? 2 : 1;
-    } else if ((double)total * (ws_key + res_key) > avail) {
+    } else if ((double)total * one_key > avail) {
         // beside a bound-sized table: the 3/4 margin over both (room_a), or —
         // the last resort below, when per-group tables could not be joined —
         // over the groups' working sets only (room_l: the table's size is exact)
@@ -2238,6 +2239,11 @@ okm_status okm_reset(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(sync(c));
+    static const bool dump = [] {
+        const char *e = getenv("OKM_POOL_DUMP");
+        return e && *e && *e != '0';
+    }();
+    if (dump) c->pool.dump("reset");
     invalidate_result(c);
     for (auto &r : c->runs) {
         if (r.borrowed) continue;
