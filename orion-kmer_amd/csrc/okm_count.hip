@@ -57,10 +57,14 @@ __shared__ unsigned long long g_prof_last;
         }                                                               \
     } while (0)
 
-constexpr int kCB = 512;                  // threads per workgroup
+#ifndef OKM_COUNT_CB  // threads per counting workgroup (512: 4096-instance items; 256: 2048)
+#define OKM_COUNT_CB 512
+#endif
+constexpr int kCB = OKM_COUNT_CB;         // threads per workgroup
+static_assert(kCB == 512 || kCB == 256, "four homes per thread at 2048 / 1024 homes");
 constexpr int kPer = 8;                   // instances per thread (tag / full modes)
 constexpr int kCapI = kCB * kPer;         // instances per tag/full-mode item (4096)
-constexpr int kHomeBits = 11;
+constexpr int kHomeBits = kCB == 512 ? 11 : 10;
 constexpr int kHomes = 1 << kHomeBits;    // 2048 homes
 constexpr int kHomesPer = kHomes / kCB;   // homes owned by one thread (4)
 constexpr int kDenseBits = kHomeBits;     // dense mode: rem_bits <= this
@@ -81,7 +85,7 @@ template <bool W> struct Lds {
     static constexpr int kFixed = kLt + kPairBytes;
     static constexpr int kRestEntry = W ? 17 : 9;        // key (+ weight) + first flag
     static constexpr int kFullBytes = kCapI * 8 * (W ? 2 : 1) + kPairBytes;  // full mode: keys (+w) + counters
-    static constexpr int kBytes = W ? kFixed + 2048 * kRestEntry : 40896;
+    static constexpr int kBytes = W ? kFixed + 2048 * kRestEntry : 40896 / (512 / kCB);
     static constexpr int kRest = ((kBytes - kFixed) / kRestEntry) & ~15;
     static constexpr int kRestIters = (kRest + kCB - 1) / kCB;
     static_assert(kFullBytes <= kBytes, "full mode must fit the carve-up");

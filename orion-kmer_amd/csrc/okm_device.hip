@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
                                                     const uint64_t *__restrict__ lc, DevItem *__restrict__ items,
                                                     DevSeg *__restrict__ segs, uint64_t item_max,
                                                     uint32_t capbits, ull *__restrict__ flags, uint32_t kw,
-                                                    FanOut fan) {
+                                                    FanOut fan, const ull *__restrict__ doff) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nout) return;
     // parent = last part whose first output bin is <= i
@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     }
     const uint32_t rem = parents[lo].rem;
     const ull o = offs[i], len = (ends ? ends[i] : offs[i + 1]) - o;
+    const ull so = doff ? doff[i] : o;  // staged output slot: dense, or the level's own range
     const uint32_t F = 1u << fan.bits;  // item slots per child (in key order)
     uint32_t b = 0;                     // this child's own fan-out
     if (len > item_max && rem > capbits) {
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
         DevItem it;
         it.seg_begin = i * F + j;
         it.seg_count = 1;
-        it.out_off = o;  // distinct <= instances: the bin's own range is a safe output slot
+        it.out_off = so;  // distinct <= instances: the child's own range is a safe output slot
         it.rem_bits = rem;
         it.pad = j == 0 ? 0u : kItemEmpty;
         it.total = s.len;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
         // larger ones from the back (flags[4]): each fan-out kernel variant
         // walks only its own
         const ull jb = len <= kFanSmallJob ? atomicAdd(&flags[3], 1ull) : nout - 1 - atomicAdd(&flags[4], 1ull);
-        fan.jobs[jb] = DevFanJob{o, len, i * F, b, rem, 0};
+        fan.jobs[jb] = DevFanJob{o, len, i * F, b, rem, 0, so};
     } else {
         atomicMax(&flags[2], len);
     }
@@ -140,10 +141,22 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
 
 void launch_make_items(void *stream, const ull *offs, const ull *ends, uint32_t nout, const DevParent *parents,
                        uint32_t nparents, const uint64_t *lk, const uint64_t *lc, DevItem *items, DevSeg *segs,
-                       uint64_t item_max, uint32_t capbits, ull *flags, uint32_t kw, const FanOut &fan) {
+                       uint64_t item_max, uint32_t capbits, ull *flags, uint32_t kw, const FanOut &fan,
+                       const ull *doff) {
     if (!nout) return;
     hipLaunchKernelGGL(k_make_items, dim3((nout + 255) / 256), dim3(256), 0, (hipStream_t)stream, offs, ends, nout,
-                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw, fan);
+                       parents, nparents, lk, lc, items, segs, item_max, capbits, flags, kw, fan, doff);
+}
+
+__global__ __launch_bounds__(256) void k_child_lens(const ull *__restrict__ offs, const ull *__restrict__ ends,
+                                                    uint32_t nout, ull *__restrict__ lens) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i <= nout) lens[i] = i < nout ? (ends ? ends[i] : offs[i + 1]) - offs[i] : 0ull;
+}
+
+void launch_child_offsets(void *stream, const ull *offs, const ull *ends, uint32_t nout, ull *doff, ull *tmp) {
+    hipLaunchKernelGGL(k_child_lens, dim3(nout / 256 + 1), dim3(256), 0, (hipStream_t)stream, offs, ends, nout, doff);
+    launch_exclusive_scan(stream, doff, doff, (uint64_t)nout + 1, tmp);
 }
 
 // Fan-out split of one oversized child per job: its keys (<= 64 Ki) are
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
         if (t < nb) {  // thread q: bin q's item, and every wave's start in bin q
             uint32_t a = 0;
             for (uint32_t q = 0; q < t; ++q) a += btot[q];
-            const ull o = jb.off + a, len = btot[t];
+            const ull o = jb.off + a, len = btot[t], so = jb.doff + a;
             uint32_t w0 = a;
             for (int w = 0; w < kWaves; ++w) {
                 const uint32_t c = wtot[w][t];
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
             DevItem it;
             it.seg_begin = jb.item0 + t;
             it.seg_count = 1;
-            it.out_off = o;
+            it.out_off = so;
             it.rem_bits = jb.rem - jb.bits;
             it.pad = len ? 0u : kItemEmpty;
             it.total = len;
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
         if (t < nb) {  // thread q: bin q's item, and every wave's start in bin q
             uint32_t a = 0;
             for (uint32_t q = 0; q < t; ++q) a += btot[q];
-            const ull o = jb.off + a, n = btot[t];
+            const ull o = jb.off + a, n = btot[t], so = jb.doff + a;
             uint32_t w0 = a;
             for (int w = 0; w < kWaves; ++w) {
                 const uint32_t c = wtot[w][t];
@@ -345,7 +358,7 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
             DevItem it;
             it.seg_begin = jb.item0 + t;
             it.seg_count = 1;
-            it.out_off = o;
+            it.out_off = so;
             it.rem_bits = jb.rem - jb.bits;
             it.pad = n ? 0u : kItemEmpty;
             it.total = n;

@@ -243,10 +243,104 @@ __global__ void k_apply_escapes(const uint64_t *__restrict__ esc, uint64_t nesc,
     counts[roff[s] + esc[2 * j]] = esc[2 * j + 1];
 }
 
-// dst[i] += src[i] (the loopback all-reduce)
+// dst[i] += src[i] (the loopback all-reduce; delta decoding)
 __global__ void k_add_u64(ull *__restrict__ dst, const ull *__restrict__ src, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[i] += src[i];
+}
+
+// Keys on the wire as 5-byte deltas.  Every destination slice of the sorted
+// table is ascending, so a key travels as its difference to the slice's
+// previous key (the slice's first key: to 0): the low 40 bits in 5 bytes, and
+// a difference of 2^40 or more (every slice's first key, rare gaps) also as a
+// key escape (position in the destination's run, difference >> 40).  The
+// receiver widens the 5-byte stream, adds the escapes' high parts and
+// prefix-sums each slice (okm_merge_owned step 3).  A table of ~1.4 G keys
+// over the 2^61 canonical k=31 keys has gaps of ~2^31: 6 B per pair with the
+// count byte instead of 9.  kDeltaPer keys per thread: 40 bytes = five
+// 8-byte words (5 * 8 keys is 8-byte aligned).
+constexpr int kDeltaPer = 8;
+constexpr uint64_t kDeltaBlock = 256 * kDeltaPer;
+constexpr uint64_t kLow40 = (uint64_t(1) << 40) - 1;
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_pack_deltas(const uint64_t *__restrict__ keys, uint64_t n,
+                                                     const ull *__restrict__ cut, uint32_t P, uint8_t *__restrict__ out5,
+                                                     ull *__restrict__ esc_cnt, ull *__restrict__ esc_cur,
+                                                     uint64_t *__restrict__ esc, uint64_t skip0, uint64_t skip1) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * kDeltaBlock;
+    if (b0 >= skip0 && b0 + kDeltaBlock <= skip1) return;  // block-uniform: the borrowed self slice
+    const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kDeltaPer;
+    if (i0 >= n) return;
+    uint32_t d = dest_of(cut, P, i0);
+    uint64_t prev = i0 ? keys[i0 - 1] : 0ull;
+    uint64_t w[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kDeltaPer; ++j) {
+        const uint64_t i = i0 + j;
+        if (i < n) {
+            while (i >= cut[d + 1]) ++d;  // empty slices are skipped; i < n = cut[P]
+            const uint64_t k = keys[i];
+            const uint64_t delta = k - (i == cut[d] ? 0ull : prev);
+            prev = k;
+            if (i < skip0 || i >= skip1) {
+                if (delta >> 40) {
+                    if (WRITE) {
+                        const ull sidx = atomicAdd(&esc_cur[d], 1ull);
+                        esc[2 * sidx] = i - cut[d];
+                        esc[2 * sidx + 1] = delta >> 40;
+                    } else {
+                        atomicAdd(&esc_cnt[d], 1ull);
+                    }
+                }
+                const uint64_t lo = delta & kLow40;
+                const int bit = 40 * j, wi = bit >> 6, sh = bit & 63;  // compile-time
+                w[wi] |= lo << sh;
+                if (sh > 24) w[wi + 1] |= lo >> (64 - sh);
+            }
+        }
+    }
+    if (WRITE) return;  // the bytes are written by the counting pass
+    if (i0 + kDeltaPer <= n) {
+        uint64_t *o = reinterpret_cast<uint64_t *>(out5 + 5 * i0);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = w[q];
+    } else {
+        const uint64_t nb = 5 * (n - i0);
+        for (uint64_t b = 0; b < nb; ++b) out5[5 * i0 + b] = (uint8_t)(w[b >> 3] >> (8 * (b & 7)));
+    }
+}
+
+// 5-byte stream -> u64 deltas (the low 40 bits; escapes add the rest)
+__global__ __launch_bounds__(256) void k_widen_deltas(const uint8_t *__restrict__ in5, uint64_t n,
+                                                      uint64_t *__restrict__ out) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kDeltaPer;
+    if (i0 >= n) return;
+    uint64_t w[5] = {0, 0, 0, 0, 0};
+    if (i0 + kDeltaPer <= n) {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(in5 + 5 * i0);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) w[q] = p[q];
+    } else {
+        const uint64_t nb = 5 * (n - i0);
+        for (uint64_t b = 0; b < nb; ++b) w[b >> 3] |= (uint64_t)in5[5 * i0 + b] << (8 * (b & 7));
+    }
+#pragma unroll
+    for (int j = 0; j < kDeltaPer; ++j) {
+        const int bit = 40 * j, wi = bit >> 6, sh = bit & 63;
+        uint64_t v = w[wi] >> sh;
+        if (sh > 24) v |= w[wi + 1] << (64 - sh);
+        if (i0 + j < n) out[i0 + j] = v & kLow40;
+    }
+}
+
+// Key escapes received from rank s sit at esc[2 * reoff[s] ..]: deltas[roff[s] + pos] += high << 40.
+__global__ void k_apply_key_escapes(const uint64_t *__restrict__ esc, uint64_t nesc, const ull *__restrict__ reoff,
+                                    const ull *__restrict__ roff, uint32_t P, uint64_t *__restrict__ deltas) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nesc) return;
+    const uint32_t s = dest_of(reoff, P, j);
+    deltas[roff[s] + esc[2 * j]] += esc[2 * j + 1] << 40;
 }
 
 // ---------------------------------------------------------------------------
@@ -494,6 +588,7 @@ struct okm_comm {
     bool broken = false;  // aborted after a failure inside a collective
     hipStream_t stream = nullptr;
     DevBuf starts, hist, hsum, cut, sizes, gsizes, low, esc_cnt, esc_cur, esc, rk, rlow, rc, resc, offs, flag;
+    DevBuf k5, kesc, kesc_cur, rk5, rkesc, stmp;  // keys as 5-byte deltas (+ key escapes, scan scratch)
     ull *hpin = nullptr;  // pinned landing area for the small readbacks
     size_t hpin_cap = 0;
     double last_ms[4] = {0, 0, 0, 0};  // plan, exchange, unpack, merge (host wall, last okm_merge_owned)
@@ -549,7 +644,18 @@ struct Table {
 // summed, then over ranks; the owner split balances the sum, so equal keys of
 // different tables meet on one rank.  Returns with every rank agreeing on
 // success: the word nb of the all-reduce carries "this rank failed".
-okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32_t shift, std::vector<uint32_t> &bounds) {
+// Keys as 5-byte deltas on the wire (OKM_WIRE_DELTAS=1 / 0; default: with 2
+// to 4 ranks, where one to three xGMI links per GPU bound the exchange and
+// 9 -> 6 B per pair pays for the receiver's decode passes; with 8 ranks and
+// seven links per GPU the decode costs about what the bytes save).
+bool want_deltas(uint32_t P) {
+    const char *e = getenv("OKM_WIRE_DELTAS");
+    if (e && *e) return *e != '0';
+    return P > 1 && P <= 4;
+}
+
+okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32_t shift, std::vector<uint32_t> &bounds,
+                      bool *deltas) {
     const uint32_t P = (uint32_t)m->size;
     const size_t nt = tabs.size();
     hipStream_t s = m->stream;
@@ -558,24 +664,28 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     {
         okm_status a = OKM_OK;
         for (auto [b, bytes] : {std::pair<DevBuf *, size_t>{&m->starts, nt * (nb + 1) * sizeof(ull)},
-                                {&m->hist, (nb + 1) * sizeof(ull)},
-                                {&m->hsum, (nb + 1) * sizeof(ull)},
+                                {&m->hist, (nb + 2) * sizeof(ull)},
+                                {&m->hsum, (nb + 2) * sizeof(ull)},
                                 {&m->cut, (P + 1) * sizeof(ull)},
-                                {&m->sizes, (2 * P + 1) * sizeof(ull)},
-                                {&m->gsizes, (2 * (size_t)P + 1) * P * sizeof(ull)},
+                                {&m->sizes, (3 * P + 1) * sizeof(ull)},
+                                {&m->gsizes, (3 * (size_t)P + 1) * P * sizeof(ull)},
                                 {&m->esc_cnt, P * sizeof(ull)},
                                 {&m->esc_cur, (P + 1) * sizeof(ull)},
-                                {&m->offs, 2 * (P + 1) * sizeof(ull)},
+                                {&m->kesc_cur, (P + 1) * sizeof(ull)},
+                                {&m->offs, 4 * (P + 1) * sizeof(ull)},
                                 {&m->flag, 2 * sizeof(ull)}})
             if (a == OKM_OK) a = b->ensure(bytes);
-        if (a == OKM_OK) a = ensure_hpin(m, (nt + 1) * (nb + 1) + (2 * (size_t)P + 1) * P + 64);
+        if (a == OKM_OK) a = ensure_hpin(m, (nt + 1) * (nb + 2) + (3 * (size_t)P + 1) * P + 64);
         if (a != OKM_OK) return broke(m, a);
     }
-    const ull one = 1;  // host source of an async copy: lives until the sync below
+    // host sources of async copies: live until the sync below
+    const ull one = 1;
+    const ull wd = want_deltas(P) ? 1 : 0;
     okm_status st = OKM_OK;
     for (size_t i = 0; i < nt && st == OKM_OK; ++i)  // counts the local shards if needed (synchronous)
         st = okm_result_device(tabs[i].local, &tabs[i].dk, &tabs[i].dc, &tabs[i].n);
     HIP_TRY(hipMemsetAsync(m->hist.p, 0, (nb + 1) * sizeof(ull), s));
+    HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb + 1, &wd, sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->starts.p, 0, nt * (nb + 1) * sizeof(ull), s));
     if (st == OKM_OK) {
         for (size_t i = 0; i < nt; ++i) {
@@ -589,24 +699,27 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
         HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb, &one, sizeof(ull), hipMemcpyHostToDevice, s));
     }
     {
-        okm_status c = m->tp->all_reduce_sum(m->hist.as<ull>(), m->hsum.as<ull>(), nb + 1, s);
+        okm_status c = m->tp->all_reduce_sum(m->hist.as<ull>(), m->hsum.as<ull>(), nb + 2, s);
         if (c != OKM_OK) return broke(m, c);
     }
-    ull *h_sum = m->hpin, *h_starts = m->hpin + nb + 1;
-    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
+    ull *h_sum = m->hpin, *h_starts = m->hpin + nb + 2;
+    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, (nb + 2) * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_starts, m->starts.p, nt * (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (st != OKM_OK) return st;
     if (h_sum[nb]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed before the exchange");
+    if (h_sum[nb + 1] != 0 && h_sum[nb + 1] != P)
+        return fail(OKM_E_COMM, "okm_merge_owned: ranks disagree on the key wire format (OKM_WIRE_DELTAS)");
+    *deltas = h_sum[nb + 1] == P;
     for (size_t i = 0; i < nt; ++i) tabs[i].starts.assign(h_starts + i * (nb + 1), h_starts + (i + 1) * (nb + 1));
-    bounds.assign(P + 1, 0);
+    bounds.assign(P + 1, 0);  // (h_starts stays valid: tabs[i].starts copied above)
     owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());
     return OKM_OK;
 }
 
 // Steps 3-4 for one table under agreed bounds: sizes, escapes, the grouped
 // exchange, then the owner's count of the received slices.
-okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bounds, uint32_t nb,
+okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bounds, uint32_t nb, bool deltas,
                           uint64_t *n_owned, double *ms3, uint64_t *bytes2) {
     const auto t0 = std::chrono::steady_clock::now();
     okm_ctx *local = t.local, *owner = t.owner;
@@ -618,15 +731,16 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     const uint64_t n = t.n;
     // host sources of async copies live until the stream is synchronised
     ull bad = 0;
-    std::vector<ull> esc_offs(2 * (P + 1));
+    std::vector<ull> esc_offs(4 * (P + 1));
     std::vector<ull> cut(P + 1);
     for (uint32_t r = 0; r <= P; ++r) cut[r] = bounds[r] >= nb ? n : t.starts[bounds[r]];
     cut[0] = 0;
     cut[P] = n;
 
-    // 3. sizes (and escape counts) of every pair of ranks; word 2P = status
+    // 3. sizes, count escapes and key escapes of every pair of ranks; word 3P = status
     HIP_TRY(hipMemcpyAsync(m->cut.p, cut.data(), (P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
-    std::vector<ull> hs(2 * P + 1, 0);
+    const size_t row = 3 * (size_t)P + 1;
+    std::vector<ull> hs(row, 0);
     for (uint32_t r = 0; r < P; ++r) hs[r] = cut[r + 1] - cut[r];
     // This rank's own slice never crosses the transport when the owner is
     // another context: the owner borrows it straight from the local table (it
@@ -635,60 +749,88 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     const bool self_borrow = owner != local;
     const uint64_t skip0 = self_borrow ? cut[me] : 0, skip1 = self_borrow ? cut[me + 1] : 0;
     const uint64_t pblocks = (n + kPackBlock - 1) / kPackBlock;
+    const uint64_t dblocks = (n + kDeltaBlock - 1) / kDeltaBlock;
     okm_status st = OKM_OK;
     if (!set) st = m->low.ensure(std::max<uint64_t>(n, 16));
-    hs[2 * P] = st != OKM_OK;
-    HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), (2 * P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, P * sizeof(ull), s));
+    if (deltas && st == OKM_OK) st = m->k5.ensure(5 * std::max<uint64_t>(n, 16));
+    hs[3 * P] = st != OKM_OK;
+    HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), row * sizeof(ull), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, 2 * P * sizeof(ull), s));
     if (!set && st == OKM_OK && pblocks) {
         hipLaunchKernelGGL(k_pack_counts<false>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
                            m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr, skip0, skip1);
         HIP_TRY(hipGetLastError());
     }
+    if (deltas && st == OKM_OK && dblocks) {
+        hipLaunchKernelGGL(k_pack_deltas<false>, dim3((uint32_t)dblocks), dim3(256), 0, s, dk, n, m->cut.as<ull>(), P,
+                           m->k5.as<uint8_t>(), m->sizes.as<ull>() + 2 * P, nullptr, nullptr, skip0, skip1);
+        HIP_TRY(hipGetLastError());
+    }
     {
-        okm_status c = tp.all_gather(m->sizes.as<ull>(), m->gsizes.as<ull>(), 2 * P + 1, s);
+        okm_status c = tp.all_gather(m->sizes.as<ull>(), m->gsizes.as<ull>(), row, s);
         if (c != OKM_OK) return broke(m, c);
     }
-    const size_t row = 2 * (size_t)P + 1;
     std::vector<ull> h_g(row * P);
     HIP_TRY(hipMemcpyAsync(m->hpin, m->gsizes.p, row * P * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::copy(m->hpin, m->hpin + row * P, h_g.begin());
     if (st != OKM_OK) return st;
     for (uint32_t r = 0; r < P; ++r)
-        if (h_g[(size_t)r * row + 2 * P]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed while sizing");
-    std::vector<ull> ss(P), rs(P), es(P), er(P), roff(P + 1, 0), reoff(P + 1, 0), eoff(P + 1, 0);
+        if (h_g[(size_t)r * row + 3 * P]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed while sizing");
+    // per peer: pairs sent / received, count escapes sent / received, key
+    // escapes sent / received (and their offsets)
+    std::vector<ull> ss(P), rs(P), es(P), er(P), ks(P), kr(P), roff(P + 1, 0), reoff(P + 1, 0), eoff(P + 1, 0),
+        kroff(P + 1, 0), ksoff(P + 1, 0);
     for (uint32_t r = 0; r < P; ++r) {
         ss[r] = h_g[(size_t)me * row + r];
         es[r] = h_g[(size_t)me * row + P + r];
+        ks[r] = h_g[(size_t)me * row + 2 * P + r];
         rs[r] = h_g[(size_t)r * row + me];
         er[r] = h_g[(size_t)r * row + P + me];
+        kr[r] = h_g[(size_t)r * row + 2 * P + me];
         roff[r + 1] = roff[r] + rs[r];
         reoff[r + 1] = reoff[r] + er[r];
         eoff[r + 1] = eoff[r] + es[r];
+        kroff[r + 1] = kroff[r] + kr[r];
+        ksoff[r + 1] = ksoff[r] + ks[r];
     }
     const uint64_t self_n = ss[me];
     if (self_borrow) {
-        for (uint32_t r = me + 1; r <= P; ++r) roff[r] -= rs[me], reoff[r] -= er[me];
-        rs[me] = er[me] = 0;
-        ss[me] = es[me] = 0;
+        for (uint32_t r = me + 1; r <= P; ++r) roff[r] -= rs[me], reoff[r] -= er[me], kroff[r] -= kr[me];
+        rs[me] = er[me] = kr[me] = 0;
+        ss[me] = es[me] = ks[me] = 0;
     }
-    const uint64_t nrecv = roff[P], nresc = reoff[P], nesc = eoff[P];
+    const uint64_t nrecv = roff[P], nresc = reoff[P], nesc = eoff[P], nkr = kroff[P], nks = ksoff[P];
 
     // receive buffers and the escapes, then one more status word: a rank that
     // cannot allocate them tells its peers before any send is posted
     st = m->rk.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
     if (!set) {
         if (st == OKM_OK) st = m->rlow.ensure(std::max<uint64_t>(nrecv, 16));
-        if (st == OKM_OK) st = m->rc.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
         if (st == OKM_OK) st = m->resc.ensure(std::max<uint64_t>(2 * nresc, 2) * sizeof(uint64_t));
         if (st == OKM_OK && nesc) st = m->esc.ensure(2 * nesc * sizeof(uint64_t));
+    }
+    // rc: the received counts, and first the deltas' scan (keys decoded before the counts)
+    if (st == OKM_OK && (!set || deltas)) st = m->rc.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
+    uint64_t max_rs = 0;
+    for (uint32_t r = 0; r < P; ++r) max_rs = std::max<uint64_t>(max_rs, rs[r]);
+    if (deltas) {
+        if (st == OKM_OK) st = m->rk5.ensure(5 * std::max<uint64_t>(nrecv, 16));
+        if (st == OKM_OK) st = m->rkesc.ensure(std::max<uint64_t>(2 * nkr, 2) * sizeof(uint64_t));
+        if (st == OKM_OK && nks) st = m->kesc.ensure(2 * nks * sizeof(uint64_t));
+        if (st == OKM_OK) st = m->stmp.ensure(scan_tmp_elems(max_rs + 1) * sizeof(ull));
     }
     if (st == OKM_OK && debug_fail_rank() == (int)me) st = fail(OKM_E_NOMEM, "okm_merge_owned: OKM_DIST_FAIL_RANK test hook");
     if (st == OKM_OK && !set && nesc) {  // escapes grouped by destination
         HIP_TRY(hipMemcpyAsync(m->esc_cur.p, eoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_pack_counts<true>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
                            m->low.as<uint8_t>(), nullptr, m->esc_cur.as<ull>(), m->esc.as<uint64_t>(), skip0, skip1);
+        HIP_TRY(hipGetLastError());
+    }
+    if (st == OKM_OK && deltas && nks) {  // key escapes grouped by destination
+        HIP_TRY(hipMemcpyAsync(m->kesc_cur.p, ksoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_pack_deltas<true>, dim3((uint32_t)dblocks), dim3(256), 0, s, dk, n, m->cut.as<ull>(), P,
+                           m->k5.as<uint8_t>(), nullptr, m->kesc_cur.as<ull>(), m->kesc.as<uint64_t>(), skip0, skip1);
         HIP_TRY(hipGetLastError());
     }
     if (P > 1) {
@@ -723,8 +865,15 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     };
     uint64_t bytes_out = 0, bytes_in = 0;
     for (uint32_t r = 0; r < P; ++r) {
-        add(true, dk + cut[r], ss[r], 8, r);
-        add(false, m->rk.as<uint64_t>() + roff[r], rs[r], 8, r);
+        if (deltas) {  // 5 bytes per key + key escapes
+            add(true, m->k5.as<uint8_t>() + 5 * cut[r], 5 * ss[r], 1, r);
+            add(false, m->rk5.as<uint8_t>() + 5 * roff[r], 5 * rs[r], 1, r);
+            add(true, m->kesc.as<uint64_t>() + 2 * ksoff[r], 2 * ks[r], 8, r);
+            add(false, m->rkesc.as<uint64_t>() + 2 * kroff[r], 2 * kr[r], 8, r);
+        } else {
+            add(true, dk + cut[r], ss[r], 8, r);
+            add(false, m->rk.as<uint64_t>() + roff[r], rs[r], 8, r);
+        }
         if (!set) {
             add(true, m->low.as<uint8_t>() + cut[r], ss[r], 1, r);
             add(false, m->rlow.as<uint8_t>() + roff[r], rs[r], 1, r);
@@ -732,13 +881,25 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
             add(false, m->resc.as<uint64_t>() + 2 * reoff[r], 2 * er[r], 8, r);
         }
         if (r != me) {
-            bytes_out += ss[r] * (set ? 8 : 9) + (set ? 0 : 16 * es[r]);
-            bytes_in += rs[r] * (set ? 8 : 9) + (set ? 0 : 16 * er[r]);
+            const uint64_t kb = deltas ? 5 : 8;
+            bytes_out += ss[r] * (kb + (set ? 0 : 1)) + (set ? 0 : 16 * es[r]) + (deltas ? 16 * ks[r] : 0);
+            bytes_in += rs[r] * (kb + (set ? 0 : 1)) + (set ? 0 : 16 * er[r]) + (deltas ? 16 * kr[r] : 0);
         }
     }
+    // every rank runs the same number of groups: the most pieces of ANY
+    // message between any two ranks (the all-gathered sizes), so the loopback
+    // barriers pair up; an RCCL group with nothing of this rank's in it is empty
     const uint64_t piece = piece_bytes();
     uint64_t npieces = 0;
-    for (const Msg &g : msgs) npieces = std::max<uint64_t>(npieces, (g.count * g.esize + piece - 1) / piece);
+    for (uint32_t a = 0; a < P; ++a)
+        for (uint32_t b = 0; b < P; ++b) {  // a == b too: whether a rank's owner borrows is its own choice
+            const uint64_t pairs = h_g[(size_t)a * row + b], ce = h_g[(size_t)a * row + P + b],
+                           ke = h_g[(size_t)a * row + 2 * P + b];
+            uint64_t big = pairs * (deltas ? 5 : 8);
+            if (!set) big = std::max(big, std::max<uint64_t>(pairs, 16 * ce));
+            if (deltas) big = std::max<uint64_t>(big, 16 * ke);
+            npieces = std::max<uint64_t>(npieces, (big + piece - 1) / piece);
+        }
     std::vector<P2POp> ops;
     for (uint64_t j = 0; j < npieces; ++j) {
         ops.clear();
@@ -748,6 +909,28 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
         }
         okm_status c = tp.exchange(ops, s);
         if (c != OKM_OK) return broke(m, c);
+    }
+    if (deltas && nrecv) {
+        // keys: 40-bit deltas widened, escapes' high parts added, then every
+        // source rank's slice prefix-summed (exclusive scan into rc, rk += rc)
+        const uint64_t db = (nrecv + kDeltaBlock - 1) / kDeltaBlock;
+        hipLaunchKernelGGL(k_widen_deltas, dim3((uint32_t)db), dim3(256), 0, s, m->rk5.as<uint8_t>(), nrecv,
+                           m->rk.as<uint64_t>());
+        if (nkr) {
+            std::copy(kroff.begin(), kroff.end(), esc_offs.begin() + 2 * (P + 1));
+            std::copy(roff.begin(), roff.end(), esc_offs.begin() + 3 * (P + 1));
+            HIP_TRY(hipMemcpyAsync(m->offs.as<ull>() + 2 * (P + 1), esc_offs.data() + 2 * (P + 1),
+                                   2 * (P + 1) * sizeof(ull), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_apply_key_escapes, dim3((uint32_t)((nkr + 255) / 256)), dim3(256), 0, s,
+                               m->rkesc.as<uint64_t>(), nkr, m->offs.as<ull>() + 2 * (P + 1),
+                               m->offs.as<ull>() + 3 * (P + 1), P, m->rk.as<uint64_t>());
+        }
+        for (uint32_t r = 0; r < P; ++r)
+            if (rs[r])
+                launch_exclusive_scan(s, m->rk.as<ull>() + roff[r], m->rc.as<ull>() + roff[r], rs[r], m->stmp.as<ull>());
+        hipLaunchKernelGGL(k_add_u64, dim3((uint32_t)((nrecv + 255) / 256)), dim3(256), 0, s, m->rk.as<ull>(),
+                           m->rc.as<ull>(), nrecv);
+        HIP_TRY(hipGetLastError());
     }
     if (!set && nrecv) {
         const uint64_t wb = (nrecv + kPackBlock - 1) / kPackBlock;
@@ -804,11 +987,12 @@ okm_status merge_owned_n(okm_ctx *const *locals, okm_comm *m, okm_ctx *const *ow
         tabs[i].owner = owners[i];
     }
     std::vector<uint32_t> bounds;
-    OKM_TRY(plan_split(m, tabs, nb, shift, bounds));
+    bool deltas = false;
+    OKM_TRY(plan_split(m, tabs, nb, shift, bounds, &deltas));
     double ms3[3] = {ms_since(t0), 0, 0};
     uint64_t bytes2[2] = {0, 0};
     for (int i = 0; i < nt; ++i)
-        OKM_TRY(move_and_merge(m, tabs[i], bounds, nb, n_owned ? n_owned + i : nullptr, ms3, bytes2));
+        OKM_TRY(move_and_merge(m, tabs[i], bounds, nb, deltas, n_owned ? n_owned + i : nullptr, ms3, bytes2));
     m->last_ms[0] = ms3[0];
     m->last_ms[1] = ms3[1];
     m->last_ms[2] = 0;
@@ -911,7 +1095,8 @@ void okm_comm_destroy(okm_comm *m) {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     m->tp.reset();
     for (DevBuf *b : {&m->starts, &m->hist, &m->hsum, &m->cut, &m->sizes, &m->gsizes, &m->low, &m->esc_cnt,
-                      &m->esc_cur, &m->esc, &m->rk, &m->rlow, &m->rc, &m->resc, &m->offs, &m->flag})
+                      &m->esc_cur, &m->esc, &m->rk, &m->rlow, &m->rc, &m->resc, &m->offs, &m->flag, &m->k5, &m->kesc,
+                      &m->kesc_cur, &m->rk5, &m->rkesc, &m->stmp})
         b->release();
     if (m->hpin) (void)hipHostFree(m->hpin);
     if (m->stream) (void)hipStreamDestroy(m->stream);

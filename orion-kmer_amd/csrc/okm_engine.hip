@@ -1825,8 +1825,16 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                     level_bufs.push_back(fan.jobs);
                 }
                 OKM_TRY(h2d(c, d_par, par.data(), par.size() * sizeof(DevParent)));
+                // items stage their runs densely: slots = the pass's keys, not the
+                // level's sampled capacity (~1.5x the keys at C2)
+                unsigned long long *doff, *dtmp;
+                OKM_TRY(pool_get(c->pool, (size_t)L.nout + 1, &doff));
+                OKM_TRY(pool_get(c->pool, scan_tmp_elems(L.nout + 1), &dtmp));
+                level_bufs.push_back(doff);
+                level_bufs.push_back(dtmp);
+                launch_child_offsets(c->stream, L.d_offs, L.d_ends, L.nout, doff, dtmp);
                 launch_make_items(c->stream, L.d_offs, L.d_ends, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc,
-                                  d_items, d_segs, item_max, capbits, flags, c->kw, fan);
+                                  d_items, d_segs, item_max, capbits, flags, c->kw, fan, doff);
                 HIP_TRY(hipGetLastError());
                 if (fan.bits) {  // oversized children split into a second level array (same offsets)
                     uint64_t *fk, *fc = nullptr;
@@ -1858,7 +1866,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 c->info.work_items = nslots;
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
-                OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.padded, L.total, weighted, level_bufs, flags,
+                OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
                                           hf, &aborted, d_nitems, dst));
                 if (!aborted) {
                     c->info.max_partition = hf[2];

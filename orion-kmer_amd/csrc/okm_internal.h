@@ -175,6 +175,7 @@ struct DevParent {
 struct DevFanJob {
     uint64_t off, len;
     uint32_t item0, bits, rem, pad;
+    uint64_t doff;  // the child's first staged output slot (dense: the scan of child lengths)
 };
 struct FanOut {
     uint32_t bits = 0;          // 0: one item per child (no fan-out)
@@ -196,10 +197,18 @@ uint64_t fan_split_max();
 // 16 Ki keys (filed from the front / the back of fan.jobs[nout]).  Count and compact
 // kernels given `guard` (= flags) return at once when guard[0] or guard[1] is
 // set.  With fan.bits, item/segment slot i * 2^bits + j belongs to child i.
+// doff (optional): every child's first staged output slot, the exclusive scan
+// of the child lengths (launch_child_offsets) -- items then stage their
+// (key, count) runs densely (L.total slots) instead of at their level offsets
+// (the level's padded size).
 void launch_make_items(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
                        const DevParent *parents, uint32_t nparents, const uint64_t *lk, const uint64_t *lc,
                        DevItem *items, DevSeg *segs, uint64_t item_max, uint32_t capbits,
-                       unsigned long long *flags, uint32_t kw, const FanOut &fan);
+                       unsigned long long *flags, uint32_t kw, const FanOut &fan,
+                       const unsigned long long *doff = nullptr);
+// doff[b] = sum of the lengths of children < b (b = 0..nout); tmp >= scan_tmp_elems(nout + 1).
+void launch_child_offsets(void *stream, const unsigned long long *offs, const unsigned long long *ends, uint32_t nout,
+                          unsigned long long *doff, unsigned long long *tmp);
 // The fan-out jobs (flags[3] of them, <= max_jobs): keys of [off, off + len)
 // of sk/sc are split into the same range of dk/dc and their sub-items written;
 // oflags[0] += sub-ranges still too big, oflags[2] = max sub-range.

@@ -9,6 +9,7 @@ drained, filtered and sorted once (count.rs:106-119): the owners' ranges in
 rank order must equal the oracle's table of the whole input, exactly.  Sets
 (build.rs:46-58) and the distributed compare (compare.rs:51-66) likewise."""
 
+import os
 import threading
 
 import numpy as np
@@ -18,6 +19,8 @@ import okm
 from oracle import OracleCounter
 
 pytestmark = pytest.mark.gpu
+# a rank that never reaches a collective ends it after a minute, not five
+os.environ.setdefault("OKM_LOOPBACK_TIMEOUT_S", "60")
 
 
 def run_ranks(P, fn):
@@ -314,3 +317,36 @@ def test_loopback_distributed_compare(P):
     for got in res:  # every rank holds the summed sizes
         assert got == (len(A), len(B), inter)
     assert 0 < inter < min(len(A), len(B))
+
+
+@pytest.mark.parametrize("P", [2, 8])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_loopback_wire_formats(monkeypatch, P, sparse):
+    """Keys on the wire as u64 and as 5-byte deltas (OKM_WIRE_DELTAS), with
+    key escapes for gaps >= 2^40: a dense table (gaps ~2^30) and a sparse one
+    (~100 K keys over 2^61: most gaps escape); counts past the byte escape.
+    Both formats give the oracle's table; deltas cut the dense table's bytes
+    on the wire by about a third (9 -> 6 B per pair)."""
+    k = 31
+    recs = _records(1_500 if sparse else 40_000, 2_000_000 if sparse else 300_000, 28 + P,
+                    hot_every=0 if sparse else 35)
+    ek, ec = _oracle(recs, k)
+    sent = {}
+    for deltas in ("1", "0"):
+        monkeypatch.setenv("OKM_WIRE_DELTAS", deltas)
+        res = _merge_case(P, k, _shards(recs, P), "separate")
+        _check_ranges(res, ek, ec)
+        sent[deltas] = sum(r[3][0] for r in res)
+    if not sparse:
+        assert sent["1"] < 0.75 * sent["0"], sent
+
+
+def test_loopback_wire_deltas_multi_piece_set_mode(monkeypatch):
+    """5-byte keys cut into odd-sized pieces (a key straddles two pieces), set mode."""
+    monkeypatch.setenv("OKM_WIRE_DELTAS", "1")
+    monkeypatch.setenv("OKM_RCCL_PIECE", "4104")
+    k, P = 27, 3
+    recs = _records(25_000, 500_000, 29)
+    ek, _ = _oracle(recs, k)
+    res = _merge_case(P, k, _shards(recs, P), "local", mode="set")
+    _check_ranges(res, ek, None, with_counts=False)
