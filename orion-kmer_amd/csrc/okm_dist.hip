@@ -644,14 +644,22 @@ struct Table {
 // summed, then over ranks; the owner split balances the sum, so equal keys of
 // different tables meet on one rank.  Returns with every rank agreeing on
 // success: the word nb of the all-reduce carries "this rank failed".
-// Keys as 5-byte deltas on the wire (OKM_WIRE_DELTAS=1 / 0; default: with 2
-// to 4 ranks, where one to three xGMI links per GPU bound the exchange and
-// 9 -> 6 B per pair pays for the receiver's decode passes; with 8 ranks and
-// seven links per GPU the decode costs about what the bytes save).
-bool want_deltas(uint32_t P) {
+// Keys as 5-byte deltas on the wire: OKM_WIRE_DELTAS=1 / 0 forces either;
+// by default (2) with 2 to 4 ranks, where one to three xGMI links per GPU
+// bound the exchange and 9 -> 6 B per pair pays for the receiver's decode
+// passes (with 8 ranks and seven links per GPU the decode costs about what
+// the bytes save), and only for tables dense enough that gaps of 2^40 and
+// more (16-B key escapes) are rare: a rank's table (the agreed histogram's
+// total / P) leaves a mean gap of at most 2^38 over the 2^(2k-1) canonical
+// keys (an exponential gap passes 2^40 with probability e^-4: +0.3 B a pair).
+int want_deltas(uint32_t P) {
     const char *e = getenv("OKM_WIRE_DELTAS");
-    if (e && *e) return *e != '0';
-    return P > 1 && P <= 4;
+    if (e && *e) return *e != '0' ? 1 : 0;
+    return P > 1 && P <= 4 ? 2 : 0;
+}
+bool dense_enough(uint64_t pairs_per_rank, uint32_t k) {
+    const uint32_t space_bits = 2 * k - 1;  // canonical keys: about half of the 2k-bit values
+    return space_bits <= 38 || (double)pairs_per_rank >= std::ldexp(1.0, (int)space_bits - 38);
 }
 
 okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32_t shift, std::vector<uint32_t> &bounds,
@@ -680,7 +688,7 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     }
     // host sources of async copies: live until the sync below
     const ull one = 1;
-    const ull wd = want_deltas(P) ? 1 : 0;
+    const ull wd = want_deltas(P) ? 1 : 0;  // 1: deltas wanted (forced or auto), agreed below
     okm_status st = OKM_OK;
     for (size_t i = 0; i < nt && st == OKM_OK; ++i)  // counts the local shards if needed (synchronous)
         st = okm_result_device(tabs[i].local, &tabs[i].dk, &tabs[i].dc, &tabs[i].n);
@@ -710,7 +718,10 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     if (h_sum[nb]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed before the exchange");
     if (h_sum[nb + 1] != 0 && h_sum[nb + 1] != P)
         return fail(OKM_E_COMM, "okm_merge_owned: ranks disagree on the key wire format (OKM_WIRE_DELTAS)");
-    *deltas = h_sum[nb + 1] == P;
+    uint64_t pairs = 0;
+    for (uint32_t b = 0; b < nb; ++b) pairs += h_sum[b];
+    // every rank sees the same sums: the same decision everywhere
+    *deltas = h_sum[nb + 1] == P && (want_deltas(P) == 1 || dense_enough(pairs / P, ctx_k(tabs[0].local)));
     for (size_t i = 0; i < nt; ++i) tabs[i].starts.assign(h_starts + i * (nb + 1), h_starts + (i + 1) * (nb + 1));
     bounds.assign(P + 1, 0);  // (h_starts stays valid: tabs[i].starts copied above)
     owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());

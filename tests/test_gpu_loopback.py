@@ -322,23 +322,43 @@ def test_loopback_distributed_compare(P):
 @pytest.mark.parametrize("P", [2, 8])
 @pytest.mark.parametrize("sparse", [False, True])
 def test_loopback_wire_formats(monkeypatch, P, sparse):
-    """Keys on the wire as u64 and as 5-byte deltas (OKM_WIRE_DELTAS), with
-    key escapes for gaps >= 2^40: a dense table (gaps ~2^30) and a sparse one
-    (~100 K keys over 2^61: most gaps escape); counts past the byte escape.
-    Both formats give the oracle's table; deltas cut the dense table's bytes
-    on the wire by about a third (9 -> 6 B per pair)."""
+    """Keys on the wire as u64 and as 5-byte deltas (OKM_WIRE_DELTAS forced),
+    with key escapes for gaps >= 2^40: most gaps of a ~100 K-key table
+    escape; counts past the byte escape.  Both formats give the oracle's
+    table."""
     k = 31
     recs = _records(1_500 if sparse else 40_000, 2_000_000 if sparse else 300_000, 28 + P,
                     hot_every=0 if sparse else 35)
     ek, ec = _oracle(recs, k)
-    sent = {}
     for deltas in ("1", "0"):
         monkeypatch.setenv("OKM_WIRE_DELTAS", deltas)
         res = _merge_case(P, k, _shards(recs, P), "separate")
         _check_ranges(res, ek, ec)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_loopback_wire_deltas_dense_table_bytes(monkeypatch, P):
+    """A table of ~14 M keys (gaps ~2^37 of the 2^61 canonical 31-mers): the
+    default wire format at 2-4 ranks is the 5-byte deltas, and both formats
+    give the same owner ranges.  Measured 7.1 B per pair against 9: keys with
+    first base T are ~1/7 as dense as those with A (canonical skew), so there
+    ~1/3 of the gaps pass 2^40 and escape; a C3 shard table (~1.4 G keys,
+    gaps ~2^31) hardly escapes at all (6 B per pair)."""
+    k = 31
+    recs = _records(1_000_000, 10_000_000, 30)
+    sent, tables = {}, {}
+    for deltas in ("", "0"):
+        if deltas:
+            monkeypatch.setenv("OKM_WIRE_DELTAS", deltas)
+        else:
+            monkeypatch.delenv("OKM_WIRE_DELTAS", raising=False)
+        res = _merge_case(P, k, _shards(recs, P), "separate")
         sent[deltas] = sum(r[3][0] for r in res)
-    if not sparse:
-        assert sent["1"] < 0.75 * sent["0"], sent
+        tables[deltas] = (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
+    assert np.array_equal(tables[""][0], tables["0"][0]) and np.array_equal(tables[""][1], tables["0"][1])
+    assert len(tables["0"][0]) > 10_000_000
+    assert bool((tables["0"][0][1:] > tables["0"][0][:-1]).all())
+    assert sent[""] < 0.82 * sent["0"], sent
 
 
 def test_loopback_wire_deltas_multi_piece_set_mode(monkeypatch):
