@@ -1702,7 +1702,7 @@ static okm_status count_general(okm_ctx *c) {
                                                        // gradients and line padding must still fit)
     bool weighted = false;
     for (auto &r : c->runs) weighted |= (r.counts != nullptr);
-    uint32_t maxb = log2_floor(part_max_bins(weighted));  // bits one pass can split
+    uint32_t maxb = log2_floor(part_max_bins(weighted, c->wide));  // bits one pass can split
     if (const char *e = getenv("OKM_PART_MAXB"))                // tests: force small passes (fan-out, host rounds)
         maxb = std::max(1, std::min((int)maxb, atoi(e)));
     c->hprof.mark("pre_count");
@@ -2196,12 +2196,14 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->nbins = 1u << c->l1_bits;
     c->shift1 = 2u * k - c->l1_bits;
     {
-        // fold threshold: OKM_FOLD_BYTES (tests), else 8 % of the device's memory
-        // (the count of the folded runs needs ~6x their bytes of working set)
+        // fold threshold: OKM_FOLD_BYTES (tests), else 10 % of the device's memory
+        // (the count of the folded runs needs ~4.5x their bytes of working set;
+        // C3 on one GPU: 8 % 596 ms, 10 % 569 ms; 12 % needs key-range groups
+        // and re-maps pool blocks: 2.5 s)
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) (void)hipGetLastError();
         const char *fe = getenv("OKM_FOLD_BYTES");
-        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(0.08 * (double)total_b);
+        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(0.10 * (double)total_b);
     }
     if (create_ctx_stream(device, &c->stream) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||

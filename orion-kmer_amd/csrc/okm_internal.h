@@ -127,7 +127,7 @@ void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_
                             const unsigned long long *cap = nullptr);
 uint32_t extract_tile();
 uint32_t extract_max_bins(bool wide);  // L1 bins: k <= 32 kernels vs k in 33..64
-uint32_t part_max_bins(bool weighted);
+uint32_t part_max_bins(bool weighted, bool wide);
 
 // Exclusive scan of n u64 values (in -> out, out may equal in); tmp >= scan_tmp_elems(n).
 size_t scan_tmp_elems(uint64_t n);

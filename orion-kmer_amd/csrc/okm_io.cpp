@@ -586,9 +586,22 @@ okm_status OutWriter::write(const void *data, size_t n) {
 }
 
 // Blocks in order.  Kind 4 compresses each block into its own gzip member on
-// parallel threads (level 6, flate2's default) and writes the members in
-// order: the concatenation decompresses to the blocks' concatenation
-// (MultiGzDecoder, gzip -d, zcat).
+// parallel threads and writes the members in order: the concatenation
+// decompresses to the blocks' concatenation (MultiGzDecoder, gzip -d, zcat).
+// Level: OKM_GZ_LEVEL, default 1.  flate2's default (6, utils.rs:172) makes
+// a k-mer TSV 5 % smaller (0.274 vs 0.289 of the text) at 4.6x the CPU
+// (libdeflate, one thread: 35.6 vs 163 MB/s), and it bound `count -o x.tsv.gz`:
+// 3.9 of the C2 run's 4.6 s (profiles/r03_e2e_cli.txt).  Parity is on the
+// decompressed bytes.
+static int gz_level() {
+    static const int lvl = [] {
+        const char *e = getenv("OKM_GZ_LEVEL");
+        const int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 12 ? v : 1;
+    }();
+    return lvl;
+}
+
 okm_status OutWriter::write_blocks(const std::vector<std::pair<const uint8_t *, size_t>> &blocks) {
     Impl &I = *p_;
     if (!I.f) return fail(OKM_E_STATE, "writer not open");
@@ -605,7 +618,7 @@ okm_status OutWriter::write_blocks(const std::vector<std::pair<const uint8_t *, 
     std::atomic<int> bad{0};
     const size_t nt = std::min<size_t>(nb, (size_t)host_threads());
     parallel_for(nt, [&](size_t t) {
-        void *c = D->alloc_compressor(6);
+        void *c = D->alloc_compressor(gz_level());
         if (!c) {
             bad = 1;
             return;
@@ -634,7 +647,7 @@ okm_status OutWriter::close() {
     okm_status st = OKM_OK;
     if (I.kind == 4 && !I.wrote) {  // an empty output is still one (empty) gzip member
         Deflate *D = deflate_lib();
-        void *c = D->alloc_compressor(6);
+        void *c = D->alloc_compressor(gz_level());
         Bytes o(c ? D->gzip_compress_bound(c, 0) : 0);
         const size_t m = c ? D->gzip_compress(c, "", 0, o.data(), o.size()) : 0;
         if (c) D->free_compressor(c);

@@ -35,7 +35,17 @@ template <typename KT> struct Line {
     static constexpr int kKeys = 128 / (int)sizeof(KT);  // keys per 128-B line
 };
 
-uint32_t part_max_bins(bool weighted) { return weighted ? 512u : 1024u; }
+// Output bins one pass can split a part into.  u64 unweighted passes take up
+// to 2048 (two bins per scatter thread, 15 Ki-key tiles), so a fold's L1 bin
+// of ~8 M instances splits straight into ~4 Ki-key children -- one item each,
+// with no fan-out pass (k_fan_split) after the partition (OKM_PART_2048=0:
+// 1024, one bin per thread).
+#ifndef OKM_PART_2048
+#define OKM_PART_2048 1
+#endif
+uint32_t part_max_bins(bool weighted, bool wide) {
+    return weighted ? 512u : (!wide && OKM_PART_2048 ? 2048u : 1024u);
+}
 
 template <typename KT>
 __device__ __forceinline__ uint32_t local_bin(const KT &key, const DevSeg &s) {
@@ -213,22 +223,25 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
 // Tile variant: every 64-Ki-key chunk is processed in LDS tiles that are
 // counting-sorted by local bin, and each bin's run leaves as one contiguous
 // stretch of the chunk's exact slice (no padding, no append rounds).
-template <typename KT, bool W> struct Tile {
-    // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state
+template <typename KT, bool W, bool BIG = false> struct Tile {
+    // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state; BIG
+    // (2048 bins: 32 KiB of per-bin state): 120 KiB of staged keys
 #ifndef OKM_PART_TILE_KEYS
 #define OKM_PART_TILE_KEYS 16384
 #endif
-    static constexpr int kKeys = (W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : OKM_PART_TILE_KEYS);
+    static constexpr int kKeys = BIG ? 15 * kPartBlock
+                                     : ((W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : OKM_PART_TILE_KEYS));
     static constexpr int kPer = kKeys / kPartBlock;
 };
 
-template <typename KT, bool W>
+template <typename KT, bool W, bool BIG = false>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
     const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
     uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
     uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts, const ull *__restrict__ cap_end,
     ull *__restrict__ ovf) {
-    constexpr int T = Tile<KT, W>::kKeys, P = Tile<KT, W>::kPer;
+    constexpr int T = Tile<KT, W, BIG>::kKeys, P = Tile<KT, W, BIG>::kPer;
+    constexpr uint32_t BPT = BIG ? 2 : 1;  // bins per thread in the scan / claim phase
     extern __shared__ __attribute__((aligned(16))) ull lds[];
     KT *stage = reinterpret_cast<KT *>(lds);                              // [T]
     ull *cstage = reinterpret_cast<ull *>(stage + T);                     // [T] (W)
@@ -271,16 +284,32 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                 }
             }
             __syncthreads();
-            // tile-local bin offsets (nl <= kPartBlock: one bin per thread)
-            const uint32_t my = t < nl ? hist[t] : 0u;
+            // tile-local bin offsets (nl <= BPT * kPartBlock: thread t owns
+            // bins BPT t .. BPT t + BPT - 1, so the scan runs in bin order)
+            uint32_t my[BPT];
+            uint32_t mine = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < BPT; ++q) {
+                const uint32_t b = BPT * t + q;
+                my[q] = b < nl ? hist[b] : 0u;
+                mine += my[q];
+            }
             // sampled capacities: this tile's claim on its run of each bin is
             // issued now and consumed after the scan and the staging, so the
             // global atomic's round trip overlaps them
-            ull claim = 0;
-            if (!HC && my) claim = atomicAdd(&cursor[s.out_base + t], (ull)my);
+            ull claim[BPT];
+#pragma unroll
+            for (uint32_t q = 0; q < BPT; ++q) {
+                claim[q] = 0;
+                if (!HC && my[q]) claim[q] = atomicAdd(&cursor[s.out_base + BPT * t + q], (ull)my[q]);
+            }
             ull tile_n;
-            const uint32_t off = (uint32_t)block_excl_scan<kPartBlock>(my, wsum, &tile_n);
-            if (t < nl) lofs[t] = off;
+            uint32_t off = (uint32_t)block_excl_scan<kPartBlock>(mine, wsum, &tile_n);
+#pragma unroll
+            for (uint32_t q = 0; q < BPT; ++q) {
+                if (BPT * t + q < nl) lofs[BPT * t + q] = off;
+                off += my[q];
+            }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < P; ++u) {
@@ -290,15 +319,20 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                     if (W) cstage[dst] = ww[u];
                 }
             }
-            if (!HC && t < nl) {
-                ull g = ~0ull;
-                if (my) {
-                    if (claim + my <= cap_end[s.out_base + t])
-                        g = claim;
-                    else
-                        atomicOr(ovf, 1ull);
+            if (!HC) {
+#pragma unroll
+                for (uint32_t q = 0; q < BPT; ++q) {
+                    const uint32_t b = BPT * t + q;
+                    if (b >= nl) continue;
+                    ull g = ~0ull;
+                    if (my[q]) {
+                        if (claim[q] + my[q] <= cap_end[s.out_base + b])
+                            g = claim[q];
+                        else
+                            atomicOr(ovf, 1ull);
+                    }
+                    gcur[b] = g;
                 }
-                gcur[t] = g;
             }
             __syncthreads();
             // each bin's run is contiguous in `stage` and in the output slice
@@ -312,7 +346,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                 if (W) out_counts[o] = cstage[j];
             }
             __syncthreads();
-            if (HC && t < nl) gcur[t] += hist[t];
+            if (HC)
+                for (uint32_t b = t; b < nl; b += kPartBlock) gcur[b] += hist[b];
         }
         __syncthreads();
     }
@@ -358,12 +393,22 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
                 optin = 64 * 1024;
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, optin);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, optin);
             (void)hipGetLastError();
             attr_tile = true;
         }
+        const size_t bin_state = (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
+        if (max_local > (uint32_t)kPartBlock) {  // 2048 bins: u64 unweighted passes only (part_max_bins)
+            constexpr int T = Tile<KT, W, true>::kKeys;
+            const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) + bin_state;
+            hipLaunchKernelGGL((k_part_scatter_tile<KT, W, true>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
+                               (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
+                               cap_end, ovf);
+            return;
+        }
         constexpr int T = Tile<KT, W>::kKeys;
-        const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) +
-                           (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
+        const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) + bin_state;
         hipLaunchKernelGGL((k_part_scatter_tile<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
                            (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
                            cap_end, ovf);

@@ -9,6 +9,7 @@
 #include <cmath>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -29,25 +30,41 @@ struct Genome {
     std::vector<uint8_t> codes;  // one 2-bit code per byte
 };
 
+// The last few genomes, shared: callers on several threads (one per sample,
+// tools/bench_paths.py --loopback) may ask for different genomes at once, and
+// a genome stays alive while any caller still reads it.
 static std::mutex g_mu;
-static Genome g_genome;
+static std::vector<std::shared_ptr<const Genome>> g_genomes;  // most recent last
+constexpr size_t kGenomesKept = 8;
 
-static const Genome &genome(uint64_t seed, uint64_t len) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_genome.seed == seed && g_genome.len == len && !g_genome.codes.empty()) return g_genome;
-    g_genome.seed = seed;
-    g_genome.len = len;
-    g_genome.codes.resize(len);
+static std::shared_ptr<const Genome> genome(uint64_t seed, uint64_t len) {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (size_t i = 0; i < g_genomes.size(); ++i)
+            if (g_genomes[i]->seed == seed && g_genomes[i]->len == len) {
+                auto g = g_genomes[i];
+                g_genomes.erase(g_genomes.begin() + i);
+                g_genomes.push_back(g);
+                return g;
+            }
+    }
+    auto G = std::make_shared<Genome>();
+    G->seed = seed;
+    G->len = len;
+    G->codes.resize(len);
     // 32 bases per splitmix64 draw
     for (uint64_t i = 0; i < len; i += 32) {
         uint64_t r = splitmix64(seed * 0xD1B54A32D192ED03ull + i / 32);
         const uint64_t m = std::min<uint64_t>(32, len - i);
         for (uint64_t j = 0; j < m; ++j) {
-            g_genome.codes[i + j] = (uint8_t)(r & 3);
+            G->codes[i + j] = (uint8_t)(r & 3);
             r >>= 2;
         }
     }
-    return g_genome;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_genomes.push_back(G);
+    if (g_genomes.size() > kGenomesKept) g_genomes.erase(g_genomes.begin());
+    return G;
 }
 
 }  // namespace okm
@@ -58,8 +75,8 @@ extern "C" okm_status okm_synth_reads(uint64_t genome_seed, uint64_t genome_len,
                                       uint64_t n_reads, uint32_t read_len, double sub_rate, double n_rate,
                                       uint8_t *out, int threads) {
     if (!out || read_len == 0 || genome_len < read_len) return fail(OKM_E_ARG, "okm_synth_reads: bad arguments");
-    const Genome &G = genome(genome_seed, genome_len);
-    const uint8_t *g = G.codes.data();
+    const std::shared_ptr<const Genome> G = genome(genome_seed, genome_len);
+    const uint8_t *g = G->codes.data();
     const uint64_t npos = genome_len - read_len + 1;
     // per-base draw: 32-bit uniform u; u < t_sub => substitution, t_sub <= u < t_sub + t_n => N
     const uint64_t t_sub = (uint64_t)(sub_rate * 4294967296.0);
@@ -148,8 +165,8 @@ extern "C" okm_status okm_synth_long_reads(uint64_t genome_seed, uint64_t genome
     if (!out) return OKM_OK;  // lengths only
     uint8_t *buf = (uint8_t *)malloc(std::max<uint64_t>(off[n_reads], 1));
     if (!buf) return fail(OKM_E_NOMEM, "okm_synth_long_reads: host allocation");
-    const Genome &G = genome(genome_seed, genome_len);
-    const uint8_t *g = G.codes.data();
+    const std::shared_ptr<const Genome> G = genome(genome_seed, genome_len);
+    const uint8_t *g = G->codes.data();
     const uint64_t npos = genome_len - 2ull * max_len;  // a read consumes < 2 L source bases
     // per-base draw u (32 bits): [0, t1) substitution, [t1, t2) insertion after
     // the base, [t2, t3) deletion of the base, else the base as it is
