@@ -442,6 +442,17 @@ struct okm_ctx {
     // counted from are gone (borrowed runs are dropped once counted, since
     // their memory belongs to the caller); the next add keeps it as a table
     bool res_is_input = false;
+    // the count in progress is the runs' last use (do_count releases them, a
+    // fold replaces them): its staged keys may go into a run's block (C2: the
+    // L1 run's 3.2 GB, instead of a block of their own)
+    bool may_take_runs = false;
+    bool took_runs = false;    // ... and it did
+    bool input_lost = false;   // a count failed after overwriting a run: only okm_reset recovers
+    // the result goes to the caller (okm_count), not into a kept table: it may
+    // take the dead level array's block (keys, then counts) instead of blocks
+    // of its own (C2: 1.8 GB fewer held; a table kept later is moved by
+    // result_to_folded_run's shrink)
+    bool share_result = false;
     uint64_t *res_keys = nullptr, *res_counts = nullptr;
     uint64_t n_res = 0;
     okm_engine_info info{};
@@ -715,6 +726,7 @@ static okm_status result_to_folded_run(okm_ctx *c, Run *out) {
 // in which case it stays as a folded run that the next count merges with the
 // new input (count.rs:48: one map across every add).
 static okm_status before_add(okm_ctx *c) {
+    if (c->input_lost) return fail(OKM_E_STATE, "a failed count overwrote this context's input: okm_reset it");
     if (!(c->counted && c->res_is_input)) {
         invalidate_result(c);
         return OKM_OK;
@@ -747,7 +759,12 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
     for (auto &r : c->runs) (r.sorted ? keep : batches).push_back(std::move(r));
     c->runs = std::move(batches);
     c->counted = false;
+    const bool outer = !c->may_take_runs, shared = c->share_result;
+    c->may_take_runs = true;  // the batches are released below
+    c->share_result = false;  // ... and the table is kept
     okm_status st = c->runs.empty() ? OKM_OK : count_general(c);
+    if (outer) c->may_take_runs = false;
+    c->share_result = shared;
     Run t;
     if (st == OKM_OK && !c->runs.empty()) st = result_to_folded_run(c, &t);
     release_runs(c, c->runs);
@@ -1169,6 +1186,9 @@ struct ResDst {
 // distinct key, 3.6x more at C2).  Into a caller's table (dst: key-range
 // groups) the compaction is launched with the count, before the sync.
 // Releases level_bufs, d_items and d_segs.
+// last_use: no run is read after this count (its items lie in level arrays,
+// and c->may_take_runs: the runs are released once counted); the staged keys
+// then go into the smallest run block that holds them, when one does.
 // guard (a speculative launch over round-0 items, make_items' flags): the
 // kernels return at once when guard[0] or guard[1] is set; then *aborted is
 // set, hguard[0..2] receives the flags, and the caller keeps level_bufs,
@@ -1177,12 +1197,30 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     uint64_t out_total, uint64_t in_total, bool weighted,
                                     std::vector<void *> &level_bufs, const unsigned long long *guard = nullptr,
                                     unsigned long long *hguard = nullptr, bool *aborted = nullptr,
-                                    const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr) {
-    uint64_t *sk, *sc;
+                                    const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr,
+                                    bool last_use = false) {
+    uint64_t *sk = nullptr, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
     // staged counts: u64 for weighted launches, u32 otherwise (okm_count.hip store_count)
     const uint64_t sc_words = weighted ? std::max<uint64_t>(out_total, 1) : (std::max<uint64_t>(out_total, 1) + 1) / 2;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
+    if (last_use && c->may_take_runs && !dst) {
+        const size_t need = std::max<uint64_t>(out_total, 1) * 8 * c->kw;
+        size_t best = 0;
+        for (auto &r : c->runs) {
+            const size_t b = r.borrowed ? 0 : c->pool.size_of(r.keys);
+            if (b >= need && (!best || b < best)) best = b, sk = r.keys;
+        }
+    }
+    const bool donated = sk != nullptr;
+    // a failure once the count may have written into a run: the input is gone
+    struct Lost {
+        okm_ctx *c;
+        bool on;
+        ~Lost() {
+            if (on) c->input_lost = true;
+        }
+    } lost{c, false};
+    if (!donated) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
     OKM_TRY(pool_get(c->pool, sc_words, &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
@@ -1191,7 +1229,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     OKM_TRY(pool_get(c->pool, nitems, &defer));
     auto release_own = [&]() {
         for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer})
-            c->pool.put(p);
+            if (!(donated && p == (void *)sk)) c->pool.put(p);
     };
     auto release_level = [&]() {
         for (void *p : level_bufs) c->pool.put(p);
@@ -1204,6 +1242,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                            (d_nitems ? nitems + 1 : 1) * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
+    lost.on = donated;
     launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
                        d_nitems);
     c->timer.end(c->stream, "count_items", (8.0 * c->kw + (weighted ? 8.0 : 0.0)) * (double)in_total);
@@ -1229,7 +1268,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     if (guard) {
         for (int i = 0; i < 3; ++i) hguard[i] = hv[2 + i];
         *aborted = (hv[2] | hv[3]) != 0;
-        if (*aborted) {
+        if (*aborted) {  // the kernels returned at once: nothing was written
+            lost.on = false;
             release_own();
             return OKM_OK;
         }
@@ -1250,10 +1290,28 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     }
     // nothing is in flight: the level arrays (and the item flags the kernels
     // read) are dead, and their blocks may hold the result
+    const size_t kpad = (std::max<uint64_t>(nd, 1) * 8 * c->kw + 255) & ~(size_t)255;
+    uint8_t *blk = nullptr;
+    if (!dst && c->share_result) {  // the smallest level block that holds keys and counts
+        size_t best = 0, at = 0;
+        for (size_t i = 0; i < level_bufs.size(); ++i) {
+            const size_t b = c->pool.size_of(level_bufs[i]);
+            if (b >= kpad + std::max<uint64_t>(nd, 1) * 8 && (!best || b < best)) best = b, at = i;
+        }
+        if (best) {
+            blk = static_cast<uint8_t *>(level_bufs[at]);
+            level_bufs.erase(level_bufs.begin() + at);
+        }
+    }
     release_level();
     if (!dst) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        if (blk) {
+            c->res_keys = reinterpret_cast<uint64_t *>(blk);
+            c->res_counts = reinterpret_cast<uint64_t *>(blk + kpad);  // inside the block: the pool ignores it on put
+        } else {
+            OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+            OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        }
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nkept, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide,
                              !weighted, nullptr, nullptr, nullptr);
@@ -1263,6 +1321,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     OKM_TRY(sync(c));  // the result is complete (and a group's buffers may serve the next group)
     c->pool.put(d_items);
     release_own();
+    lost.on = false;
+    c->took_runs |= donated;
     c->n_res = nd;
     c->info.distinct = nd;
     c->counted = true;
@@ -1604,10 +1664,18 @@ static okm_status do_count_runs(okm_ctx *c);
 // returns, so those runs are released and the result stands for the input.
 static okm_status do_count(okm_ctx *c) {
     if (c->counted) return OKM_OK;
-    OKM_TRY(do_count_runs(c));
+    if (c->input_lost) return fail(OKM_E_STATE, "a failed count overwrote this context's input: okm_reset it");
+    // the runs are released once counted, so the count may stage into their blocks
+    const bool outer = !c->may_take_runs;
+    if (outer) c->took_runs = false;
+    c->may_take_runs = true;
+    if (outer) c->share_result = true;
+    const okm_status st = do_count_runs(c);
+    if (outer) c->may_take_runs = c->share_result = false;
+    OKM_TRY(st);
     bool borrowed = false;
     for (auto &r : c->runs) borrowed |= r.borrowed;
-    if (borrowed && c->counted) {
+    if ((borrowed || c->took_runs) && c->counted) {
         release_runs(c, c->runs);
         c->res_is_input = true;
     }
@@ -1866,8 +1934,9 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 c->info.work_items = nslots;
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
+                // every item lies in the level arrays: the runs are not read again
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
-                                          hf, &aborted, d_nitems, dst));
+                                          hf, &aborted, d_nitems, dst, true));
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;
@@ -1997,6 +2066,16 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         group_keys = std::max<uint64_t>(group_keys, 1);
     }
     if (mode == 0 || group_keys >= total) return count_parts(c, segtab, parts, weighted, cp, nullptr);
+    // every group reads the runs: none may hold a group's staged keys
+    struct Keep {
+        okm_ctx *c;
+        bool saved, shared;
+        ~Keep() {
+            c->may_take_runs = saved;
+            c->share_result = shared;
+        }
+    } keep{c, c->may_take_runs, c->share_result};
+    c->may_take_runs = c->share_result = false;
 
     ResDst d{nullptr, nullptr, 0};
     struct Tab {
@@ -2263,6 +2342,7 @@ okm_status okm_reset(okm_ctx *c) {
     c->runs.clear();
     c->info = okm_engine_info{};
     c->folds = 0;
+    c->input_lost = false;
     c->hprof.mark("reset");
     return OKM_OK;
 }

@@ -22,7 +22,7 @@ import okm
 import restate as R
 from conftest import case_file_bytes, materialize
 from okm import _lib
-from oracle import OracleCounter, count_separated_mt
+from oracle import OracleCounter, OracleCounterWide, count_separated_mt
 
 pytestmark = pytest.mark.gpu
 
@@ -380,6 +380,47 @@ def test_full_size_properties():
     thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
     ek, ec = count_separated_mt(batch, k, thr)
     assert np.array_equal(keys, ek) and np.array_equal(counts, ec)
+
+
+@pytest.mark.parametrize("k", [31, 45])
+def test_count_add_count(k):
+    # okm_count stages its sorted runs in the L1 run's block and releases the
+    # runs (the result then stands for the input): counting again, adding
+    # after a count, and host batches beside device batches all still equal
+    # one count of everything added
+    thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+    sep = np.frombuffer(b"\n", np.uint8)
+    parts = [okm.synth_reads(n, 150, genome_len=2_000_000, genome_seed=7, seed=30 + i, first_read=i * 10 ** 6,
+                             sub_rate=0.01) for i, n in enumerate((120_000, 90_000, 60_000))]
+    with okm.KmerCounter(k, wide=k > 32) as ctr:
+        seen = []
+        for i, b in enumerate(parts):
+            if i == 1:  # a host batch: records and their offsets
+                cut = np.flatnonzero(b == sep[0])
+                starts = np.concatenate([[0], cut + 1])
+                ends_ = np.concatenate([cut, [len(b)]])
+                keep = ends_ > starts
+                data = np.concatenate([b[s_:e_] for s_, e_ in zip(starts[keep], ends_[keep])])
+                offs = np.concatenate([[0], np.cumsum(ends_[keep] - starts[keep])]).astype(np.uint64)
+                ctr.add_batch(data, offs)
+            else:
+                buf = okm.DeviceBuffer(len(b))
+                buf.upload(b)
+                ctr.add_device_batch(buf.address, len(b))
+                buf.free()
+            seen.append(b)
+            n = ctr.count()
+            assert ctr.count() == n  # counting again changes nothing
+            keys, counts = ctr.result(1)
+            joined = np.concatenate([x for b_ in seen for x in (b_, sep)])
+            if k <= 32:
+                ek, ec = count_separated_mt(joined, k, thr)
+            else:
+                oc = OracleCounterWide(k)
+                oc.add_separated(joined)
+                ek, ec = oc.result(1)
+            assert np.array_equal(keys, ek) and np.array_equal(counts, ec), f"after batch {i}"
+            assert n == len(ek)
 
 
 def _upload(arr):
