@@ -41,6 +41,9 @@ namespace okm {
 #ifndef OKM_COUNT_PROF
 #define OKM_COUNT_PROF 0
 #endif
+#ifndef OKM_COUNT_DESC_PF  // tag kernel: load the next item's descriptor while this item is counted
+#define OKM_COUNT_DESC_PF 0
+#endif
 #ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
 #define OKM_FULL_RANK 1
 #endif
@@ -692,9 +695,12 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     if (OKM_COUNT_PROF && t == 0) g_prof_last = clock64();
     // Block-uniform values that steer code containing barriers come from
     // blockIdx / scalar loads (see DESIGN.md on the structuriser).
+    DevItem nxt{};
+    if (OKM_COUNT_DESC_PF && blockIdx.x < nitems) nxt = items[blockIdx.x];
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         PMARK(0);
-        const DevItem it = items[item];
+        const DevItem it = OKM_COUNT_DESC_PF ? nxt : items[item];
+        if (OKM_COUNT_DESC_PF && item + gridDim.x < nitems) nxt = items[item + gridDim.x];
         const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
         if (total == 0) {  // an empty fan-out slot (block-uniform)
             if (t == 0) n_out[item] = 0;

@@ -27,6 +27,9 @@ constexpr int kPartBlock = OKM_PART_BLOCK;  // threads per workgroup (scatter: L
 constexpr int kLoadU = OKM_PART_LOADU;  // keys per thread in flight per scatter batch
 constexpr int kHistU = 4;      // 16-B loads per thread in flight (histogram)
 
+#ifndef OKM_PART_COPY_BINS  // tile copy-out by bin (one wave per bin's run) when runs average >= 48 keys
+#define OKM_PART_COPY_BINS 0
+#endif
 #ifndef OKM_PART_TILE
 #define OKM_PART_TILE 1  // 1: LDS tile counting sort (exact runs, no padding); 0: per-bin line buffers
 #endif
@@ -336,6 +339,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
             }
             __syncthreads();
             // each bin's run is contiguous in `stage` and in the output slice
+            if (OKM_PART_COPY_BINS && (uint32_t)tile_n >= 48u * nl) {  // long runs: one wave per bin, no lookups
+                const uint32_t lane = t & 63u;
+                for (uint32_t b = t >> 6; b < nl; b += kPartBlock / 64) {
+                    const ull g = gcur[b];
+                    if (g == ~0ull) continue;
+                    const uint32_t lo = lofs[b], n = hist[b];
+                    for (uint32_t q = lane; q < n; q += 64) {
+                        out_keys[g + q] = stage[lo + q];
+                        if (W) out_counts[g + q] = cstage[lo + q];
+                    }
+                }
+            } else
             for (uint32_t j = t; j < (uint32_t)tile_n; j += kPartBlock) {
                 const KT key = stage[j];
                 const uint32_t b = local_bin(key, s);
