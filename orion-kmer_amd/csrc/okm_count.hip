@@ -122,7 +122,7 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_scan32(v);
     if (lane == 63) wsum[wid] = inc;
-    __syncthreads();
+    lds_sync();
     uint32_t wbase = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kCB / 64; ++w) {
@@ -130,7 +130,7 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
         wbase += w < wid ? s : 0u;
         tot += s;
     }
-    __syncthreads();
+    lds_sync();
     *total = tot;
     return wbase + inc - v;
 }
@@ -220,12 +220,12 @@ __device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *
         cc[t] = s.counts;
         coff[t + 1] = (uint32_t)s.len;
     }
-    __syncthreads();
+    lds_sync();
     if (t == 0) {
         coff[0] = 0;
         for (uint32_t r = 0; r < R; ++r) coff[r + 1] += coff[r];
     }
-    __syncthreads();
+    lds_sync();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         kk[u] = KeyOps<KT>::empty();
@@ -265,10 +265,10 @@ __device__ __forceinline__ void slice_sort(KT *sk, ull *sw, uint32_t a, uint32_t
 template <bool W>
 __device__ __forceinline__ void tag_reset(ull *lds) {
     uint32_t *p = reinterpret_cast<uint32_t *>(lds);
-    __syncthreads();
+    lds_sync();
     for (int j = threadIdx.x; j < kHomes; j += kCB) lds[j] = kEmptyKey;
     for (int j = kTagBytes / 4 + threadIdx.x; j < Lds<W>::kFixed / 4; j += kCB) p[j] = 0;
-    __syncthreads();
+    lds_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -288,10 +288,10 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     ull *sw = reinterpret_cast<ull *>(sk + kCapI);
     uint32_t *hc = reinterpret_cast<uint32_t *>(sw + (W ? kCapI : 0));
     uint16_t *first = reinterpret_cast<uint16_t *>(hc + kHomes / 2);  // [D + 1]: run starts in sk
-    __syncthreads();  // the previous item's LDS state is dead
+    lds_sync();  // the previous item's LDS state is dead
     hc[2 * t] = 0;
     hc[2 * t + 1] = 0;
-    __syncthreads();
+    lds_sync();
     uint32_t hp[kPer];  // home << 16 | pos
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -303,7 +303,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             hp[u] = (h << 16) | half_of(o, h);
         }
     }
-    __syncthreads();
+    lds_sync();
     const uint32_t w0 = hc[2 * t], w1 = hc[2 * t + 1];
     const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
     const uint32_t n = c0 + c1 + c2 + (w1 >> 16);
@@ -311,7 +311,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     const uint32_t a = block_excl_scan32(n, wsum, &ntot);
     hc[2 * t] = a | ((a + c0) << 16);
     hc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
-    __syncthreads();
+    lds_sync();
     PMARK(11);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -323,7 +323,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             if (W) sw[dst] = ww[u];
         }
     }
-    __syncthreads();
+    lds_sync();
     PMARK(12);
     uint32_t m = 0;  // run-start flags of positions p0 .. p0 + 7 (p0 = 8t)
     constexpr int kPerT = kCapI / kCB;  // 8 positions per thread
@@ -352,7 +352,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
                 dst[u] = rank;
             }
         }
-        __syncthreads();  // every read of the home-ordered keys is done
+        lds_sync();  // every read of the home-ordered keys is done
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             if ((uint32_t)u >= nrows) break;
@@ -361,7 +361,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
                 if (W) sw[dst[u]] = ww[u];
             }
         }
-        __syncthreads();
+        lds_sync();
         PMARK(13);
         // count.rs:33: a key's count = its run's length (weight); flag run starts
         KT prev = p0 > 0 && p0 <= ntot ? sk[p0 - 1] : KeyOps<KT>::empty();
@@ -388,7 +388,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
                 prev = x;
             }
         }
-        __syncthreads();
+        lds_sync();
         const uint32_t *rw = reinterpret_cast<const uint32_t *>(rf);
         const uint64_t fw = (uint64_t)rw[2 * t] | ((uint64_t)rw[2 * t + 1] << 32);
 #pragma unroll
@@ -402,7 +402,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             if (m & (1u << j)) first[q++] = (uint16_t)(p0 + j);
         if (t == 0) first[D] = (uint16_t)ntot;  // ntot <= kCapI fits u16
     }
-    __syncthreads();
+    lds_sync();
     PMARK(14);
     for (uint32_t p = t; p < (nowrite ? 0u : D); p += kCB) {
         const uint32_t b = first[p], e = first[p + 1];
@@ -465,7 +465,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             }
         }
     }
-    __syncthreads();
+    lds_sync();
     PMARK(2);
     // 2. rest offsets: thread t owns homes [4t, 4t+4) = words 2t, 2t+1
     {
@@ -481,7 +481,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         rc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
         if (t == 0) wsum[kCB / 64] = rtot;  // rest total, read by every rest position below
     }
-    __syncthreads();
+    lds_sync();
     PMARK(3);
     // 3. scatter rest instances into home order
 #pragma unroll
@@ -494,7 +494,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             if (W) rw[dst] = ww[u];
         }
     }
-    __syncthreads();
+    lds_sync();
     PMARK(4);
     // 4. rest positions, one per lane: count, first occurrence in the home's
     //    run, and what the home's distinct count / tag rank must include
@@ -529,7 +529,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             }
         }
     }
-    __syncthreads();
+    lds_sync();
     PMARK(5);
     // 5. output offsets per home: [tag] + rest distinct keys
     ull tg[kHomesPer];
@@ -552,7 +552,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         hd[2 * t] = ho[0] | (ho[1] << 16);
         hd[2 * t + 1] = ho[2] | (ho[3] << 16);
     }
-    __syncthreads();
+    lds_sync();
     PMARK(6);
     // 6a. tags: rank = home offset + rest distinct keys below the tag
     {
@@ -592,7 +592,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     }
     PMARK(7);
     // reset this thread's homes for the next item once every reader is done
-    __syncthreads();
+    lds_sync();
 #pragma unroll
     for (int q = 0; q < kHomesPer; ++q) {
         tag[kHomesPer * t + q] = kEmptyKey;
@@ -605,7 +605,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     rc[2 * t] = rc[2 * t + 1] = 0;
     hd[2 * t] = hd[2 * t + 1] = 0;
     lt[2 * t] = lt[2 * t + 1] = 0;
-    __syncthreads();
+    lds_sync();
     return __builtin_amdgcn_readfirstlane(D);
 }
 
@@ -625,9 +625,9 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
     KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
     KT *slot_key = reinterpret_cast<KT *>(lds);               // [kHomes]
     CT *cnt = reinterpret_cast<CT *>(slot_key + kHomes);      // [kHomes]
-    __syncthreads();  // the previous item's LDS state is dead
+    lds_sync();  // the previous item's LDS state is dead
     for (uint32_t j = t; j < nslots; j += kCB) cnt[j] = 0;
-    __syncthreads();
+    lds_sync();
     for (uint32_t sg = 0; sg < it.seg_count; ++sg) {
         const DevSeg s = segs[it.seg_begin + sg];
         const KT *keys = reinterpret_cast<const KT *>(s.keys);
@@ -650,7 +650,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
             }
         }
     }
-    __syncthreads();
+    lds_sync();
     uint32_t d = 0;
     for (uint32_t q = 0; q < kHomesPer; ++q) {
         const uint32_t j = t * kHomesPer + q;
@@ -813,7 +813,7 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
         }
         if (threadIdx.x == 0) n_out[item] = written;
-        __syncthreads();  // LDS reuse by the next item
+        lds_sync();  // LDS reuse by the next item
     }
 }
 

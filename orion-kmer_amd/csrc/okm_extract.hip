@@ -42,6 +42,12 @@ __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
 #ifndef OKM_EXTRACT_WPE  // scatter: waves per SIMD the register budget must allow
 #define OKM_EXTRACT_WPE 4
 #endif
+#ifndef OKM_EXTRACT_EXPT  // timing experiments only (tools/extract_only.py): 1 no HBM writes, 2 no staging
+#define OKM_EXTRACT_EXPT 0
+#endif
+#ifndef OKM_EXTRACT_PF_LATE  // scatter: issue that load after the tile's claim, not before it
+#define OKM_EXTRACT_PF_LATE 0
+#endif
 #ifndef OKM_EXTRACT_PREFETCH  // scatter: load the next tile's bytes during this tile
 #define OKM_EXTRACT_PREFETCH 1
 #endif
@@ -71,7 +77,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
                                                                 uint32_t *__restrict__ HC, ull *__restrict__ Hg) {
     __shared__ uint32_t lh[kMaxL1Bins + 1];  // + dummy bin for invalid windows
     for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
-    __syncthreads();
+    lds_sync();
     const uint64_t beg = (uint64_t)blockIdx.x * g.stride * g.chunk;  // stride > 1: a sample of the chunks
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift, nb = g.nbins;
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
                 atomicAdd(&lh[valid ? bin_of(key, shift) : nb], 1u);
             });
     }
-    __syncthreads();
+    lds_sync();
     for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
         const uint32_t h = lh[b];
         if (HC) HC[(uint64_t)blockIdx.x * nb + b] = h;
@@ -146,45 +152,50 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
     const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
-    WinWords<kSegS> ww;  // this tile's bytes, loaded one tile ahead
-    if (OKM_EXTRACT_PREFETCH && beg + (uint64_t)t * kSegS < end)
-        load_windows<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
+    WinWords<kSegS> ww;  // this tile's bytes, loaded one tile ahead (branch-free: load_windows_clamped)
+    if (OKM_EXTRACT_PREFETCH) load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
         for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
-        __syncthreads();
+        lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
         const bool live = w0 < end;
         uint32_t tile_n;
         {  // one sweep: keys and their within-bin ranks stay in registers
             ull kk[kSegS];
-            uint32_t rk[kSegS];  // bin << 16 | rank; invalid: nb << 16
+            uint32_t rk[kSegS / 2];  // two within-bin ranks (< 2^15) per word; the bin is recomputed
+            uint32_t vm = 0;         // valid windows
 #pragma unroll
-            for (int j = 0; j < kSegS; ++j) rk[j] = nb << 16;
-            if (!OKM_EXTRACT_PREFETCH && live) load_windows<kSegS>(seq, g.n, w0, ww);
+            for (int j = 0; j < kSegS / 2; ++j) rk[j] = 0;
+            if (!OKM_EXTRACT_PREFETCH && live) load_windows_clamped<kSegS>(seq, g.n, w0, ww);
             if (live)
-                scan_words<kSegS, K>(ww, g.k, [&](int j, uint64_t key, bool valid) {
-                    const uint32_t b = valid ? bin_of(key, shift) : nb;
-                    kk[j] = key;
-                    rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
-                });
-            if (OKM_EXTRACT_PREFETCH && w0 + kTile < end)  // next tile, in flight meanwhile
-                load_windows<kSegS>(seq, g.n, w0 + kTile, ww);
-            __syncthreads();
+                scan_words<kSegS, K>(
+                    ww, g.k,
+                    [&](int j, uint64_t key, bool valid) {
+                        const uint32_t b = valid ? bin_of(key, shift) : nb;
+                        kk[j] = key;
+                        rk[j >> 1] |= atomicAdd(&hist[b], 1u) << (16 * (j & 1));
+                        vm |= valid ? 1u << j : 0u;
+                    },
+                    g.n - w0);
+            // next tile, in flight meanwhile; unconditional (a clamped load past the
+            // end is harmless), so the loaded registers need no merge copies
+            if (OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE) load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
+            lds_sync();
             tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
             // sampled capacities: issue this tile's claim now, consume it after the staging
             uint32_t ch = 0;
-            ull cp = 0;
+            ull cp;
             if (!HC && t < nb) {
                 ch = hist[t];
-                if (ch) cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);
+                cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);  // + 0 when empty: no branch
             }
-            __syncthreads();
+            lds_sync();
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) {
-                const uint32_t b = rk[j] >> 16;
-                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTile + (t & 63u);
-                stage[dst] = kk[j];
+                const uint32_t rank = (rk[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t dst = (vm >> j) & 1u ? lofs[bin_of(kk[j], shift)] + rank : (uint32_t)kTile + (t & 63u);
+                if (OKM_EXTRACT_EXPT != 2 || kk[j] == 0x123456789ull) stage[dst] = kk[j];
             }
             if (!HC && t < nb) {
                 const bool fits = ch && cp + ch <= capb;
@@ -192,15 +203,18 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                 gcur[t] = fits ? cp : ~0ull;
             }
         }
-        __syncthreads();
+        // late prefetch: after the claim's returning atomic was consumed (vmcnt
+        // retires in order, so waiting for the claim waits for any load before it)
+        if (OKM_EXTRACT_PREFETCH && OKM_EXTRACT_PF_LATE) load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
+        lds_sync();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
-        for (uint32_t j = t; j < tile_n; j += kScatBlock) {
+        for (uint32_t j = t; j < (OKM_EXTRACT_EXPT == 2 ? 0u : tile_n); j += kScatBlock) {
             const ull key = stage[j];
             const uint32_t b = bin_of(key, shift);
             const ull gb = gcur[b];
-            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
+            if (gb != ~0ull && (OKM_EXTRACT_EXPT != 1 || key == 0x123456789ull)) out[gb + (j - lofs[b])] = key;
         }
-        __syncthreads();
+        lds_sync();
         if (HC && t < nb) gcur[t] += hist[t];
     }
 }
@@ -255,7 +269,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8
                                                                      ull *__restrict__ Hg) {
     __shared__ uint32_t lh[kMaxL1BinsW + 1];
     for (uint32_t b = threadIdx.x; b <= g.nbins; b += kExtractBlock) lh[b] = 0;
-    __syncthreads();
+    lds_sync();
     const uint64_t beg = (uint64_t)blockIdx.x * g.stride * g.chunk;  // stride > 1: a sample of the chunks
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift, nb = g.nbins;
@@ -266,7 +280,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8
                 atomicAdd(&lh[valid ? bin_of_wide(key, shift) : nb], 1u);
             });
     }
-    __syncthreads();
+    lds_sync();
     for (uint32_t b = threadIdx.x; b < nb; b += kExtractBlock) {
         const uint32_t h = lh[b];
         if (HC) HC[(uint64_t)blockIdx.x * nb + b] = h;
@@ -301,29 +315,29 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
     const uint32_t shift = g.shift;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
         if (t <= nb) hist[t] = 0;
-        __syncthreads();
+        lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
         const bool live = w0 < end;
         if (live)
             scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
                 atomicAdd(&hist[valid ? bin_of_wide(key, shift) : nb], 1u);
             });
-        __syncthreads();
+        lds_sync();
         const uint32_t tile_n = tile_offsets<kExtractBlock>(t, nb, hist, lofs, lcur, wsum);
         if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
-        __syncthreads();
+        lds_sync();
         if (live)
             scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
                 if (valid) stage[atomicAdd(&lcur[bin_of_wide(key, shift)], 1u)] = key;
             });
-        __syncthreads();
+        lds_sync();
         for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
             const K128 key = stage[j];
             const uint32_t b = bin_of_wide(key, shift);
             const ull gb = gcur[b];
             if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
-        __syncthreads();
+        lds_sync();
         if (HC && t < nb) gcur[t] += hist[t];
     }
 }
@@ -366,7 +380,7 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW1) {
         if (t <= nb) hist[t] = 0;
-        __syncthreads();
+        lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
         const bool live = w0 < end;
         uint32_t tile_n;
@@ -388,15 +402,15 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
                 }
             }
             if (w0 + kTileW1 < end) load_windows<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);  // next tile, in flight
-            __syncthreads();
+            lds_sync();
             tile_n = tile_offsets<kScatBlockW>(t, nb, hist, lofs, lcur, wsum);
             uint32_t ch = 0;
-            ull cp = 0;
+            ull cp;
             if (!HC && t < nb) {
                 ch = hist[t];
-                if (ch) cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);
+                cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);  // + 0 when empty: no branch
             }
-            __syncthreads();
+            lds_sync();
 #pragma unroll
             for (int j = 0; j < kSegW; ++j) {
                 const uint32_t b = rk[j] >> 16;
@@ -409,14 +423,14 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
                 gcur[t] = fits ? cp : ~0ull;
             }
         }
-        __syncthreads();
+        lds_sync();
         for (uint32_t j = t; j < tile_n; j += kScatBlockW) {
             const K128 key = stage[j];
             const uint32_t b = bin_of_wide(key, shift);
             const ull gb = gcur[b];
             if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
-        __syncthreads();
+        lds_sync();
         if (HC && t < nb) gcur[t] += hist[t];
     }
 }
@@ -505,7 +519,7 @@ __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs,
         cap[t] = ((ull)c + align - 1) / align * align;
     }
     const uint32_t t = threadIdx.x;
-    __syncthreads();
+    lds_sync();
     if (t == 0) {
         ull o = 0;
         for (uint32_t b = 0; b < nb; ++b) {

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
         const DevChunk ch = chunks[c];
         const DevSeg s = segs[ch.seg];
         for (uint32_t b = threadIdx.x; b < s.nlocal; b += kPartBlock) lh[b] = 0;
-        __syncthreads();
+        lds_sync();
         const KT *keys = reinterpret_cast<const KT *>(s.keys) + ch.begin;
         if (sizeof(KT) == 8 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0) {  // block-uniform: 2 keys / 16 B
             const uint4 *k4 = reinterpret_cast<const uint4 *>(keys);
@@ -113,13 +113,13 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
                 for (int u = 0; u < kHistU; ++u) hist_key(v[u], s, lh);
             }
         }
-        __syncthreads();
+        lds_sync();
         for (uint32_t b = threadIdx.x; b < s.nlocal; b += kPartBlock) {
             const uint32_t h = lh[b];
             if (HC) HC[(uint64_t)c * max_local + b] = h;
             if (h) atomicAdd(&Hg[s.out_base + b], pad_line<KT>(h));
         }
-        __syncthreads();
+        lds_sync();
     }
 }
 
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
         const uint64_t *cnts = s.counts ? s.counts + ch.begin : nullptr;
         for (uint64_t base = 0; base < ch.len; base += T) {
             for (uint32_t b = t; b < nl; b += kPartBlock) hist[b] = 0;
-            __syncthreads();
+            lds_sync();
             KT kk[P];
             ull ww[P];
             uint32_t br[P];  // bin << 16 | rank; ~0 = empty
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                     br[u] = (b << 16) | atomicAdd(&hist[b], 1u);
                 }
             }
-            __syncthreads();
+            lds_sync();
             // tile-local bin offsets (nl <= BPT * kPartBlock: thread t owns
             // bins BPT t .. BPT t + BPT - 1, so the scan runs in bin order)
             uint32_t my[BPT];
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                 if (BPT * t + q < nl) lofs[BPT * t + q] = off;
                 off += my[q];
             }
-            __syncthreads();
+            lds_sync();
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 if (br[u] != ~0u) {
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                     gcur[b] = g;
                 }
             }
-            __syncthreads();
+            lds_sync();
             // each bin's run is contiguous in `stage` and in the output slice
             if (OKM_PART_COPY_BINS && (uint32_t)tile_n >= 48u * nl) {  // long runs: one wave per bin, no lookups
                 const uint32_t lane = t & 63u;
@@ -360,11 +360,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
                 out_keys[o] = key;
                 if (W) out_counts[o] = cstage[j];
             }
-            __syncthreads();
+            lds_sync();
             if (HC)
                 for (uint32_t b = t; b < nl; b += kPartBlock) gcur[b] += hist[b];
         }
-        __syncthreads();
+        lds_sync();
     }
 }
 

@@ -45,6 +45,33 @@ __device__ __forceinline__ void load_windows(const uint8_t *__restrict__ seq, ui
     }
 }
 
+// The same bytes without a data-dependent branch (the tail-safe byte loop of
+// load_windows sits on a path the wait-count pass must join, and it then
+// waits for every load in flight, the next tile's prefetch included): each
+// 16-B granule is loaded from min(its address, the batch's last granule) --
+// a 16-B aligned granule that starts inside the batch never leaves the
+// allocation -- and bytes at or past n are marked invalid afterwards
+// (mark_tail), so their contents never matter.  seq is 16-B aligned and
+// w0 % 16 == 0; any w0 is safe (past the end: the last granule, again).
+template <int SEG, int HALO>
+__device__ __forceinline__ void load_windows_clamped(const uint8_t *__restrict__ seq, uint64_t n, uint64_t w0,
+                                                     WinWords<SEG, HALO> &ww) {
+    constexpr int LOAD = WinWords<SEG, HALO>::kLoad;
+    const uint64_t lastg = (n - 1) >> 4, g0 = w0 >> 4;  // n >= 1
+    const uint64_t g0c = g0 < lastg ? g0 : lastg;
+    const uint64_t dd = lastg - g0c;  // granules after the first
+    const uint32_t d = dd < (uint64_t)(LOAD / 16) ? (uint32_t)dd : (uint32_t)(LOAD / 16);
+    const uint4 *p = reinterpret_cast<const uint4 *>(seq) + g0c;
+#pragma unroll
+    for (int q = 0; q < LOAD / 16; ++q) {
+        const uint4 v = p[(uint32_t)q < d ? (uint32_t)q : d];
+        ww.w[4 * q + 0] = v.x;
+        ww.w[4 * q + 1] = v.y;
+        ww.w[4 * q + 2] = v.z;
+        ww.w[4 * q + 3] = v.w;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Direct window extraction.  Every 16 loaded bytes become three 32-bit words
 // (SWAR, no per-byte loop): the 2-bit codes MSB-first (the forward k-mer of
@@ -115,6 +142,18 @@ __host__ __device__ __forceinline__ void make_codes(const uint32_t *w, Codes<NP>
     }
 }
 
+// Bases at or past `avail` (the bytes the batch still holds from the load's
+// first byte) become invalid: load_windows_clamped read other bytes there.
+template <int NP>
+__host__ __device__ __forceinline__ void mark_tail(Codes<NP> &c, uint64_t avail) {
+#pragma unroll
+    for (int i = 0; i < (NP * 16 + 63) / 64; ++i) {
+        const uint64_t pos = 64ull * i;
+        const uint64_t m = avail <= pos ? ~0ull : (avail - pos >= 64 ? 0ull : ~0ull << (avail - pos));
+        c.bad[i] |= m;
+    }
+}
+
 // 64 code bits starting at base j, MSB-first (needs p[j/16 .. j/16 + 2]).
 template <int NP>
 __host__ __device__ __forceinline__ uint64_t fwd_top64(const Codes<NP> &c, int j) {
@@ -173,12 +212,16 @@ __host__ __device__ __forceinline__ K128 window_key128(const Codes<NP> &c, int j
 // compile-time constant.  Bytes at or beyond n read as 0 (invalid), so windows
 // never run off the end; record separators are invalid bytes, so windows never
 // cross records.  K > 0: k known at compile time; K = 0: k_rt.
+// avail: bytes of the batch from the load's first byte (~0: no tail marking,
+// the words were loaded by load_windows).
 template <int SEG, int K, bool RAW = false, typename Emit>
-__device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_rt, Emit &&emit) {
+__device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_rt, Emit &&emit,
+                                           uint64_t avail = ~0ull) {
     constexpr int NP = WinWords<SEG>::kLoad / 16;
     const uint32_t k = K ? (uint32_t)K : k_rt;
     Codes<NP> c;
     make_codes<NP, RAW>(ww.w, c);
+    if (avail < (uint64_t)WinWords<SEG>::kLoad) mark_tail<NP>(c, avail);  // the batch's last bytes only
 #pragma unroll
     for (int j = 0; j < SEG; ++j) {
         bool valid;
