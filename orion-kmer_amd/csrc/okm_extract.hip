@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                     [&](int j, uint64_t key, bool valid) {
                         const uint32_t b = valid ? bin_of(key, shift) : nb;
                         kk[j] = key;
-                        rk[j >> 1] |= atomicAdd(&hist[b], 1u) << (16 * (j & 1));
+                        rk[j >> 1] |= (atomicAdd(&hist[b], 1u) & 0xFFFFu) << (16 * (j & 1));
                         vm |= valid ? 1u << j : 0u;
                     },
                     g.n - w0);
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
-        if (t <= nb) hist[t] = 0;
+        for (uint32_t b = t; b <= nb; b += blockDim.x) hist[b] = 0;  // + the dummy bin (nb may equal the block)
         lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
         const bool live = w0 < end;
@@ -375,33 +375,36 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     constexpr int NP = WinWords<kSegW, 64>::kLoad / 16;
-    WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead
-    if (beg + (uint64_t)t * kSegW < end) load_windows<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
+    WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead (branch-free, as k_extract_scatter)
+    load_windows_clamped<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW1) {
-        if (t <= nb) hist[t] = 0;
+        for (uint32_t b = t; b <= nb; b += blockDim.x) hist[b] = 0;  // + the dummy bin (nb may equal the block)
         lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
         const bool live = w0 < end;
         uint32_t tile_n;
         {
             K128 kk[kSegW];
-            uint32_t rk[kSegW];  // bin << 16 | rank; invalid: nb << 16
+            uint32_t rk[kSegW / 2];  // two within-bin ranks per word; the bin is recomputed
+            uint32_t vm = 0;         // valid windows
 #pragma unroll
-            for (int j = 0; j < kSegW; ++j) rk[j] = nb << 16;
+            for (int j = 0; j < kSegW / 2; ++j) rk[j] = 0;
             if (live) {
                 Codes<NP> c;
                 make_codes<NP, false>(ww.w, c);
+                if (g.n - w0 < (uint64_t)WinWords<kSegW, 64>::kLoad) mark_tail<NP>(c, g.n - w0);
 #pragma unroll
                 for (int j = 0; j < kSegW; ++j) {
                     bool valid;
                     const K128 key = window_key128(c, j, g.k, &valid);
                     const uint32_t b = valid ? bin_of_wide(key, shift) : nb;
                     kk[j] = key;
-                    rk[j] = (b << 16) | atomicAdd(&hist[b], 1u);
+                    rk[j >> 1] |= (atomicAdd(&hist[b], 1u) & 0xFFFFu) << (16 * (j & 1));
+                    vm |= valid ? 1u << j : 0u;
                 }
             }
-            if (w0 + kTileW1 < end) load_windows<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);  // next tile, in flight
+            load_windows_clamped<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);  // next tile, in flight (harmless past the end)
             lds_sync();
             tile_n = tile_offsets<kScatBlockW>(t, nb, hist, lofs, lcur, wsum);
             uint32_t ch = 0;
@@ -413,8 +416,9 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
             lds_sync();
 #pragma unroll
             for (int j = 0; j < kSegW; ++j) {
-                const uint32_t b = rk[j] >> 16;
-                const uint32_t dst = b < nb ? lofs[b] + (rk[j] & 0xFFFFu) : (uint32_t)kTileW1 + (t & 63u);
+                const uint32_t rank = (rk[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t dst =
+                    (vm >> j) & 1u ? lofs[bin_of_wide(kk[j], shift)] + rank : (uint32_t)kTileW1 + (t & 63u);
                 stage[dst] = kk[j];
             }
             if (!HC && t < nb) {
