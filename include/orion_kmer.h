@@ -106,6 +106,11 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
 void okm_destroy(okm_ctx *ctx);
 /* Forget all input and results; keep device allocations for reuse. */
 okm_status okm_reset(okm_ctx *ctx);
+/* Give the context's cached (unused) device blocks back to the HIP runtime;
+ * what the input and the result hold stays.  For processes that keep several
+ * contexts on one device and use them in turn (another context's planner
+ * sees only the device's free memory). */
+okm_status okm_trim(okm_ctx *ctx);
 
 /* Append one batch of records held in HOST memory.  Record r is
  * seq[offsets[r] .. offsets[r+1]) (offsets has n_records+1 entries).

@@ -462,12 +462,14 @@ class LoopTransport final : public Transport {
         if (!hub_->barrier()) return lost();
         okm_status st = OKM_OK;
         if (n) {
-            if (hipMemcpyAsync(recv, hub_->post[0], n * sizeof(ull), hipMemcpyDeviceToDevice, s) != hipSuccess)
-                st = fail(OKM_E_DEVICE, "loopback all-reduce: copy");
+            (void)hipGetLastError();  // a stale (handled) error of this thread is not the launch's
+            hipError_t e = hipMemcpyAsync(recv, hub_->post[0], n * sizeof(ull), hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) st = fail(OKM_E_DEVICE, std::string("loopback all-reduce: copy: ") + hipGetErrorString(e));
             for (int r = 1; r < hub_->P && st == OKM_OK; ++r) {
                 hipLaunchKernelGGL(k_add_u64, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, recv,
                                    static_cast<const ull *>(hub_->post[r]), (uint64_t)n);
-                if (hipGetLastError() != hipSuccess) st = fail(OKM_E_DEVICE, "loopback all-reduce: kernel");
+                e = hipGetLastError();
+                if (e != hipSuccess) st = fail(OKM_E_DEVICE, std::string("loopback all-reduce: kernel: ") + hipGetErrorString(e));
             }
             if (hipStreamSynchronize(s) != hipSuccess && st == OKM_OK) st = fail(OKM_E_DEVICE, "loopback all-reduce");
         }

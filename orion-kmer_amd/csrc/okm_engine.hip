@@ -2324,6 +2324,14 @@ void okm_destroy(okm_ctx *c) {
 // OKM_COUNT_PROF=1 build of the counting kernel; zeroes them.
 extern "C" void okm_debug_count_prof(unsigned long long *out16) { okm::count_prof_read(out16); }
 
+okm_status okm_trim(okm_ctx *c) {
+    if (!c) return fail(OKM_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    OKM_TRY(sync(c));
+    c->pool.trim();
+    return OKM_OK;
+}
+
 okm_status okm_reset(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));

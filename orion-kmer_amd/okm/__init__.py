@@ -311,6 +311,10 @@ class KmerCounter:
     def reset(self) -> None:
         check(lib().okm_reset(self.ctx), "okm_reset")
 
+    def trim(self) -> None:
+        """Return the context's cached device blocks (okm_trim)."""
+        check(lib().okm_trim(self.ctx), "okm_trim")
+
     def add_records(self, seqs: Sequence[bytes], normalized: bool = False) -> None:
         data, offs = pack_records(list(seqs))
         self.add_batch(data, offs, normalized)

@@ -77,6 +77,7 @@ PROTOTYPES = {
     "okm_create": (c_int, [POINTER(c_void_p), c_uint8, c_int, c_int, c_uint64]),
     "okm_destroy": (None, [c_void_p]),
     "okm_reset": (c_int, [c_void_p]),
+    "okm_trim": (c_int, [c_void_p]),
     "okm_add_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int]),
     "okm_add_batch_device": (c_int, [c_void_p, c_void_p, c_uint64]),
     "okm_add_pairs_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),

@@ -20,6 +20,10 @@ input, warmup then timed steps bracketed by device syncs).
                      (P virtual ranks on one GPU) the samples shard over the
                      ranks and the unions are owner-partitioned by the
                      library's exchange (wl_c5_dist, okm_merge_owned_n).
+  --workload c3      BASELINE configs[2] over --loopback P virtual ranks on one
+                     GPU (wl_c3_loop): per-rank one-card count times, then
+                     okm_merge_owned at once; the owners' tables must digest
+                     exactly like the one-GPU table.
   --workload classify classify.rs:215-308 — probe a 32-reference database
                      (the genome split in 32 slices, ~100 M keys) against the
                      counted table of the batch (okm_classifier_probe_db).
@@ -477,6 +481,142 @@ def wl_c5_dist(args):
                        "union_size": union_, "jaccard_index": inter / union_ if union_ else 0.0}}
 
 
+C3_READS, C3_GENOME_BP, C3_SEED, C3_BATCH_READS = 167_772_160, 1_000_000_000, 3, 4_194_304  # bench.py
+
+
+def _table_digest(kp: int, cp: int, n: int, pos0: int, chunk: int = 1 << 26):
+    """Order-sensitive digests of a device (key, count) table as int64 sums
+    (wrapping), positions counted from pos0: the owners' tables, concatenated
+    in rank order, digest like the one-GPU table."""
+    import torch
+    from okm import dist as okm_dist
+    if not n:
+        return [0, 0, 0, 0]
+    keys = torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda")
+    counts = torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda")
+    d = [n, 0, 0, 0]
+    for o in range(0, n, chunk):
+        kk, cc = keys[o:o + chunk], counts[o:o + chunk]
+        pos = torch.arange(pos0 + o, pos0 + o + kk.numel(), dtype=torch.int64, device=kk.device)
+        mix = kk * 0x1E3779B97F4A7C15 - 0x61C8864680B583EB
+        d[1] += int(cc.sum().item())
+        d[2] += int((mix ^ cc).sum().item())
+        d[3] += int(((mix + pos) * (cc | 1)).sum().item())
+        del pos, mix
+    return d
+
+
+def wl_c3_loop(args):
+    """BASELINE configs[2] (C3) over P virtual ranks on ONE GPU
+    (okm_comm_init_loopback): rank r counts its contiguous 1/P shard of the
+    167,772,160 reads into one table (count.rs:52-89), the ranks' counts one
+    at a time (each alone on the GPU, as on its own card), then every rank runs
+    okm_merge_owned (owner == local, as bench.py at N>1) at once.  The owners'
+    tables, concatenated in rank order, must digest exactly like the one-GPU
+    table of the same reads.  A rehearsal of the N>1 path of bench.py --workload
+    c3: the per-rank count times are one-card times; the exchange + merge share
+    one device here, so they are not N-GPU times."""
+    import threading
+    P = max(1, args.loopback)
+    k, stride = 31, READ_LEN + 1
+    total = C3_READS
+    shards = []
+    t0 = time.time()
+    for r in range(P):
+        r0, r1 = total * r // P, total * (r + 1) // P
+        buf = okm.DeviceBuffer(max(1, (r1 - r0) * stride))
+        okm.synth_reads_device(buf.address, r1 - r0, READ_LEN, genome_len=C3_GENOME_BP, genome_seed=C3_SEED,
+                               seed=C3_SEED, first_read=r0, sub_rate=0.001, n_rate=0.0001)
+        spans = [(b0 * stride, (min(r1 - r0, b0 + C3_BATCH_READS) - b0) * stride)
+                 for b0 in range(0, r1 - r0, C3_BATCH_READS)]
+        shards.append((buf, spans, (r1 - r0) * READ_LEN))
+    log(f"C3 shards for {P} ranks generated on the device ({time.time() - t0:.1f}s)")
+    ref, t_one = None, None
+    if not args.no_ref:  # the one-GPU table of the same reads, shard after shard (second of two runs)
+        c = okm.KmerCounter(k)
+        for _ in range(2):
+            c.reset()
+            t = time.perf_counter()
+            for buf, spans, _ in shards:
+                for off, nb in spans:
+                    c.add_device_batch(buf.address + off, nb)
+            n1 = c.count()
+            c.synchronize()
+            t_one = time.perf_counter() - t
+        kp, cp, _ = c.result_device()
+        ref = _table_digest(kp, cp, n1, 0)
+        c.close()
+        log(f"one-GPU reference: {n1} distinct keys, {t_one * 1e3:.1f} ms")
+    comms = okm.Comm.init_loopback(P, 0)
+    ctrs = [okm.KmerCounter(k) for _ in range(P)]
+    lock, gate = threading.Lock(), threading.Barrier(P)
+    res, err = [None] * P, []
+
+    def body(r):
+        try:
+            buf, spans, bases = shards[r]
+            for rnd in range(2):  # round 0 warms the pools (first allocations), round 1 is timed
+                with lock:  # one rank's count at a time: each has the card to itself
+                    ctrs[r].reset()
+                    t = time.perf_counter()
+                    for off, nb in spans:
+                        ctrs[r].add_device_batch(buf.address + off, nb)
+                    n_local = ctrs[r].count()
+                    ctrs[r].synchronize()
+                    tc = time.perf_counter() - t
+                    info = ctrs[r].engine_info()
+                    ctrs[r].trim()
+                gate.wait()
+                t = time.perf_counter()
+                n_own = comms[r].merge_owned(ctrs[r], ctrs[r])
+                ctrs[r].synchronize()
+                tm = time.perf_counter() - t
+                gate.wait()
+            res[r] = {"n_local": n_local, "n_own": n_own, "count_ms": tc * 1e3, "merge_wall_ms": tm * 1e3,
+                      "phases": comms[r].last_times(), "bytes": comms[r].last_bytes(), "bases": bases,
+                      "folds": int(info.get("folds", 0))}
+        except BaseException as e:  # surfaced below
+            err.append(e)
+            gate.abort()
+
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(P)]
+    for t_ in th:
+        t_.start()
+    for t_ in th:
+        t_.join()
+    if err:
+        raise err[0]
+    for buf, _, _ in shards:
+        buf.free()
+    got, pos = [0, 0, 0, 0], 0
+    for r in range(P):
+        kp, cp, _ = ctrs[r].result_device()
+        d = _table_digest(kp, cp, res[r]["n_own"], pos)
+        got = [a + b for a, b in zip(got, d)]
+        pos += res[r]["n_own"]
+    m64 = (1 << 64) - 1
+    got = [got[0], got[1], got[2] & m64, got[3] & m64]
+    exact = None if ref is None else got == [ref[0], ref[1], ref[2] & m64, ref[3] & m64]
+    for c in ctrs:
+        c.close()
+    for c in comms:
+        c.close()
+    count_max = max(o["count_ms"] for o in res)
+    sent = sum(o["bytes"][0] for o in res)
+    return {"metric": f"C3 over {P} loopback ranks on one MI355X: per-rank one-card count time, owner-merged "
+                      f"table exact vs the one-GPU table",
+            "value": round(total * READ_LEN / (count_max * 1e-3), 1), "unit": "bases/s (all bases / slowest rank count)",
+            "n_gpus": 1, "ranks": P, "steps": 1, "warmup": 0, "higher_is_better": True, "dtype": "u64",
+            "data": "synthetic (C3 reads generated on the device)",
+            "config": {"workload": f"BASELINE configs[2] (C3) sharded 1/{P}: {total} reads x {READ_LEN} bp from a 1 Gbp "
+                                   f"genome", "k": k, "exchange": "okm_merge_owned over a loopback communicator",
+                       "one_gpu_ms": None if t_one is None else round(t_one * 1e3, 1),
+                       "distinct_global": pos, "exact_vs_one_gpu": exact,
+                       "bytes_sent_all_ranks": sent,
+                       "wire_bytes_per_pair": round(sent / max(1, sum(o["n_local"] for o in res)), 3)},
+            "ranks_detail": [{k_: (round(v, 2) if isinstance(v, float) else v) for k_, v in o.items()} for o in res]}
+
+
 def wl_classify(args):
     k = 31
     batch = c2_batch()
@@ -517,7 +657,8 @@ def wl_classify(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["query", "build", "wide", "classify", "c5"], required=True)
+    ap.add_argument("--workload", choices=["query", "build", "wide", "classify", "c5", "c3"], required=True)
+    ap.add_argument("--no-ref", action="store_true", help="c3: skip the one-GPU reference table")
     ap.add_argument("--c5-cap", type=float, default=256e6, help="c5: base cap per sample (SURVEY: 256 Mbases)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -528,7 +669,7 @@ def main():
     args = ap.parse_args()
     c5 = wl_c5_dist if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.loopback else wl_c5
     out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify,
-           "c5": c5}[args.workload](args)
+           "c5": c5, "c3": wl_c3_loop}[args.workload](args)
     if out is not None:
         print(json.dumps(out), flush=True)
 
