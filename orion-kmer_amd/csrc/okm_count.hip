@@ -180,8 +180,38 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
             if ((uint32_t)u * kCB >= len) break;  // block-uniform
             const uint32_t f = (uint32_t)u * kCB + t;
             if (f < len) {
-                kk[u] = reinterpret_cast<const KT *>(it.keys0)[f];
-                if (W && it.counts0) ww[u] = it.counts0[f];
+                kk[u] = gload(reinterpret_cast<const KT *>(it.keys0) + f);
+                if (W && it.counts0) ww[u] = gload(it.counts0 + f);
+            }
+        }
+        return;
+    }
+    if (it.seg_count <= 4) {  // merged sibling children (k_make_items): the <= 4 descriptors load together
+        const uint32_t R = it.seg_count;
+        const KT *kb[4];
+        const uint64_t *cb[4];
+        uint32_t st[5];
+        st[0] = 0;
+#pragma unroll
+        for (uint32_t sg = 0; sg < 4; ++sg) {
+            const DevSeg s = segs[it.seg_begin + (sg < R ? sg : 0u)];
+            kb[sg] = reinterpret_cast<const KT *>(s.keys);
+            cb[sg] = s.counts;
+            st[sg + 1] = st[sg] + (sg < R ? (uint32_t)s.len : 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            if ((uint32_t)u * kCB >= st[4]) break;  // block-uniform
+            const uint32_t f = (uint32_t)u * kCB + t;
+            if (f < st[4]) {
+                const uint32_t sg = (f >= st[1] ? 1u : 0u) + (f >= st[2] ? 1u : 0u) + (f >= st[3] ? 1u : 0u);
+                const uint32_t p = f - (sg == 0 ? 0u : sg == 1 ? st[1] : sg == 2 ? st[2] : st[3]);
+                const KT *kp = sg == 0 ? kb[0] : sg == 1 ? kb[1] : sg == 2 ? kb[2] : kb[3];
+                kk[u] = gload(kp + p);
+                if (W) {
+                    const uint64_t *cp = sg == 0 ? cb[0] : sg == 1 ? cb[1] : sg == 2 ? cb[2] : cb[3];
+                    if (cp) ww[u] = gload(cp + p);
+                }
             }
         }
         return;
@@ -195,8 +225,8 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
             if ((uint32_t)u * kCB >= sbase + len) break;  // block-uniform: rows past the segment
             const uint32_t f = (uint32_t)u * kCB + t - sbase;  // wraps for f < sbase
             if (f < len) {
-                kk[u] = reinterpret_cast<const KT *>(s.keys)[f];
-                if (W && s.counts) ww[u] = s.counts[f];
+                kk[u] = gload(reinterpret_cast<const KT *>(s.keys) + f);
+                if (W && s.counts) ww[u] = gload(s.counts + f);
             }
         }
         sbase += len;
@@ -238,8 +268,8 @@ __device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *
                 if (coff[mid] <= f) lo = mid; else hi = mid;
             }
             const uint32_t p = f - coff[lo];
-            kk[u] = reinterpret_cast<const KT *>(ck[lo])[p];
-            if (W && cc[lo]) ww[u] = cc[lo][p];
+            kk[u] = gload(reinterpret_cast<const KT *>(ck[lo]) + p);
+            if (W && cc[lo]) ww[u] = gload(cc[lo] + p);
         }
     }
 }
@@ -445,6 +475,8 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     uint8_t *rf = reinterpret_cast<uint8_t *>(rk + (W ? 2 : 1) * L::kRest);
 
     // 1. claim / count tags; rest instances take a slot in their home's run
+    //    (row by row: batching the rows' CASes before consuming them measured
+    //    slower, 1.66 -> 1.71-1.78 ms on C2 at 2 / 4 rows per batch)
     uint32_t hp[kPer];  // rest: home << 16 | pos; otherwise ~0
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -637,8 +669,8 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
 #pragma unroll
             for (int u = 0; u < kLoadU; ++u) {
                 const uint64_t idx = base + (uint64_t)u * kCB + t;
-                kk[u] = idx < s.len ? keys[idx] : KeyOps<KT>::empty();
-                ww[u] = (W && s.counts && idx < s.len) ? (CT)s.counts[idx] : (CT)1;
+                kk[u] = idx < s.len ? gload(keys + idx) : KeyOps<KT>::empty();
+                ww[u] = (W && s.counts && idx < s.len) ? (CT)gload(s.counts + idx) : (CT)1;
             }
 #pragma unroll
             for (int u = 0; u < kLoadU; ++u) {

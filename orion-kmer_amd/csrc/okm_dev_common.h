@@ -29,6 +29,29 @@ __device__ __forceinline__ void lds_sync() {
 #endif
 }
 
+// A load through a pointer the kernel read from a descriptor (DevSeg /
+// DevItem keys and counts): the compiler cannot prove such a pointer global
+// and emits FLAT loads, which also count against lgkmcnt -- so every LDS wait
+// behind them (the count's tag CASes, the partition's histogram atomics)
+// waits for the whole batch of key loads.  Every descriptor pointer is a
+// device (global) allocation.
+template <typename T>
+__device__ __forceinline__ T gload(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+// 16-B types: one global_load_dwordx4 through a plain vector type (class
+// types such as K128 and uint4 cannot be copied out of address space 1)
+__device__ __forceinline__ K128 gload(const K128 *p) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 v = *(const __attribute__((address_space(1))) u64x2 *)p;
+    return K128{v.x, v.y};
+}
+__device__ __forceinline__ uint4 gload(const uint4 *p) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ ull wave_incl_scan(ull v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

@@ -19,6 +19,13 @@ constexpr uint64_t kScanTile = (uint64_t)kScanBlock * kScanPer;
 // list and the larger ones from the back.
 constexpr uint64_t kFanSmallJob = 16384;
 
+#ifndef OKM_COMPACT_WAVE  // k_compact_items: one wave per item (0: one 256-thread block per item)
+#define OKM_COMPACT_WAVE 1
+#endif
+#ifndef OKM_MERGE_SIBLINGS  // k_make_items: count aligned groups of 2 / 4 sparse sibling children as one item
+#define OKM_MERGE_SIBLINGS 0  // measured: count_items 1.658 -> 1.711 ms on C2 (fuller items are slower)
+#endif
+
 __global__ __launch_bounds__(kScanBlock) void k_scan_block(const ull *__restrict__ in,
                                                            ull *__restrict__ out, uint64_t n,
                                                            ull *__restrict__ block_sums) {
@@ -95,6 +102,61 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     const ull o = offs[i], len = (ends ? ends[i] : offs[i + 1]) - o;
     const ull so = doff ? doff[i] : o;  // staged output slot: dense, or the level's own range
     const uint32_t F = 1u << fan.bits;  // item slots per child (in key order)
+#if OKM_MERGE_SIBLINGS
+    // Sibling merge (no fan-out rounds only): an aligned group of 2 or 4
+    // sibling children whose instances fit one item together is counted as
+    // ONE item -- their union is the key range one bit (two bits) above them,
+    // so the item's homes are that range's top bits and the output stays in
+    // key order.  Power-of-two splits leave children between 1/2 and 1x the
+    // planner's target; merging the sparse ones fills items closer to the
+    // count kernel's capacity (fewer items, same instances).  The head child's
+    // item takes the group's segments (segs of consecutive children are
+    // consecutive when fan.bits = 0); the other members' slots are empty items.
+    if (fan.bits == 0 && len <= item_max) {
+        const uint32_t pb = parents[lo].out_base;
+        const uint32_t nch = (lo + 1 < nparents ? parents[lo + 1].out_base : nout) - pb;
+        const uint32_t j = i - pb;
+        uint32_t g = 1;
+        ull gsum = len;
+#pragma unroll
+        for (uint32_t m = 2; m >= 1; --m) {
+            const uint32_t gg = 1u << m;
+            if (g != 1 || nch % gg != 0) continue;
+            const uint32_t h = pb + (j & ~(gg - 1u));
+            ull s = 0;
+            for (uint32_t q = 0; q < gg; ++q) s += (ends ? ends[h + q] : offs[h + q + 1]) - offs[h + q];
+            if (s <= item_max && rem + m <= 64) {
+                g = gg;
+                gsum = s;
+            }
+        }
+        if (g > 1) {
+            const uint32_t head = pb + (j & ~(g - 1u));
+            DevSeg s;
+            s.keys = lk + o * kw;
+            s.counts = lc ? lc + o : nullptr;
+            s.len = len;
+            s.key_base = 0;
+            s.out_base = 0;
+            s.shift = kSingleBin;
+            s.nlocal = 1;
+            s.pad = 0;
+            segs[i] = s;
+            DevItem it;
+            it.seg_begin = head;
+            it.seg_count = g;
+            it.out_off = doff ? doff[head] : offs[head];
+            it.rem_bits = rem + (g == 4 ? 2u : 1u);
+            it.pad = i == head ? 0u : kItemEmpty;
+            it.total = i == head ? gsum : 0;
+            it.keys0 = s.keys;
+            it.counts0 = s.counts;
+            items[i] = it;
+            if (i == head) atomicMax(&flags[2], gsum);
+            return;
+        }
+    }
+#endif
     uint32_t b = 0;                     // this child's own fan-out
     if (len > item_max && rem > capbits) {
         if (fan.bits && len <= fan.split_max) {
@@ -601,6 +663,55 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
                                                        const ull *__restrict__ d_nitems) {
     if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
+#if OKM_COMPACT_WAVE
+    // One wave per item (an item holds ~600 entries at C2: a 256-thread block
+    // per item left most lanes idle behind three dependent descriptor loads);
+    // the next item's descriptor is loaded during this item's copy, and every
+    // lane keeps four entries in flight.
+    // (an odd wave stride: fan-out slots, 2^bits per child, spread over waves)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * 4u - 1u;
+    uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (item >= nw) return;  // the last wave: its items belong to wave 0
+    uint64_t n = 0, src = 0, dst = 0;
+    if (item < nitems) {
+        n = n_out[item];
+        src = items[item].out_off;
+        dst = dense_off[item];
+    }
+    const uint32_t *sc32 = reinterpret_cast<const uint32_t *>(sc);
+    for (; item < nitems; item += nw) {
+        const uint32_t nxt = item + nw;
+        uint64_t nn = 0, ns = 0, nd = 0;
+        if (nxt < nitems) {
+            nn = n_out[nxt];
+            ns = items[nxt].out_off;
+            nd = dense_off[nxt];
+        }
+        uint64_t j = lane;
+        for (; j + 192 < n; j += 256) {
+            KT k[4];
+            uint64_t c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                k[q] = sk[src + j + 64 * q];
+                c[q] = NARROW ? (uint64_t)sc32[src + j + 64 * q] : sc[src + j + 64 * q];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                dk[dst + j + 64 * q] = k[q];
+                dc[dst + j + 64 * q] = c[q];
+            }
+        }
+        for (; j < n; j += 64) {
+            dk[dst + j] = sk[src + j];
+            dc[dst + j] = NARROW ? (uint64_t)sc32[src + j] : sc[src + j];
+        }
+        n = nn;
+        src = ns;
+        dst = nd;
+    }
+#else
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
         const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
         for (uint64_t j = threadIdx.x; j < n; j += 256) {
@@ -608,6 +719,7 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
             dc[dst + j] = NARROW ? (uint64_t)reinterpret_cast<const uint32_t *>(sc)[src + j] : sc[src + j];
         }
     }
+#endif
 }
 
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
@@ -616,7 +728,11 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
                           const unsigned long long *err, const unsigned long long *d_nitems) {
     if (!nitems) return;
+#if OKM_COMPACT_WAVE
+    const dim3 g(nitems / 4u + 1u < 4096u ? nitems / 4u + 1u : 4096u), b(256);  // one wave per item
+#else
     const dim3 g(nitems < 8191u ? nitems : 8191u), b(256);  // odd: fan-out slots spread over blocks
+#endif
     hipStream_t s = (hipStream_t)stream;
     const K128 *sk2 = reinterpret_cast<const K128 *>(src_keys);
     K128 *dk2 = reinterpret_cast<K128 *>(dst_keys);

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
 #pragma unroll
                 for (int u = 0; u < kHistU; ++u) {
                     const uint64_t q = i + (uint64_t)u * kPartBlock;
-                    v[u] = q < n2 ? k4[q] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                    v[u] = q < n2 ? gload(k4 + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
                 }
 #pragma unroll
                 for (int u = 0; u < kHistU; ++u) {
@@ -100,14 +100,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
                     hist_key(*reinterpret_cast<const KT *>(&b), s, lh);
                 }
             }
-            if ((ch.len & 1) && threadIdx.x == 0) hist_key(keys[ch.len - 1], s, lh);
+            if ((ch.len & 1) && threadIdx.x == 0) hist_key(gload(keys + ch.len - 1), s, lh);
         } else {
             for (uint64_t i = threadIdx.x; i < ch.len; i += (uint64_t)kPartBlock * kHistU) {
                 KT v[kHistU];
 #pragma unroll
                 for (int u = 0; u < kHistU; ++u) {
                     const uint64_t q = i + (uint64_t)u * kPartBlock;
-                    v[u] = q < ch.len ? keys[q] : KeyOps<KT>::empty();
+                    v[u] = q < ch.len ? gload(keys + q) : KeyOps<KT>::empty();
                 }
 #pragma unroll
                 for (int u = 0; u < kHistU; ++u) hist_key(v[u], s, lh);
@@ -172,8 +172,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
 #pragma unroll
             for (int u = 0; u < kLoadU; ++u) {
                 const uint64_t idx = base + (uint64_t)u * kPartBlock + t;
-                kk[u] = idx < ch.len ? keys[idx] : KeyOps<KT>::empty();
-                ww[u] = (W && idx < ch.len) ? (cnts ? cnts[idx] : 1ull) : 1ull;
+                kk[u] = idx < ch.len ? gload(keys + idx) : KeyOps<KT>::empty();
+                ww[u] = (W && idx < ch.len) ? (cnts ? gload(cnts + idx) : 1ull) : 1ull;
                 if (!KeyOps<KT>::is_empty(kk[u])) pend |= 1u << u;
             }
             // append rounds: a key whose bin buffer is full waits for the flush
@@ -275,8 +275,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 const uint64_t idx = base + (uint64_t)u * kPartBlock + t;
-                kk[u] = idx < ch.len ? keys[idx] : KeyOps<KT>::empty();
-                ww[u] = (W && idx < ch.len) ? (cnts ? cnts[idx] : 1ull) : 1ull;
+                kk[u] = idx < ch.len ? gload(keys + idx) : KeyOps<KT>::empty();
+                ww[u] = (W && idx < ch.len) ? (cnts ? gload(cnts + idx) : 1ull) : 1ull;
             }
 #pragma unroll
             for (int u = 0; u < P; ++u) {
