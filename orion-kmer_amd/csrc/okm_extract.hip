@@ -55,10 +55,14 @@ constexpr int kExtractBlock = 256;
 constexpr int kScatBlock = OKM_EXTRACT_BLOCK;  // k <= 32 scatter
 constexpr int kSegS = OKM_EXTRACT_SEG;         // scatter: window starts per thread
 constexpr int kTile = kScatBlock * kSegS;      // scatter tile: 16384 windows
-static_assert(kScatBlock >= 256 && (16384 % kTile) == 0, "scatter tile must divide the hist tile");
+static_assert(kScatBlock >= 256, "one L1 bin per scatter thread");
 static_assert(kSegS % 16 == 0, "scan_windows loads whole 16-B words");
-constexpr int kSegH = 64;                      // hist: window starts per thread
+#ifndef OKM_EXTRACT_HSEG  // hist: window starts per thread (kHTile must be a multiple of the scatter tile)
+#define OKM_EXTRACT_HSEG 64
+#endif
+constexpr int kSegH = OKM_EXTRACT_HSEG;         // hist: window starts per thread
 constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
+static_assert(kHTile % kTile == 0, "scatter tile must divide the hist tile");
 #ifndef OKM_L1_BITS  // first-level key-range bins of the k <= 32 extraction (2^bits <= kScatBlock)
 #define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
 #endif
@@ -69,7 +73,8 @@ constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
 constexpr int kMaxL1BinsW = 1 << OKM_L1_BITS_W;  // k in 33..64 kernels
 static_assert(kMaxL1Bins <= kScatBlock, "one bin per scatter thread");
 
-uint32_t extract_tile() { return (uint32_t)kHTile; }  // chunks are multiples of both tiles
+constexpr uint32_t gcd_u32(uint32_t a, uint32_t b) { return b ? gcd_u32(b, a % b) : a; }
+constexpr uint32_t lcm_u32(uint32_t a, uint32_t b) { return a / gcd_u32(a, b) * b; }
 uint32_t extract_max_bins(bool wide) { return (uint32_t)(wide ? kMaxL1BinsW : kMaxL1Bins); }
 
 template <int K>
@@ -239,7 +244,9 @@ constexpr int kTileW = kExtractBlock * kSegW;   // 4096 windows: 64 KiB stage
 #endif
 constexpr int kScatBlockW = OKM_WIDE_SCAT_BLOCK;
 constexpr int kTileW1 = kScatBlockW * kSegW;     // 256 threads: 64 KiB stage; 512: 128 KiB (one per CU)
-static_assert(kScatBlockW >= kMaxL1BinsW && (16384 % kTileW1) == 0, "wide scatter tile must divide the hist tile");
+static_assert(kScatBlockW >= kMaxL1BinsW, "one L1 bin per wide scatter thread");
+// chunks are multiples of every tile (the hist walks kHTile steps, the scatters kTile / kTileW1 steps)
+uint32_t extract_tile() { return lcm_u32(lcm_u32((uint32_t)kHTile, (uint32_t)kTile), (uint32_t)kTileW1); }
 
 // Windows [w0, w0 + SEG) with 2k-bit keys (direct extraction, okm_scan.h):
 // the forward key is the 2k code bits from base j (MSB-first) and the reverse
