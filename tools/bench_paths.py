@@ -519,7 +519,7 @@ def wl_c3_loop(args):
     import threading
     P = max(1, args.loopback)
     k, stride = 31, READ_LEN + 1
-    total = C3_READS
+    total = args.c3_reads
     shards = []
     t0 = time.time()
     for r in range(P):
@@ -608,8 +608,8 @@ def wl_c3_loop(args):
             "value": round(total * READ_LEN / (count_max * 1e-3), 1), "unit": "bases/s (all bases / slowest rank count)",
             "n_gpus": 1, "ranks": P, "steps": 1, "warmup": 0, "higher_is_better": True, "dtype": "u64",
             "data": "synthetic (C3 reads generated on the device)",
-            "config": {"workload": f"BASELINE configs[2] (C3) sharded 1/{P}: {total} reads x {READ_LEN} bp from a 1 Gbp "
-                                   f"genome", "k": k, "exchange": "okm_merge_owned over a loopback communicator",
+            "config": {"workload": f"BASELINE configs[2] (C3) shape sharded 1/{P}: {total} reads x {READ_LEN} bp from a "
+                                   f"1 Gbp genome" + ("" if total == C3_READS else f" ({total / C3_READS:.3g} of C3's reads)"), "k": k, "exchange": "okm_merge_owned over a loopback communicator",
                        "one_gpu_ms": None if t_one is None else round(t_one * 1e3, 1),
                        "distinct_global": pos, "exact_vs_one_gpu": exact,
                        "bytes_sent_all_ranks": sent,
@@ -659,6 +659,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["query", "build", "wide", "classify", "c5", "c3"], required=True)
     ap.add_argument("--no-ref", action="store_true", help="c3: skip the one-GPU reference table")
+    ap.add_argument("--c3-reads", type=int, default=C3_READS,
+                    help="c3: total reads (BASELINE configs[2]: 167,772,160; P local tables of the full size do not "
+                         "fit one GPU beyond P = 2)")
     ap.add_argument("--c5-cap", type=float, default=256e6, help="c5: base cap per sample (SURVEY: 256 Mbases)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)

@@ -3,7 +3,7 @@
 # one-GPU table, per-rank one-card count times, exchange bytes (P = 2, 4, 8).
 mkdir -p gpurun_out
 for P in "$@"; do
-  timeout -k 10 400 python tools/bench_paths.py --workload c3 --loopback $P \
+  timeout -k 10 400 python tools/bench_paths.py --workload c3 --loopback $P ${C3_READS:+--c3-reads $C3_READS} \
       > gpurun_out/r03_c3loop_$P.json 2> gpurun_out/r03_c3loop_$P.err || { tail -5 gpurun_out/r03_c3loop_$P.err; exit 1; }
   python - $P <<'PY'
 import json, sys
