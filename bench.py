@@ -21,7 +21,13 @@ others' streaming kernels; measured 2 / 3 / 4 in flight: 5.81-6.02 /
 c2) one thread counts batch i+1 into two contexts in turn while the main thread
 runs okm_merge_owned on batch i (the library's RCCL stream) into one of two
 merge contexts.  Every step still counts one full batch into its own sorted
-table.  The default workload at N>1 is C3 (BASELINE configs[2], main_c3).
+table.  The line's `value` is this configs[1] workload at every N (weak
+scaling: the driver's per-N values compare like for like).
+
+After it, the same invocation measures BASELINE configs[2] (C3: 25.17 Gbases
+from a 1 Gbp genome, sharded 1/N over the ranks, strong scaling, c3_run) and
+reports it in the same line as `c3` (`--c3-steps 0` skips it; `--workload c3`
+makes C3 the line's `value`).
 
 Prints ONE JSON line on rank 0 (the driver's contract), including `roofline`
 for the dominant kernel (HIP events on the engine's own stream, from a
@@ -147,9 +153,13 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--streams", type=int, default=3,
                     help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
-    ap.add_argument("--workload", choices=["c2", "c3"], default=None,
-                    help="c2: BASELINE configs[1] (1 GiB per GPU; default at N=1); c3: BASELINE configs[2] "
-                         "(50 GiB of reads from a 1 Gbp genome sharded 1/N over the ranks; default at N>1)")
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+                    help="c2: BASELINE configs[1] (1 GiB per GPU, weak scaling; default); c3: BASELINE configs[2] "
+                         "(50 GiB of reads from a 1 Gbp genome sharded 1/N over the ranks) as the line's value")
+    ap.add_argument("--c3-steps", type=int, default=2,
+                    help="c2 workload: timed steps of the C3 (configs[2]) measurement reported as `c3` "
+                         "in the same line (0: skip it)")
+    ap.add_argument("--c3-warmup", type=int, default=1, help="c2 workload: untimed C3 steps before those")
     ap.add_argument("--c3-reads", type=int, default=C3_READS,
                     help="c3: total reads over all ranks (BASELINE configs[2]: 167,772,160)")
     ap.add_argument("--c3-genome-bp", type=int, default=C3_GENOME_BP,
@@ -162,8 +172,7 @@ def parse():
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    workload = args.workload or ("c2" if world == 1 else "c3")
-    if workload == "c3":
+    if args.workload == "c3":
         return main_c3(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -382,6 +391,20 @@ def main():
         cpu, cpu_mt = cpu_baselines(batch, min(args.cpu_sample_reads, args.reads),
                                     min(args.cpu_mt_reads, args.reads), device, "the same batch")
 
+    # BASELINE configs[2] (C3) in the same invocation, every rank (its merge is
+    # collective): the C2 contexts go first so the C3 shard has the device
+    c3 = None
+    if args.c3_steps > 0:
+        for c in ctrs + mergers:
+            c.close()
+        dbuf.free()
+        torch.cuda.empty_cache()
+        try:
+            c3 = c3_run(args, world, rank, device, comm, dist_on, args.c3_steps, args.c3_warmup, baselines=False)
+        except Exception as e:  # reported in the line; the configs[1] measurement above stands
+            log(f"[rank {rank}] C3 measurement failed: {e!r}")
+            c3 = {"error": repr(e)}
+
     if rank != 0:
         if comm is not None:
             comm.close()
@@ -433,12 +456,18 @@ def main():
                                              "merge": round(xt[1] / args.steps * 1e3, 3)}
         out["exchange_impl"] = ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
                                 if comm is not None else "torch gloo rehearsal (okm/dist.py)")
+    if c3 is not None:
+        out["c3"] = ({k: c3[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                         "scaling", "config", "exchange_impl", "phase_ms_per_step_rank0",
+                                         "survey_roofline")}
+                     if "value" in c3 else c3)
     emit(out)
     if comm is not None:
         comm.close()
     if dist_on:
         dist.destroy_process_group()
-    dbuf.free()
+    if args.c3_steps <= 0:
+        dbuf.free()
 
 
 def main_c3(args):
@@ -473,7 +502,21 @@ def main_c3(args):
                 uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
             dist.broadcast(uid, 0)
             comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
+    out = c3_run(args, world, rank, device, comm, dist_on, args.steps, args.warmup, baselines=True)
+    if out is not None:
+        emit(out)
+    if comm is not None:
+        comm.close()
+    if dist_on:
+        dist.destroy_process_group()
 
+
+def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
+    """Time `steps` whole C3 jobs (after `warmup` untimed ones) on every rank
+    and return rank 0's line (None on the other ranks).  Every rank must call
+    it (the merge is collective); it releases its contexts and shard buffer."""
+    if dist_on:
+        from okm import dist as okm_dist
     total = args.c3_reads
     r0, r1 = total * rank // world, total * (rank + 1) // world
     nreads = r1 - r0
@@ -539,13 +582,13 @@ def main_c3(args):
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         step()
     barrier_sync()
     xt[:] = [0.0, 0.0, 0.0]
     t_start = time.perf_counter()
     n_last = 0
-    for _ in range(args.steps):
+    for _ in range(steps):
         n_last = step()
     barrier_sync()
     dt = time.perf_counter() - t_start
@@ -571,22 +614,22 @@ def main_c3(args):
         ctr.set_timing(False)
 
     cpu = cpu_mt = None
-    if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
+    if baselines and rank == 0 and world == 1 and args.cpu_sample_reads > 0:
         m = min(args.cpu_sample_reads, nreads)
         mm = min(max(m, args.cpu_mt_reads), nreads)
         host = np.empty(mm * stride, dtype=np.uint8)
         dbuf.download(host)
         cpu, cpu_mt = cpu_baselines(host, m, min(args.cpu_mt_reads, nreads), device, "the C3 shard")
 
+    if merger is not None and merger is not ctr:
+        merger.close()
+    ctr.close()
+    dbuf.free()
     if rank != 0:
-        if comm is not None:
-            comm.close()
-        if dist_on:
-            dist.destroy_process_group()
-        return
+        return None
     shard_bases = nreads * READ_LEN
     all_bases = total * READ_LEN
-    value = all_bases * args.steps / dt
+    value = all_bases * steps / dt
     roof, kernels = roofline_from_stats(stats, shard_bases)
     kmers = info["kmers"]
     surv_bytes = shard_bases + 16.0 * kmers
@@ -595,9 +638,9 @@ def main_c3(args):
         "value": round(value, 1),
         "unit": "bases/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1000, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1000, 3),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -616,23 +659,19 @@ def main_c3(args):
         "cpu_baseline": cpu,
         "cpu_baseline_mt": cpu_mt,
         "survey_roofline": {"alg_bytes_per_step_per_gpu": surv_bytes,
-                            "achieved_GBs_per_gpu": round(surv_bytes * args.steps / dt / 1e9, 1),
-                            "frac_of_8TBs": round(surv_bytes * args.steps / dt / 8e12, 4),
-                            "input_stream_frac": round(shard_bases * args.steps / dt / 8e12, 5)},
+                            "achieved_GBs_per_gpu": round(surv_bytes * steps / dt / 1e9, 1),
+                            "frac_of_8TBs": round(surv_bytes * steps / dt / 8e12, 4),
+                            "input_stream_frac": round(shard_bases * steps / dt / 8e12, 5)},
         "exchange_impl": ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
                           if comm is not None else ("torch gloo rehearsal" if dist_on else None)),
-        "phase_ms_per_step_rank0": {"count": round(xt[0] / args.steps * 1e3, 2),
-                                    "exchange": round(xt[1] / args.steps * 1e3, 2),
-                                    "merge": round(xt[2] / args.steps * 1e3, 2)},
+        "phase_ms_per_step_rank0": {"count": round(xt[0] / steps * 1e3, 2),
+                                    "exchange": round(xt[1] / steps * 1e3, 2),
+                                    "merge": round(xt[2] / steps * 1e3, 2)},
         "kernels": kernels,
         "engine": info,
     }
-    emit(out)
-    if comm is not None:
-        comm.close()
-    if dist_on:
-        dist.destroy_process_group()
-    dbuf.free()
+    return out
+
 
 
 def cpu_baselines(host, m, m_mt, device, what):

@@ -47,7 +47,8 @@ template <typename KT> struct Line {
 #define OKM_PART_2048 1
 #endif
 uint32_t part_max_bins(bool weighted, bool wide) {
-    return weighted ? 512u : (!wide && OKM_PART_2048 ? 2048u : 1024u);
+    // the tile scan gives each thread one bin (two in the 2048-bin variant)
+    return weighted ? 512u : (!wide && OKM_PART_2048 ? 2u * kPartBlock : (uint32_t)kPartBlock);
 }
 
 template <typename KT>
@@ -237,8 +238,11 @@ template <typename KT, bool W, bool BIG = false> struct Tile {
     static constexpr int kPer = kKeys / kPartBlock;
 };
 
+// OKM_PART_BLOCK=512 builds: two workgroups per CU (half-size tiles), so one
+// workgroup's loads overlap the other's LDS phases and stores; <= 128 VGPRs
 template <typename KT, bool W, bool BIG = false>
-__global__ __launch_bounds__(kPartBlock) void k_part_scatter_tile(
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(kPartBlock == 512 ? 4 : 1)))
+void k_part_scatter_tile(
     const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
     uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
     uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts, const ull *__restrict__ cap_end,

@@ -1,5 +1,5 @@
 cd $GRAFT_REPO_ROOT
-B="python bench.py --steps 20 --warmup 3 --cpu-sample-reads 0 --cpu-mt-reads 0 --no-timing"
+B="python bench.py --c3-steps 0 --steps 20 --warmup 3 --cpu-sample-reads 0 --cpu-mt-reads 0 --no-timing"
 for i in 1 2; do
   for cfg in "0 3" "3 3" "2 2" "4 4"; do
     set -- $cfg

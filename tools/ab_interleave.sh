@@ -8,7 +8,7 @@ reps=$1; shift
 for r in $(seq 1 "$reps"); do
   for n in "$@"; do
     if [ "$n" = main ]; then lib=orion-kmer_amd/build/liborion_kmer.so; else lib=orion-kmer_amd/build_$n/liborion_kmer.so; fi
-    OKM_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 2 --cpu-sample-reads 0 --cpu-mt-reads 0 \
+    OKM_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 2 --cpu-sample-reads 0 --cpu-mt-reads 0 --c3-steps 0 \
       > gpurun_out/abi/${n}_$r.json 2> gpurun_out/abi/${n}_$r.err || exit 1
   done
 done

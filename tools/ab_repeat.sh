@@ -8,7 +8,7 @@ for r in $(seq 1 $reps); do
   args=("$@")
   for ((i=0; i<${#args[@]}; i+=2)); do
     n=${args[i]}; e=${args[i+1]}
-    env $e timeout -k 10 200 python bench.py --steps 5 --warmup 2 --cpu-sample-reads 0 > gpurun_out/ab/${n}_$r.json 2> gpurun_out/ab/${n}_$r.err || exit 1
+    env $e timeout -k 10 200 python bench.py --c3-steps 0 --steps 5 --warmup 2 --cpu-sample-reads 0 > gpurun_out/ab/${n}_$r.json 2> gpurun_out/ab/${n}_$r.err || exit 1
   done
 done
 for f in gpurun_out/ab/*_[0-9]*.json; do
