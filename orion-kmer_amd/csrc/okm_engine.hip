@@ -901,7 +901,10 @@ struct Part {
     uint32_t consumed;
 };
 
-static const uint64_t kChunkKeys = 1u << 16;
+#ifndef OKM_PART_CHUNK  // keys per partition chunk (a multiple of the scatter tiles)
+#define OKM_PART_CHUNK 65536
+#endif
+static const uint64_t kChunkKeys = OKM_PART_CHUNK;
 
 // Output of one partition pass: a level array whose bins are the children, in
 // key order, of the parts that took part (offsets stay on the device).

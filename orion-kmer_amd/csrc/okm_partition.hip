@@ -227,27 +227,31 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(
 // Tile variant: every 64-Ki-key chunk is processed in LDS tiles that are
 // counting-sorted by local bin, and each bin's run leaves as one contiguous
 // stretch of the chunk's exact slice (no padding, no append rounds).
-template <typename KT, bool W, bool BIG = false> struct Tile {
+#ifndef OKM_PART_TILE_XL  // u64 unweighted passes of <= 512 bins: tiles of this many keys (0: off)
+#define OKM_PART_TILE_XL 0
+#endif
+template <typename KT, bool W, bool BIG = false, bool XL = false> struct Tile {
     // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state; BIG
     // (2048 bins: 32 KiB of per-bin state): 120 KiB of staged keys
 #ifndef OKM_PART_TILE_KEYS
 #define OKM_PART_TILE_KEYS 16384
 #endif
-    static constexpr int kKeys = BIG ? 15 * kPartBlock
+    static constexpr int kKeys = XL ? (OKM_PART_TILE_XL ? OKM_PART_TILE_XL : OKM_PART_TILE_KEYS)
+                                : BIG ? 15 * kPartBlock
                                      : ((W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : OKM_PART_TILE_KEYS));
     static constexpr int kPer = kKeys / kPartBlock;
 };
 
 // OKM_PART_BLOCK=512 builds: two workgroups per CU (half-size tiles), so one
 // workgroup's loads overlap the other's LDS phases and stores; <= 128 VGPRs
-template <typename KT, bool W, bool BIG = false>
+template <typename KT, bool W, bool BIG = false, bool XL = false>
 __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(kPartBlock == 512 ? 4 : 1)))
 void k_part_scatter_tile(
     const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
     uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
     uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts, const ull *__restrict__ cap_end,
     ull *__restrict__ ovf) {
-    constexpr int T = Tile<KT, W, BIG>::kKeys, P = Tile<KT, W, BIG>::kPer;
+    constexpr int T = Tile<KT, W, BIG, XL>::kKeys, P = Tile<KT, W, BIG, XL>::kPer;
     constexpr uint32_t BPT = BIG ? 2 : 1;  // bins per thread in the scan / claim phase
     extern __shared__ __attribute__((aligned(16))) ull lds[];
     KT *stage = reinterpret_cast<KT *>(lds);                              // [T]
@@ -414,6 +418,9 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
                                       hipFuncAttributeMaxDynamicSharedMemorySize, optin);
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, optin);
+            if (OKM_PART_TILE_XL)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, false, true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, optin);
             (void)hipGetLastError();
             attr_tile = true;
         }
@@ -424,6 +431,14 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
             hipLaunchKernelGGL((k_part_scatter_tile<KT, W, true>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
                                (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
                                cap_end, ovf);
+            return;
+        }
+        if (OKM_PART_TILE_XL && !W && sizeof(KT) == 8 && max_local <= 512u) {  // longer runs where they fit
+            constexpr int T = Tile<KT, W, false, true>::kKeys;
+            const size_t lds = (size_t)T * sizeof(KT) + bin_state;
+            hipLaunchKernelGGL((k_part_scatter_tile<KT, W, false, true>), dim3(part_grid(nchunks)), dim3(kPartBlock),
+                               lds, (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys,
+                               out_counts, cap_end, ovf);
             return;
         }
         constexpr int T = Tile<KT, W>::kKeys;
