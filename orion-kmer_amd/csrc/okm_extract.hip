@@ -32,6 +32,13 @@ namespace okm {
 __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
     return shift >= 64 ? 0u : (uint32_t)(key >> shift);
 }
+// K >= 21 (compile time): shift = 2K - l1_bits lies in [33, 55] (l1_bits <= 9),
+// so the bin is a 32-bit shift of the key's high word
+template <int K>
+__device__ __forceinline__ uint32_t bin_k(uint64_t key, uint32_t shift) {
+    if (K >= 21) return (uint32_t)(key >> 32) >> (shift - 32u);
+    return bin_of(key, shift);
+}
 
 #ifndef OKM_EXTRACT_BLOCK
 #define OKM_EXTRACT_BLOCK 1024
@@ -67,6 +74,7 @@ static_assert(kHTile % kTile == 0, "scatter tile must divide the hist tile");
 #define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
 #endif
 constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
+static_assert(2 * 21 - OKM_L1_BITS >= 32, "bin_k: the L1 shift of k >= 21 lies in the key's high word");
 #ifndef OKM_L1_BITS_W  // first-level bins of the k in 33..64 extraction (2^bits <= OKM_WIDE_SCAT_BLOCK)
 #define OKM_L1_BITS_W 9  // 8: k=63 1 Gbases 39.3 vs 34.8 ms (children past one fan-out job), C4 248 vs 237 ms
 #endif
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *_
         const uint64_t w0 = t0 + (uint64_t)threadIdx.x * kSegH;
         if (w0 < end)
             scan_windows<kSegH, K>(seq, g.n, w0, g.k, [&](int, uint64_t key, bool valid) {
-                atomicAdd(&lh[valid ? bin_of(key, shift) : nb], 1u);
+                atomicAdd(&lh[valid ? bin_k<K>(key, shift) : nb], 1u);
             });
     }
     lds_sync();
@@ -132,6 +140,22 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
     }
 }
 
+#ifndef OKM_EXTRACT_SHARE  // scatter: each thread codes only its own 16 bytes; the 32-byte halo comes from LDS
+#define OKM_EXTRACT_SHARE 0  // measured: no change (1.483 vs 1.474 ms), 2 VGPRs spill
+#endif
+constexpr bool kShareCodes = OKM_EXTRACT_SHARE && kSegS == 16 && OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE;
+
+// The 16 bytes at w0 as (MSB-first codes, LSB-first complemented codes,
+// invalid-base bits, 0); bytes at or past n are invalid (the clamped load read
+// other bytes there).
+__device__ __forceinline__ uint4 own_codes(const WinWords<kSegS, 0> &b, uint64_t n, uint64_t w0) {
+    Codes<1> c;
+    make_codes<1, false>(b.w, c);
+    const uint64_t avail = w0 < n ? n - w0 : 0;
+    if (avail < 16) mark_tail<1>(c, avail);
+    return make_uint4(c.p[0], c.q[0], (uint32_t)c.bad[0] & 0xFFFFu, 0u);
+}
+
 template <int K>
 __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_EXTRACT_WPE))) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
                                                                    const uint32_t *__restrict__ HC,
@@ -145,6 +169,9 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
     __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
     __shared__ uint32_t lcur[kMaxL1Bins];
     __shared__ ull wsum[kScatBlock / 64];
+    // shared codes: thread t's 16 bytes as (fwd codes, rc codes, invalid bits);
+    // [kScatBlock, +2): the 32 bytes after the tile (the last two threads' halo)
+    __shared__ uint4 xcode[kShareCodes ? kScatBlock + 2 : 1];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     // HC: exact per-block counts (one claim per bin for the whole chunk);
@@ -158,12 +185,28 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     WinWords<kSegS> ww;  // this tile's bytes, loaded one tile ahead (branch-free: load_windows_clamped)
-    if (OKM_EXTRACT_PREFETCH) load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
+    WinWords<kSegS, 0> own, extra;  // kShareCodes: this thread's 16 bytes; the halo after the tile (last two threads)
+    // the extra 16 B: threads kScatBlock-2.. load the 32 bytes after the tile; the others
+    // reload their own (a cached line: the load stays unconditional and branch-free)
+    auto extra_at = [&](uint64_t tt0) -> uint64_t {
+        return t >= (uint32_t)kScatBlock - 2 ? tt0 + kTile + (uint64_t)kSegS * (t - (kScatBlock - 2))
+                                              : tt0 + (uint64_t)t * kSegS;
+    };
+    if (kShareCodes) {
+        load_windows_clamped<kSegS, 0>(seq, g.n, beg + (uint64_t)t * kSegS, own);
+        load_windows_clamped<kSegS, 0>(seq, g.n, extra_at(beg), extra);
+    } else if (OKM_EXTRACT_PREFETCH) {
+        load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
+    }
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
         for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
-        lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
+        if (kShareCodes) {  // every thread codes its own 16 bytes once; neighbours read them from LDS
+            xcode[t] = own_codes(own, g.n, w0);
+            if (t >= (uint32_t)kScatBlock - 2) xcode[t + 2] = own_codes(extra, g.n, extra_at(t0));
+        }
+        lds_sync();
         const bool live = w0 < end;
         uint32_t tile_n;
         {  // one sweep: keys and their within-bin ranks stay in registers
@@ -172,20 +215,42 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
             uint32_t vm = 0;         // valid windows
 #pragma unroll
             for (int j = 0; j < kSegS / 2; ++j) rk[j] = 0;
-            if (!OKM_EXTRACT_PREFETCH && live) load_windows_clamped<kSegS>(seq, g.n, w0, ww);
-            if (live)
-                scan_words<kSegS, K>(
-                    ww, g.k,
-                    [&](int j, uint64_t key, bool valid) {
-                        const uint32_t b = valid ? bin_of(key, shift) : nb;
-                        kk[j] = key;
-                        rk[j >> 1] |= (atomicAdd(&hist[b], 1u) & 0xFFFFu) << (16 * (j & 1));
-                        vm |= valid ? 1u << j : 0u;
-                    },
-                    g.n - w0);
-            // next tile, in flight meanwhile; unconditional (a clamped load past the
-            // end is harmless), so the loaded registers need no merge copies
-            if (OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE) load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
+            auto emit = [&](int j, uint64_t key, bool valid) {
+                const uint32_t b = valid ? bin_k<K>(key, shift) : nb;
+                kk[j] = key;
+                rk[j >> 1] |= (atomicAdd(&hist[b], 1u) & 0xFFFFu) << (16 * (j & 1));
+                vm |= valid ? 1u << j : 0u;
+            };
+            if (kShareCodes) {
+                if (live) {
+                    constexpr int NP = WinWords<kSegS>::kLoad / 16;  // 3: own 16 bytes + a 32-byte halo
+                    Codes<NP> c;
+                    uint64_t bad = 0;
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        const uint4 x = xcode[t + i];
+                        c.p[i] = x.x;
+                        c.q[i] = x.y;
+                        bad |= (uint64_t)x.z << (16 * i);
+                    }
+                    c.bad[0] = bad;
+                    c.bad[1] = 0;
+                    const uint32_t k = K ? (uint32_t)K : g.k;
+                    const uint32_t inv = invalid_windows<kSegS, NP>(c, k);
+#pragma unroll
+                    for (int j = 0; j < kSegS; ++j) emit(j, window_key_nv(c, j, k), ((inv >> j) & 1u) == 0);
+                }
+                // next tile's bytes, in flight meanwhile
+                load_windows_clamped<kSegS, 0>(seq, g.n, w0 + kTile, own);
+                load_windows_clamped<kSegS, 0>(seq, g.n, extra_at(t0 + kTile), extra);
+            } else {
+                if (!OKM_EXTRACT_PREFETCH && live) load_windows_clamped<kSegS>(seq, g.n, w0, ww);
+                if (live) scan_words<kSegS, K>(ww, g.k, emit, g.n - w0);
+                // next tile, in flight meanwhile; unconditional (a clamped load past the
+                // end is harmless), so the loaded registers need no merge copies
+                if (OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE)
+                    load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
+            }
             lds_sync();
             tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
             // sampled capacities: issue this tile's claim now, consume it after the staging
@@ -199,7 +264,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) {
                 const uint32_t rank = (rk[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                const uint32_t dst = (vm >> j) & 1u ? lofs[bin_of(kk[j], shift)] + rank : (uint32_t)kTile + (t & 63u);
+                const uint32_t dst = (vm >> j) & 1u ? lofs[bin_k<K>(kk[j], shift)] + rank : (uint32_t)kTile + (t & 63u);
                 if (OKM_EXTRACT_EXPT != 2 || kk[j] == 0x123456789ull) stage[dst] = kk[j];
             }
             if (!HC && t < nb) {
@@ -215,7 +280,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
         // each bin's keys are contiguous in `stage` and go to a contiguous run
         for (uint32_t j = t; j < (OKM_EXTRACT_EXPT == 2 ? 0u : tile_n); j += kScatBlock) {
             const ull key = stage[j];
-            const uint32_t b = bin_of(key, shift);
+            const uint32_t b = bin_k<K>(key, shift);
             const ull gb = gcur[b];
             if (gb != ~0ull && (OKM_EXTRACT_EXPT != 1 || key == 0x123456789ull)) out[gb + (j - lofs[b])] = key;
         }

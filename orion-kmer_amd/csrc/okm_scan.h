@@ -180,14 +180,71 @@ __host__ __device__ __forceinline__ uint64_t bad_low64(const Codes<NP> &c, int j
     return (c.bad[w] >> o) | (c.bad[w + 1] << (64 - o));
 }
 
+// Low 32 bits of (hi:lo) >> s, s in [0, 31]: one v_alignbit_b32.
+__host__ __device__ __forceinline__ uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
+// 32 MSB-first code bits from stream bit s = 2 * base (p[s/32 .. s/32 + 1]).
+template <int NP>
+__host__ __device__ __forceinline__ uint32_t fwd32(const Codes<NP> &c, int s) {
+    const int w = s >> 5, r = s & 31;
+    return r == 0 ? c.p[w] : funnel32(c.p[w], c.p[w + 1], 32u - (uint32_t)r);
+}
+
+// 32 LSB-first complemented code bits from stream bit s (q[s/32 .. s/32 + 1]).
+template <int NP>
+__host__ __device__ __forceinline__ uint32_t rc32(const Codes<NP> &c, int s) {
+    return funnel32(c.q[(s >> 5) + 1], c.q[s >> 5], (uint32_t)(s & 31));
+}
+
+// Canonical k-mer (k <= 32) of window j, validity not checked.  With j and k
+// compile-time constants every word is one funnel shift of two code words
+// (v_alignbit_b32) and a shift or mask: 6 VALU for both strands, where 64-bit
+// shifts of 64-bit slices (fwd_top64 / rc_low64) took ~3x that.
+template <int NP>
+__host__ __device__ __forceinline__ uint64_t window_key_nv(const Codes<NP> &c, int j, uint32_t k) {
+    uint32_t fh = 0, fl, rh = 0, rl;
+    if (2 * k > 32) {
+        fl = fwd32(c, 2 * j + 2 * (int)k - 32);                   // kmer.rs:37-57: bases j+k-16 .. j+k-1
+        fh = fwd32(c, 2 * j) >> (64u - 2 * k);                      // ... and j .. j+k-17
+        rl = rc32(c, 2 * j);                                        // kmer.rs:79-94
+        const uint32_t hb = 2 * k - 32;                             // 2..32 bits in the high word
+        rh = rc32(c, 2 * j + 32) & (hb >= 32 ? ~0u : ((1u << hb) - 1u));
+    } else {
+        fl = fwd32(c, 2 * j) >> (32u - 2 * k);
+        rl = rc32(c, 2 * j) & (2 * k >= 32 ? ~0u : ((1u << (2 * k)) - 1u));
+    }
+    const uint64_t f = ((uint64_t)fh << 32) | fl, r = ((uint64_t)rh << 32) | rl;
+    return f < r ? f : r;  // kmer.rs:99-106
+}
+
 // Canonical k-mer (k <= 32) of window j and its validity.
 template <int NP>
 __host__ __device__ __forceinline__ uint64_t window_key(const Codes<NP> &c, int j, uint32_t k, bool *valid) {
-    const uint64_t kmask = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
-    const uint64_t f = fwd_top64(c, j) >> (64 - 2 * k);  // kmer.rs:37-57
-    const uint64_t r = rc_low64(c, j) & kmask;           // kmer.rs:79-94
     *valid = (bad_low64(c, j) & (k >= 64 ? ~0ull : ((1ull << k) - 1ull))) == 0;
-    return f < r ? f : r;                                // kmer.rs:99-106
+    return window_key_nv(c, j, k);
+}
+
+// Invalid windows among j = 0 .. SEG-1 (bit j: a base of j .. j+k-1 is
+// invalid), for SEG + k - 1 <= 64: an OR over runs of k bits of the
+// per-base invalid bits, by doubling -- ~5 64-bit steps per thread instead of
+// a 64-bit shift, mask and compare per window.
+template <int SEG, int NP>
+__host__ __device__ __forceinline__ uint32_t invalid_windows(const Codes<NP> &c, uint32_t k) {
+    static_assert(SEG + 31 <= 64, "one 64-bit word of invalid bits");
+    uint64_t x = c.bad[0];
+    uint32_t len = 1;
+    while (2 * len <= k) {  // x bit j: any invalid base in j .. j+len-1
+        x |= x >> len;
+        len *= 2;
+    }
+    x |= x >> (k - len);  // j .. j+k-1 (the two runs of len overlap)
+    return (uint32_t)x & (SEG >= 32 ? ~0u : ((1u << SEG) - 1u));
 }
 
 // Canonical k-mer (k in 33..64, K128 {lo, hi} over 2k bits) of window j and
@@ -222,6 +279,12 @@ __device__ __forceinline__ void scan_words(const WinWords<SEG> &ww, uint32_t k_r
     Codes<NP> c;
     make_codes<NP, RAW>(ww.w, c);
     if (avail < (uint64_t)WinWords<SEG>::kLoad) mark_tail<NP>(c, avail);  // the batch's last bytes only
+    if (SEG + 31 <= 64) {  // validity of all SEG windows at once
+        const uint32_t inv = invalid_windows<(SEG + 31 <= 64 ? SEG : 32), NP>(c, k);
+#pragma unroll
+        for (int j = 0; j < SEG; ++j) emit(j, window_key_nv(c, j, k), ((inv >> j) & 1u) == 0);
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < SEG; ++j) {
         bool valid;

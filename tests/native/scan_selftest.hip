@@ -71,6 +71,28 @@ static int check(const unsigned char *buf, int seg, int kmax) {
     return 0;
 }
 
+// invalid_windows (scan_words' all-windows validity mask) against the per-window test
+template <int NP, int SEG, bool RAW>
+static int check_inv(const unsigned char *buf) {
+    uint32_t w[NP * 4];
+    memcpy(w, buf, sizeof(w));
+    Codes<NP> c;
+    make_codes<NP, RAW>(w, c);
+    for (int k = 1; k <= 32; ++k) {
+        const uint32_t inv = invalid_windows<SEG, NP>(c, (uint32_t)k);
+        for (int j = 0; j < SEG; ++j) {
+            unsigned long long hi, lo;
+            const bool nv = naive(buf, j, k, RAW, &hi, &lo);
+            if ((((inv >> j) & 1u) == 0) != nv) {
+                printf("invalid_windows k=%d j=%d seg=%d raw=%d: mask says %d, naive %d\n", k, j, SEG, RAW,
+                       (int)(((inv >> j) & 1u) == 0), nv);
+                return 1;
+            }
+        }
+    }
+    return 0;
+}
+
 int main() {
     srand(12345);
     static const char alpha[] = "ACGTACGTACGTACGTacgtUuNn\n-.~ RYK";
@@ -86,6 +108,7 @@ int main() {
             buf[i] = ch;
         }
         if (check<3, false>(buf, 16, 32) || check<3, true>(buf, 16, 32)) return 1;   // scatter / query
+        if (check_inv<3, 16, false>(buf) || check_inv<3, 16, true>(buf) || check_inv<4, 32, false>(buf)) return 1;
         if (check<6, false>(buf, 64, 32)) return 1;                                   // hist
         if (check<5, false>(buf, 16, 64) || check<8, false>(buf, 64, 64)) return 1;   // wide
     }
