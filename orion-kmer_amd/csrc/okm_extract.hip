@@ -143,6 +143,10 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
 #ifndef OKM_EXTRACT_SHARE  // scatter: each thread codes only its own 16 bytes; the 32-byte halo comes from LDS
 #define OKM_EXTRACT_SHARE 0  // measured: no change (1.483 vs 1.474 ms), 2 VGPRs spill
 #endif
+#ifndef OKM_EXTRACT_STORE_NOWAIT
+#define OKM_EXTRACT_STORE_NOWAIT 0  // measured: 1.495 vs 1.476 ms (no gain)
+#endif
+constexpr unsigned kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0), expcnt / lgkmcnt not waited (gfx9 encoding)
 constexpr bool kShareCodes = OKM_EXTRACT_SHARE && kSegS == 16 && OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE;
 
 // The 16 bytes at w0 as (MSB-first codes, LSB-first complemented codes,
@@ -199,6 +203,9 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
         load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     }
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
+    // (the first tile's bytes: no loop-carried load is then pending at the loop head,
+    // so the head does not wait for the previous tile's stores; see the copy-out)
+    if (OKM_EXTRACT_STORE_NOWAIT) __builtin_amdgcn_s_waitcnt(kWaitVm0);
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
         for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
@@ -276,6 +283,10 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
         // late prefetch: after the claim's returning atomic was consumed (vmcnt
         // retires in order, so waiting for the claim waits for any load before it)
         if (OKM_EXTRACT_PREFETCH && OKM_EXTRACT_PF_LATE) load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
+        // the next tile's bytes are waited for HERE, before this tile's stores: vmcnt
+        // retires in issue order, so a wait at the next tile's first use would also
+        // wait for every store of the copy-out below to complete
+        if (OKM_EXTRACT_STORE_NOWAIT) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         lds_sync();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
         for (uint32_t j = t; j < (OKM_EXTRACT_EXPT == 2 ? 0u : tile_n); j += kScatBlock) {
