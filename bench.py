@@ -288,10 +288,25 @@ def main():
     def exchange_merge(c, n, release):
         return merge_runs(mergers[0], exchange_only(c, n, release))
 
-    def merge_owned(i, c, release):
+    def count_batch_joined(c):
+        """count_batch for the RCCL path: a failed count is handed to the
+        merge (below) instead of raised on the worker thread, so this rank still
+        takes part in that merge's collectives and every rank fails together."""
+        try:
+            return count_batch(c)
+        except Exception as e:
+            return e
+
+    def merge_owned(i, c, release, counted=None):
         """okm_merge_owned: this rank's key range of every rank's table of
         batch i, into merge context i % 2 (the library's RCCL path)."""
-        n_m = comm.merge_owned(c, mergers[i % 2])
+        try:
+            n_m = comm.merge_owned(c, mergers[i % 2])
+        except Exception:
+            if not isinstance(counted, Exception):
+                raise
+        if isinstance(counted, Exception):
+            raise counted
         release()
         t = comm.last_times()
         xt[0] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
@@ -330,8 +345,8 @@ def main():
                 raise err[0]
             return res[-1]
         if comm is not None:
-            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
-                                         lambda i, j, n, release: merge_owned(i, ctrs[j], release))
+            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch_joined(ctrs[j]),
+                                         lambda i, j, n, release: merge_owned(i, ctrs[j], release, n))
         elif merge_thread:
             res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
                                          lambda i, j, n, release: exchange_only(ctrs[j], n, release),
@@ -522,9 +537,31 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
     nreads = r1 - r0
     stride = READ_LEN + 1
     t0 = time.time()
-    dbuf = okm.DeviceBuffer(max(1, nreads * stride), device)
-    okm.synth_reads_device(dbuf.address, nreads, READ_LEN, genome_len=args.c3_genome_bp, genome_seed=C3_SEED,
-                           seed=C3_SEED, first_read=r0, sub_rate=0.001, n_rate=0.0001, device=device)
+    dbuf = ctr = merger = None
+    setup_err = None
+    try:
+        dbuf = okm.DeviceBuffer(max(1, nreads * stride), device)
+        okm.synth_reads_device(dbuf.address, nreads, READ_LEN, genome_len=args.c3_genome_bp, genome_seed=C3_SEED,
+                               seed=C3_SEED, first_read=r0, sub_rate=0.001, n_rate=0.0001, device=device)
+        ctr = okm.KmerCounter(K, "count", device)
+        # the owner's merge reuses the counting context (okm_merge_owned allows
+        # owner == local): one device pool per rank, no cross-context trimming
+        merger = (ctr if comm is not None else okm.KmerCounter(K, "count", device)) if dist_on else None
+    except Exception as e:
+        setup_err = e
+    if dist_on:  # every rank learns whether all could set up, before any collective of the merge
+        bad = torch.tensor([0 if setup_err is None else 1], dtype=torch.int64)
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+        if int(bad.item()) and setup_err is None:
+            setup_err = RuntimeError(f"C3 setup failed on {int(bad.item())} rank(s)")
+    if setup_err is not None:
+        if merger is not None and merger is not ctr:
+            merger.close()
+        if ctr is not None:
+            ctr.close()
+        if dbuf is not None:
+            dbuf.free()
+        raise setup_err
     batches = []
     for b0 in range(0, nreads, args.batch_reads):
         b1 = min(nreads, b0 + args.batch_reads)
@@ -532,23 +569,34 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
     log(f"[rank {rank}] C3 shard: reads [{r0}, {r1}) = {nreads * READ_LEN} bases in {len(batches)} batches, "
         f"generated on the device ({time.time() - t0:.1f}s)")
 
-    ctr = okm.KmerCounter(K, "count", device)
-    # the owner's merge reuses the counting context (okm_merge_owned allows
-    # owner == local): one device pool per rank, no cross-context trimming
-    merger = (ctr if comm is not None else okm.KmerCounter(K, "count", device)) if dist_on else None
     xt = [0.0, 0.0, 0.0]  # count, exchange, merge (wall, this rank)
 
     def step():
         tc = time.perf_counter()
-        ctr.reset()
-        for off, nb in batches:
-            ctr.add_device_batch(dbuf.address + off, nb)
-        n = ctr.count()
+        err = None
+        try:
+            ctr.reset()
+            for off, nb in batches:
+                ctr.add_device_batch(dbuf.address + off, nb)
+            n = ctr.count()
+        except Exception as e:
+            if comm is None:
+                raise
+            # still take part in the merge's collectives: okm_merge_owned agrees
+            # on the failure (status word) and every rank returns an error
+            # instead of the others blocking in a collective this rank never joins
+            err = e
         xt[0] += time.perf_counter() - tc
         if not dist_on:
             return n
         if comm is not None:
-            n_m = comm.merge_owned(ctr, merger)
+            try:
+                n_m = comm.merge_owned(ctr, merger)
+            except Exception:
+                if err is None:
+                    raise
+            if err is not None:
+                raise err
             t = comm.last_times()
             xt[1] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
             xt[2] += t["merge_ms"] * 1e-3
