@@ -274,8 +274,10 @@ int okm_comm_size(const okm_comm *comm);
 /* Collective over every rank of `comm`: `local` (counted or not) holds this
  * rank's shard; afterwards `owner` (reset first) holds this rank's key range
  * of the union of all ranks' tables, counted and sorted, and *n_owned its
- * distinct keys.  local, owner and comm share one device; k <= 32; owner may
- * be local itself (its table is only read until the exchange completes).
+ * distinct keys.  local, owner and comm share one device and k; k > 32
+ * contexts (OKM_MODE_WIDE) move their K128 keys as u64 word pairs (never as
+ * 5-byte deltas); owner may be local itself (its table is only read until
+ * the exchange completes).
  * Set-mode contexts exchange keys only (build.rs / compare.rs sets).  The
  * owner keeps no pointer into local or the communicator afterwards: it may
  * take more input, and local may be reset.  A rank that fails between the
@@ -309,7 +311,7 @@ okm_status okm_owner_bounds(const uint64_t *hist, uint32_t nbins, int world, uin
  * returns); okm_group_count merges the GPUs' tables by key-range owner
  * (okm_merge_owned over okm_comm_init_all communicators).  n_gpus <= 0: every
  * visible device; 1: no RCCL at all.  devices: the n_gpus ordinals (NULL:
- * 0..n_gpus-1).  k > 32 (OKM_MODE_WIDE) only with one GPU. */
+ * 0..n_gpus-1).  k > 32 (OKM_MODE_WIDE) too: its K128 keys cross as word pairs. */
 typedef struct okm_group okm_group;
 okm_status okm_group_create(okm_group **out, uint8_t k, okm_mode mode, int n_gpus, const int *devices,
                             uint64_t distinct_hint);

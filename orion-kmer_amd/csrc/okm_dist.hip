@@ -690,7 +690,8 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     }
     // host sources of async copies: live until the sync below
     const ull one = 1;
-    const ull wd = want_deltas(P) ? 1 : 0;  // 1: deltas wanted (forced or auto), agreed below
+    const bool wide = ctx_is_wide(tabs[0].local);  // K128 keys (k > 32): u64 word pairs, never deltas
+    const ull wd = want_deltas(P) && !wide ? 1 : 0;  // 1: deltas wanted (forced or auto), agreed below
     okm_status st = OKM_OK;
     for (size_t i = 0; i < nt && st == OKM_OK; ++i)  // counts the local shards if needed (synchronous)
         st = okm_result_device(tabs[i].local, &tabs[i].dk, &tabs[i].dc, &tabs[i].n);
@@ -700,7 +701,7 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     if (st == OKM_OK) {
         for (size_t i = 0; i < nt; ++i) {
             ull *st_i = m->starts.as<ull>() + i * (nb + 1);
-            launch_bin_bounds(s, tabs[i].dk, tabs[i].n, shift, nb, st_i, false);
+            launch_bin_bounds(s, tabs[i].dk, tabs[i].n, shift, nb, st_i, wide);
             hipLaunchKernelGGL(k_hist_from_starts, dim3((nb + 255) / 256), dim3(256), 0, s, st_i, nb,
                                m->hist.as<ull>());
             HIP_TRY(hipGetLastError());
@@ -742,6 +743,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     Transport &tp = *m->tp;
     const uint64_t *dk = t.dk, *dc = t.dc;
     const uint64_t n = t.n;
+    const uint64_t kw = ctx_is_wide(local) ? 2 : 1;  // u64 words per key (K128 keys travel as word pairs)
     // host sources of async copies live until the stream is synchronised
     ull bad = 0;
     std::vector<ull> esc_offs(4 * (P + 1));
@@ -817,7 +819,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
 
     // receive buffers and the escapes, then one more status word: a rank that
     // cannot allocate them tells its peers before any send is posted
-    st = m->rk.ensure(std::max<uint64_t>(nrecv, 1) * sizeof(uint64_t));
+    st = m->rk.ensure(std::max<uint64_t>(nrecv, 1) * kw * sizeof(uint64_t));
     if (!set) {
         if (st == OKM_OK) st = m->rlow.ensure(std::max<uint64_t>(nrecv, 16));
         if (st == OKM_OK) st = m->resc.ensure(std::max<uint64_t>(2 * nresc, 2) * sizeof(uint64_t));
@@ -884,8 +886,8 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
             add(true, m->kesc.as<uint64_t>() + 2 * ksoff[r], 2 * ks[r], 8, r);
             add(false, m->rkesc.as<uint64_t>() + 2 * kroff[r], 2 * kr[r], 8, r);
         } else {
-            add(true, dk + cut[r], ss[r], 8, r);
-            add(false, m->rk.as<uint64_t>() + roff[r], rs[r], 8, r);
+            add(true, dk + kw * cut[r], kw * ss[r], 8, r);
+            add(false, m->rk.as<uint64_t>() + kw * roff[r], kw * rs[r], 8, r);
         }
         if (!set) {
             add(true, m->low.as<uint8_t>() + cut[r], ss[r], 1, r);
@@ -894,7 +896,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
             add(false, m->resc.as<uint64_t>() + 2 * reoff[r], 2 * er[r], 8, r);
         }
         if (r != me) {
-            const uint64_t kb = deltas ? 5 : 8;
+            const uint64_t kb = deltas ? 5 : 8 * kw;
             bytes_out += ss[r] * (kb + (set ? 0 : 1)) + (set ? 0 : 16 * es[r]) + (deltas ? 16 * ks[r] : 0);
             bytes_in += rs[r] * (kb + (set ? 0 : 1)) + (set ? 0 : 16 * er[r]) + (deltas ? 16 * kr[r] : 0);
         }
@@ -908,7 +910,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
         for (uint32_t b = 0; b < P; ++b) {  // a == b too: whether a rank's owner borrows is its own choice
             const uint64_t pairs = h_g[(size_t)a * row + b], ce = h_g[(size_t)a * row + P + b],
                            ke = h_g[(size_t)a * row + 2 * P + b];
-            uint64_t big = pairs * (deltas ? 5 : 8);
+            uint64_t big = pairs * (deltas ? 5 : 8 * kw);
             if (!set) big = std::max(big, std::max<uint64_t>(pairs, 16 * ce));
             if (deltas) big = std::max<uint64_t>(big, 16 * ke);
             npieces = std::max<uint64_t>(npieces, (big + piece - 1) / piece);
@@ -967,11 +969,11 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     OKM_TRY(okm_reset(owner));
     for (uint32_t r = 0; r < P; ++r) {
         if (r == me && self_borrow && self_n) {
-            OKM_TRY(okm_add_sorted_pairs_device(owner, dk + cut[me], set ? nullptr : dc + cut[me], self_n));
+            OKM_TRY(okm_add_sorted_pairs_device(owner, dk + kw * cut[me], set ? nullptr : dc + cut[me], self_n));
             continue;
         }
         if (!rs[r]) continue;
-        OKM_TRY(okm_add_sorted_pairs_device(owner, m->rk.as<uint64_t>() + roff[r],
+        OKM_TRY(okm_add_sorted_pairs_device(owner, m->rk.as<uint64_t>() + kw * roff[r],
                                             set ? nullptr : m->rc.as<uint64_t>() + roff[r], rs[r]));
     }
     uint64_t nd = 0;
@@ -1145,8 +1147,10 @@ okm_status okm_merge_owned_n(okm_ctx *const *locals, okm_comm *m, okm_ctx *const
             return fail(OKM_E_ARG, "okm_merge_owned: local, owner and communicator must share one device");
         // owner == local is allowed (and cheapest: one context, one device
         // pool): the local table is only read until the exchange has completed
-        if (ctx_is_wide(local) || ctx_is_wide(owner) || ctx_k(local) != ctx_k(owner) || ctx_k(local) != ctx_k(locals[0]))
-            return fail(OKM_E_ARG, "okm_merge_owned: k must match and be <= 32");
+        // k > 32: K128 keys (two u64 words a key) on the wire, never 5-byte deltas
+        if (ctx_k(local) != ctx_k(owner) || ctx_k(local) != ctx_k(locals[0]) ||
+            ctx_is_wide(local) != ctx_is_wide(owner) || ctx_is_wide(local) != ctx_is_wide(locals[0]))
+            return fail(OKM_E_ARG, "okm_merge_owned: every table must have the same k (and key width)");
         for (int j = 0; j < i; ++j)
             if (owners[j] == owner || owners[j] == local || locals[j] == owner)
                 return fail(OKM_E_ARG, "okm_merge_owned_n: every table needs its own contexts");

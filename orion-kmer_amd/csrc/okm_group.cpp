@@ -115,8 +115,6 @@ okm_status okm_group_create(okm_group **out, uint8_t k, okm_mode mode, int n_gpu
     if (n > avail)
         return okm::fail(OKM_E_ARG, "okm_group_create: " + std::to_string(n) + " GPUs asked, " + std::to_string(avail) +
                                         " visible");
-    if (n > 1 && ((mode & OKM_MODE_WIDE) != 0 && k > 32))
-        return okm::fail(OKM_E_ARG, "okm_group_create: k > 32 counts on one GPU (the exchange moves u64 keys)");
     okm_group *g = new okm_group();
     g->k = k;
     g->mode = mode;

@@ -119,6 +119,36 @@ def test_merge_owned_argument_errors(comm1):
     with okm.KmerCounter(21) as a, okm.KmerCounter(25) as b:
         with pytest.raises(okm.OkmError):
             comm1.merge_owned(a, b)  # k mismatch
+    with okm.KmerCounter(45, wide=True) as a, okm.KmerCounter(63, wide=True) as b:
+        with pytest.raises(okm.OkmError):
+            comm1.merge_owned(a, b)  # k mismatch among K128 contexts
+
+
+@pytest.mark.parametrize("piece", ["", "4104"])  # 4,104 B = 513 words: pieces split keys' word pairs
+def test_merge_owned_wide_rccl(comm1, monkeypatch, piece):
+    """k = 63 (K128 keys): the slices cross RCCL as u64 word pairs, the owner
+    counts them; exact against the restatement (one rank: self send/recv)."""
+    if piece:
+        monkeypatch.setenv("OKM_RCCL_PIECE", piece)
+    from oracle import OracleCounterWide
+    k = 63
+    b = _batch(30_000, 200_000, 9)
+    b.reshape(30_000, 151)[::20, :150] = ord("A")  # a hot key: counts past the one-byte escape
+    ref = OracleCounterWide(k)
+    ref.add_separated_range(b, 0, 0, 1)
+    ek, ec = ref.result(1)
+    assert (ec > 255).any()
+    buf = okm.DeviceBuffer(len(b))
+    buf.upload(b)
+    with okm.KmerCounter(k, wide=True) as local, okm.KmerCounter(k, wide=True) as owner:
+        local.add_device_batch(buf.address, len(b))
+        n = comm1.merge_owned(local, owner)
+        gk, gc = owner.result(1)
+        sent, recv = comm1.last_bytes()
+    buf.free()
+    assert n == len(ec)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert sent == recv == 0  # one rank: the self slice is borrowed, nothing crosses a link
 
 
 def test_merge_owned_into_local_context(comm1):

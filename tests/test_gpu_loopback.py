@@ -70,13 +70,13 @@ def _oracle(recs, k):
     return oc.result(1)
 
 
-def _merge_case(P, k, shards, owner_mode, mode="count"):
+def _merge_case(P, k, shards, owner_mode, mode="count", wide=False):
     """Every rank counts its shard and merges; returns [(keys, counts, n_owned)]."""
     comms = okm.Comm.init_loopback(P, 0)
 
     def rank(r):
-        local = okm.KmerCounter(k, mode)
-        owner = local if owner_mode == "local" else okm.KmerCounter(k, mode)
+        local = okm.KmerCounter(k, mode, wide=wide)
+        owner = local if owner_mode == "local" else okm.KmerCounter(k, mode, wide=wide)
         buf = None
         try:
             if len(shards[r]):
@@ -370,3 +370,53 @@ def test_loopback_wire_deltas_multi_piece_set_mode(monkeypatch):
     ek, _ = _oracle(recs, k)
     res = _merge_case(P, k, _shards(recs, P), "local", mode="set")
     _check_ranges(res, ek, None, with_counts=False)
+
+
+# ---------------------------------------------------------------------------
+# k > 32 (K128 keys, the two-u64 extension of BASELINE configs[3]): the keys
+# cross as u64 word pairs (never 5-byte deltas); the same plan, count bytes,
+# escapes and owner merge
+# ---------------------------------------------------------------------------
+
+def _oracle_wide(recs, k):
+    from oracle import OracleCounterWide
+    oc = OracleCounterWide(k)
+    oc.add_separated_range(np.ascontiguousarray(recs).reshape(-1), 0, 0, 1)  # 0 key bits: every key
+    return oc.result(1)
+
+
+def _check_ranges_wide(res, ek, ec):
+    keys = np.concatenate([r[0].reshape(-1, 2) for r in res])
+    assert np.array_equal(keys, ek)  # rank order = the sorted global table
+    assert np.array_equal(np.concatenate([r[1] for r in res]), ec)
+    assert [r[2] for r in res] == [len(r[1]) for r in res]
+    ints = [okm.keys128_to_int(r[0]) for r in res]
+    for a, b in zip(ints, ints[1:]):  # contiguous, ascending, disjoint ranges
+        if a and b:
+            assert a[-1] < b[0]
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("k,owner_mode", [(45, "separate"), (63, "local"), (63, "separate")])
+def test_loopback_merge_wide_exact(P, k, owner_mode):
+    recs = _records(20_000, 200_000, 31, hot_every=30)
+    ek, ec = _oracle_wide(recs, k)
+    assert ec.max() > 255  # counts past the one-byte escape
+    res = _merge_case(P, k, _shards(recs, P), owner_mode, wide=True)
+    _check_ranges_wide(res, ek, ec)
+    sent = sum(r[3][0] for r in res)
+    assert sent == sum(r[3][1] for r in res) > 0
+
+
+def test_loopback_merge_wide_multi_piece_empty_rank(monkeypatch):
+    """Small pieces split every 16-B-key message (a piece boundary may fall
+    between a key's two words: the pieces count u64 words), plus an empty rank;
+    OKM_WIRE_DELTAS=1 must not apply to K128 keys."""
+    monkeypatch.setenv("OKM_RCCL_PIECE", "4104")
+    monkeypatch.setenv("OKM_WIRE_DELTAS", "1")
+    k, P = 63, 3
+    recs = _records(15_000, 150_000, 32, hot_every=20)
+    ek, ec = _oracle_wide(recs, k)
+    res = _merge_case(P, k, _shards(recs, P, empty_rank=2), "separate", wide=True)
+    _check_ranges_wide(res, ek, ec)
+    assert max(r[3][0] for r in res) > 20 * 4104
