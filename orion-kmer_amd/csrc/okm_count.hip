@@ -47,6 +47,9 @@ namespace okm {
 #ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
 #define OKM_FULL_RANK 1
 #endif
+#ifndef OKM_FULL_FLAG_ROWS  // full mode: run-start flags from lane-contiguous rows + ballots (1)
+#define OKM_FULL_FLAG_ROWS 1
+#endif
 // OKM_COUNT_PROF=1 builds: thread 0 of every block accumulates clock64()
 // deltas between phase marks (debug/tuning only; okm_debug_count_prof()).
 __device__ unsigned long long g_count_prof[16];
@@ -393,14 +396,34 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         }
         lds_sync();
         PMARK(13);
-        // count.rs:33: a key's count = its run's length (weight); flag run starts
-        KT prev = p0 > 0 && p0 <= ntot ? sk[p0 - 1] : KeyOps<KT>::empty();
+        // count.rs:33: a key's count = its run's length (weight); flag run starts.
+        // The flags are taken in rows of lane-contiguous positions (conflict-free
+        // LDS reads; a thread's own 8 consecutive keys sit 128 B apart from its
+        // neighbours' and read 8-way bank-conflicted as K128) into one ballot
+        // word per wave and row, in the dead home counters
+        if (OKM_FULL_FLAG_ROWS) {
+            uint64_t *fm = reinterpret_cast<uint64_t *>(hc);  // [kCapI / 64] run-start masks
+            static_assert(kCapI / 64 * 8 <= kHomes * 2, "run-start masks fit the home counters");
 #pragma unroll
-        for (int j = 0; j < kPerT; ++j) {
-            if (p0 + j >= ntot) break;
-            const KT x = sk[p0 + j];
-            m |= KeyOps<KT>::eq(x, prev) ? 0u : 1u << j;
-            prev = x;
+            for (int i = 0; i < kPer; ++i) {
+                const uint32_t p = (uint32_t)i * kCB + t;
+                bool f = false;
+                if (p < ntot) f = p == 0 || !KeyOps<KT>::eq(sk[p], sk[p - 1]);
+                const uint64_t b = __ballot(f);
+                if ((t & 63u) == 0) fm[(uint32_t)i * (kCB / 64) + (t >> 6)] = b;
+            }
+            lds_sync();
+            const uint32_t r = p0 % kCB;
+            m = (uint32_t)(fm[(p0 / kCB) * (kCB / 64) + r / 64] >> (r % 64)) & 0xFFu;
+        } else {
+            KT prev = p0 > 0 && p0 <= ntot ? sk[p0 - 1] : KeyOps<KT>::empty();
+#pragma unroll
+            for (int j = 0; j < kPerT; ++j) {
+                if (p0 + j >= ntot) break;
+                const KT x = sk[p0 + j];
+                m |= KeyOps<KT>::eq(x, prev) ? 0u : 1u << j;
+                prev = x;
+            }
         }
     } else {
         // each thread's 4 homes are one slice of sk: sort it and flag the first
