@@ -47,6 +47,9 @@ namespace okm {
 #ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
 #define OKM_FULL_RANK 1
 #endif
+#ifndef OKM_FULL_HB_W  // full mode, K128 keys: home bits (12: 4096 homes, ~1 key each at 4096 instances)
+#define OKM_FULL_HB_W 12
+#endif
 #ifndef OKM_FULL_FLAG_ROWS  // full mode: run-start flags from lane-contiguous rows + ballots (1)
 #define OKM_FULL_FLAG_ROWS 1
 #endif
@@ -308,11 +311,24 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 // full mode (fallback): every instance counting-sorted by home
 // ---------------------------------------------------------------------------
 
-template <bool W, typename KT>
+// Full-mode LDS bytes: keys (+ weights), then the home counters, which the
+// run starts (u16 [kCapI + 1]) reuse once the homes are dead.
+template <bool W, typename KT, int HB>
+constexpr int full_lds_bytes() {
+    return kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + ((1 << HB) * 2 > (kCapI + 16) * 2 ? (1 << HB) * 2 : (kCapI + 16) * 2);
+}
+
+// HB: home bits.  K128 items (k > 32, ~all keys distinct) take 4096 homes, so
+// a home holds ~1 key and each instance's rank scan reads ~1 key (random
+// 16-B LDS reads are the kernel's most bank-conflicted accesses).
+template <bool W, typename KT, int HB = kHomeBits>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
                                               const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
                                               uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
                                               bool nowrite) {
+    constexpr uint32_t kH = 1u << HB;         // homes (key sub-ranges in order)
+    constexpr uint32_t kHW = kH / 2 / kCB;    // u16-pair counter words per thread (2 or 4)
+    static_assert(kHW >= 1 && kH / 2 == kHW * kCB, "whole counter words per thread");
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
@@ -320,10 +336,10 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     KT *sk = reinterpret_cast<KT *>(lds);
     ull *sw = reinterpret_cast<ull *>(sk + kCapI);
     uint32_t *hc = reinterpret_cast<uint32_t *>(sw + (W ? kCapI : 0));
-    uint16_t *first = reinterpret_cast<uint16_t *>(hc + kHomes / 2);  // [D + 1]: run starts in sk
+    uint16_t *first = reinterpret_cast<uint16_t *>(hc);  // [D + 1]: run starts in sk (the homes are dead by then)
     lds_sync();  // the previous item's LDS state is dead
-    hc[2 * t] = 0;
-    hc[2 * t + 1] = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kHW; ++q) hc[kHW * t + q] = 0;
     lds_sync();
     uint32_t hp[kPer];  // home << 16 | pos
 #pragma unroll
@@ -331,19 +347,31 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         if ((uint32_t)u >= nrows) break;  // block-uniform
         hp[u] = 0;
         if (!KeyOps<KT>::is_empty(kk[u])) {
-            const uint32_t h = home_of(kk[u], r);
+            const uint32_t h = (uint32_t)KeyOps<KT>::shr(kk[u], r - HB) & (kH - 1u);  // r > kDenseBits >= HB - 1
             const uint32_t o = atomicAdd(&hc[h >> 1], 1u << half_shift(h));
             hp[u] = (h << 16) | half_of(o, h);
         }
     }
     lds_sync();
-    const uint32_t w0 = hc[2 * t], w1 = hc[2 * t + 1];
-    const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
-    const uint32_t n = c0 + c1 + c2 + (w1 >> 16);
+    uint32_t wv[kHW];
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kHW; ++q) {
+        wv[q] = hc[kHW * t + q];
+        n += (wv[q] & 0xFFFFu) + (wv[q] >> 16);
+    }
     uint32_t ntot;
     const uint32_t a = block_excl_scan32(n, wsum, &ntot);
-    hc[2 * t] = a | ((a + c0) << 16);
-    hc[2 * t + 1] = (a + c0 + c1) | ((a + c0 + c1 + c2) << 16);
+    {
+        uint32_t run = a;
+#pragma unroll
+        for (uint32_t q = 0; q < kHW; ++q) {
+            const uint32_t lo = run;
+            run += wv[q] & 0xFFFFu;
+            hc[kHW * t + q] = lo | (run << 16);
+            run += wv[q] >> 16;
+        }
+    }
     lds_sync();
     PMARK(11);
 #pragma unroll
@@ -375,7 +403,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             if (!KeyOps<KT>::is_empty(kk[u])) {
                 const uint32_t h = hp[u] >> 16;
                 const uint32_t hs = half_of(hc[h >> 1], h);
-                const uint32_t he = h + 1 < (uint32_t)kHomes ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
+                const uint32_t he = h + 1 < kH ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
                 const uint32_t me = hs + (hp[u] & 0xFFFFu);
                 uint32_t rank = hs;
                 for (uint32_t q = hs; q < he; ++q) {
@@ -403,7 +431,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         // word per wave and row, in the dead home counters
         if (OKM_FULL_FLAG_ROWS) {
             uint64_t *fm = reinterpret_cast<uint64_t *>(hc);  // [kCapI / 64] run-start masks
-            static_assert(kCapI / 64 * 8 <= kHomes * 2, "run-start masks fit the home counters");
+            static_assert(kCapI / 64 * 8 <= (int)kH * 2, "run-start masks fit the home counters");
 #pragma unroll
             for (int i = 0; i < kPer; ++i) {
                 const uint32_t p = (uint32_t)i * kCB + t;
@@ -798,7 +826,8 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
                                                     bool nowrite) {
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
-    constexpr int kFull = kCapI * ((int)sizeof(KT) + (W ? 8 : 0)) + kHomes * 2 + (kCapI + 16) * 2;
+    constexpr int kHB = sizeof(KT) > 8 ? OKM_FULL_HB_W : kHomeBits;  // full-mode home bits
+    constexpr int kFull = full_lds_bytes<W, KT, kHB>();
     constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
     constexpr int kBytes = kFull > kDense ? kFull : kDense;
     __shared__ __attribute__((aligned(16))) ull lds[kBytes / 8];
@@ -862,7 +891,7 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
         if (it.rem_bits <= (uint32_t)kDenseBits) {
             written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite);
         } else if (total <= (uint64_t)kCapI) {
-            written = full_item<W, KT>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
+            written = full_item<W, KT, kHB>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
                                        out_counts, nowrite);
         } else if (threadIdx.x == 0) {
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
