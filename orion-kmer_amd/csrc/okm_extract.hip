@@ -435,6 +435,18 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const ui
 #ifndef OKM_WIDE_SWEEP1
 #define OKM_WIDE_SWEEP1 1
 #endif
+#ifndef OKM_WIDE_SHARE  // single sweep: each thread codes its own 16 bytes once (halo codes from LDS)
+#define OKM_WIDE_SHARE 1
+#endif
+// The 16 bytes at w0 as (MSB-first codes, LSB-first complemented codes,
+// invalid-base bits, 0); bytes at or past n are invalid.
+__device__ __forceinline__ uint4 slot_codes(const uint32_t (&w)[4], uint64_t n, uint64_t w0) {
+    Codes<1> c;
+    make_codes<1, false>(w, c);
+    const uint64_t avail = w0 < n ? n - w0 : 0;
+    if (avail < 16) mark_tail<1>(c, avail);
+    return make_uint4(c.p[0], c.q[0], (uint32_t)c.bad[0] & 0xFFFFu, 0u);
+}
 __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uint8_t *__restrict__ seq,
                                                                          ExtractGeom g,
                                                                          const uint32_t *__restrict__ HC,
@@ -448,6 +460,11 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     __shared__ uint32_t lofs[kMaxL1BinsW];
     __shared__ uint32_t lcur[kMaxL1BinsW];
     __shared__ ull wsum[kScatBlockW / 64];
+    // OKM_WIDE_SHARE: each thread codes only its own 16 bytes; the 64-byte halo's
+    // codes come from its next four neighbours' slots ([kScatBlockW, +4): the 64
+    // bytes after the tile, coded by the last four threads)
+    constexpr int kXS = 4;  // halo slots: 64 bytes
+    __shared__ uint4 xcode[OKM_WIDE_SHARE ? kScatBlockW + kXS : 1];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     if (t < nb && HC) {
@@ -458,13 +475,28 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     constexpr int NP = WinWords<kSegW, 64>::kLoad / 16;
+    static_assert(!OKM_WIDE_SHARE || (kSegW == 16 && NP == 1 + kXS), "one 16-byte slot per thread");
     WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead (branch-free, as k_extract_scatter)
-    load_windows_clamped<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
+    WinWords<kSegW, 0> own, extra;  // OKM_WIDE_SHARE: this thread's 16 bytes; a halo slot after the tile
+    auto extra_at = [&](uint64_t tt0) -> uint64_t {  // the last kXS threads: the bytes after the tile
+        return t >= (uint32_t)(kScatBlockW - kXS) ? tt0 + kTileW1 + (uint64_t)kSegW * (t - (kScatBlockW - kXS))
+                                                   : tt0 + (uint64_t)t * kSegW;
+    };
+    if (OKM_WIDE_SHARE) {
+        load_windows_clamped<kSegW, 0>(seq, g.n, beg + (uint64_t)t * kSegW, own);
+        load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(beg), extra);
+    } else {
+        load_windows_clamped<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
+    }
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW1) {
         for (uint32_t b = t; b <= nb; b += blockDim.x) hist[b] = 0;  // + the dummy bin (nb may equal the block)
-        lds_sync();
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
+        if (OKM_WIDE_SHARE) {
+            xcode[t] = slot_codes(own.w, g.n, w0);
+            if (t >= (uint32_t)(kScatBlockW - kXS)) xcode[t + kXS] = slot_codes(extra.w, g.n, extra_at(t0));
+        }
+        lds_sync();
         const bool live = w0 < end;
         uint32_t tile_n;
         {
@@ -475,8 +507,20 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
             for (int j = 0; j < kSegW / 2; ++j) rk[j] = 0;
             if (live) {
                 Codes<NP> c;
-                make_codes<NP, false>(ww.w, c);
-                if (g.n - w0 < (uint64_t)WinWords<kSegW, 64>::kLoad) mark_tail<NP>(c, g.n - w0);
+                if (OKM_WIDE_SHARE) {
+#pragma unroll
+                    for (int i = 0; i < (NP * 16 + 63) / 64 + 1; ++i) c.bad[i] = 0;
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        const uint4 x = xcode[t + i];
+                        c.p[i] = x.x;
+                        c.q[i] = x.y;
+                        c.bad[i >> 2] |= (uint64_t)x.z << (16 * (i & 3));
+                    }
+                } else {
+                    make_codes<NP, false>(ww.w, c);
+                    if (g.n - w0 < (uint64_t)WinWords<kSegW, 64>::kLoad) mark_tail<NP>(c, g.n - w0);
+                }
 #pragma unroll
                 for (int j = 0; j < kSegW; ++j) {
                     bool valid;
@@ -487,7 +531,12 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
                     vm |= valid ? 1u << j : 0u;
                 }
             }
-            load_windows_clamped<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);  // next tile, in flight (harmless past the end)
+            if (OKM_WIDE_SHARE) {  // next tile, in flight (harmless past the end)
+                load_windows_clamped<kSegW, 0>(seq, g.n, w0 + kTileW1, own);
+                load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(t0 + kTileW1), extra);
+            } else {
+                load_windows_clamped<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);
+            }
             lds_sync();
             tile_n = tile_offsets<kScatBlockW>(t, nb, hist, lofs, lcur, wsum);
             uint32_t ch = 0;
