@@ -51,6 +51,7 @@ import numpy as np  # noqa: E402
 
 import okm  # noqa: E402
 from okm import _lib  # noqa: E402
+from okm.pipeline import OwnedCountPipeline, agree_or_raise  # noqa: E402
 
 # Load the engine (and the HIP runtime it links) before torch, so the process
 # has exactly one HIP runtime.
@@ -169,6 +170,19 @@ def parse():
     return ap.parse_args()
 
 
+def init_comm(world, rank, device):
+    """The library's own RCCL communicator (okm_comm: okm_merge_owned's HIP
+    owner split / pack / unpack kernels + grouped ncclSend/ncclRecv over
+    xGMI).  torch.distributed (gloo, host) only hands out its unique id and
+    carries the barriers and the max-time reduce."""
+    dist.init_process_group("gloo")
+    uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
+    if rank == 0:
+        uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
+    dist.broadcast(uid, 0)
+    return okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,27 +195,10 @@ def main():
     # one rank per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
-    # nccl (= RCCL over xGMI) is the product path; OKM_BENCH_BACKEND=gloo rehearses
-    # the same exchange through host memory (RCCL refuses two ranks on one GPU)
-    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
     # OKM_BENCH_EXCHANGE=1 runs the N>1 exchange + merge path at world size 1
     # too (torchrun --nproc-per-node 1): its cost on one GPU, RCCL self-send
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
-    comm = None
-    if dist_on:
-        # product path: the library's own RCCL communicator (okm_comm +
-        # okm_merge_owned: HIP owner split / pack / unpack kernels, grouped
-        # ncclSend/ncclRecv over xGMI, owner count of the sorted slices); torch.distributed (gloo,
-        # host) only hands out the communicator id, barriers and the max-time
-        # reduce.  OKM_BENCH_BACKEND=gloo rehearses the exchange through torch
-        # (okm/dist.py) instead: RCCL refuses two ranks on one device.
-        dist.init_process_group("gloo")
-        if backend == "nccl":
-            uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
-            if rank == 0:
-                uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
-            dist.broadcast(uid, 0)
-            comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
+    comm = init_comm(world, rank, device) if dist_on else None
 
     # ---- synthetic batch for this rank, made resident in HBM ---------------
     t0 = time.time()
@@ -217,144 +214,59 @@ def main():
     # Batches in flight: at N=1, S contexts (each its own HIP stream and result
     # table) driven by S host threads count whole batches concurrently, so one
     # batch's host syncs and latency-bound phases overlap another's streaming
-    # kernels.  At N>1 one thread counts into two contexts in turn while this
-    # thread exchanges the previous batch's table (RCCL on its own stream) and
-    # a third thread merges the one before: the xGMI exchange overlaps the
-    # next count and the previous merge.
+    # kernels.  At N>1 (okm.pipeline.OwnedCountPipeline) a worker thread counts
+    # batch i+1 into two contexts in turn while this thread runs the step's
+    # failure agreement and okm_merge_owned of batch i (RCCL on the library's
+    # own stream) into one of two owner contexts.
     S = max(1, args.streams)
-    ctrs = [okm.KmerCounter(K, "count", device) for _ in range(2 if dist_on else S)]
-    ctr = ctrs[0]
-    # N>1: the owner's merge runs on a third thread (two merge contexts in
-    # turn), so it overlaps the next batch's exchange and the one after's
-    # count; OKM_BENCH_MERGE_THREAD=0 keeps exchange+merge on one thread
-    merge_thread = dist_on and comm is None and os.environ.get("OKM_BENCH_MERGE_THREAD", "1") != "0"
-    mergers = [okm.KmerCounter(K, "count", device) for _ in range(2 if comm is not None or merge_thread else 1)] \
-        if dist_on else []
-    if dist_on:
-        from okm import dist as okm_dist
-
-    zero_copy = [True]
-
-    def table_tensors(c, n):
-        """The counted table as int64 device tensors: views of the engine's
-        result arrays when torch takes __cuda_array_interface__, else a copy."""
-        if zero_copy[0] and n:
-            kp, cp, _ = c.result_device()
-            try:
-                return (torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda"),
-                        torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda"))
-            except Exception as e:  # pragma: no cover - torch build without the protocol
-                log(f"note: no zero-copy device views ({e}); copying the table")
-                zero_copy[0] = False
-        keys = torch.empty(n, dtype=torch.int64, device="cuda")
-        counts = torch.empty(n, dtype=torch.int64, device="cuda")
-        if n:
-            c.fetch_into_device(keys.data_ptr(), counts.data_ptr(), n)
-        return keys, counts
 
     def count_batch(c):
         c.reset()
         c.add_device_batch(dbuf.address, len(batch))
         return c.count()
 
-    xt = [0.0, 0.0]  # exchange, merge wall time (N>1 path)
-
-    def exchange_only(c, n, release):
-        t_x = time.perf_counter()
-        keys, counts = table_tensors(c, n)
-        rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)  # gloo rehearsal
-        rk, rc = rk.cuda(), rc.cuda()
-        torch.cuda.synchronize()
-        release()  # the table has been copied out: its context may count the next batch
-        xt[0] += time.perf_counter() - t_x
-        return rk, rc, rs
-
-    def merge_runs(merger, payload):
-        rk, rc, rs = payload
-        t_m = time.perf_counter()
-        # each rank's slice is sorted: the owner counts them in place (no copy,
-        # no partition pass; okm_add_sorted_pairs_device)
-        merger.reset()
-        off = 0
-        for sz in rs:
-            if sz:
-                merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
-            off += sz
-        n_m = merger.count()
-        merger.synchronize()  # rk / rc (torch memory) may be freed and reused once this returns
-        xt[1] += time.perf_counter() - t_m
-        return n_m
-
-    def exchange_merge(c, n, release):
-        return merge_runs(mergers[0], exchange_only(c, n, release))
-
-    def count_batch_joined(c):
-        """count_batch for the RCCL path: a failed count is handed to the
-        merge (below) instead of raised on the worker thread, so this rank still
-        takes part in that merge's collectives and every rank fails together."""
-        try:
-            return count_batch(c)
-        except Exception as e:
-            return e
-
-    def merge_owned(i, c, release, counted=None):
-        """okm_merge_owned: this rank's key range of every rank's table of
-        batch i, into merge context i % 2 (the library's RCCL path)."""
-        try:
-            n_m = comm.merge_owned(c, mergers[i % 2])
-        except Exception:
-            if not isinstance(counted, Exception):
-                raise
-        if isinstance(counted, Exception):
-            raise counted
-        release()
-        t = comm.last_times()
-        xt[0] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
-        xt[1] += t["merge_ms"] * 1e-3
-        return n_m
+    pipe = None
+    if dist_on:
+        pipe = OwnedCountPipeline(comm, lambda: okm.KmerCounter(K, "count", device),
+                                  lambda c, i: c.add_device_batch(dbuf.address, len(batch)))
+        ctrs, mergers = list(pipe.local), list(pipe.owners)
+    else:
+        ctrs, mergers = [okm.KmerCounter(K, "count", device) for _ in range(S)], []
+    ctr = ctrs[0]
 
     def run_steps(nsteps):
         """nsteps batches through the path; returns the distinct count (N=1)
         or this rank's owned distinct count of the last merge (N>1)."""
         import threading
-        if not dist_on:
-            if S == 1:
-                n = 0
-                for _ in range(nsteps):
-                    n = count_batch(ctr)
-                return n
-            nxt, lock, res, err = [0], threading.Lock(), [], []
+        if dist_on:
+            res = pipe.run(nsteps)
+            return res[-1] if res else 0
+        if S == 1:
+            n = 0
+            for _ in range(nsteps):
+                n = count_batch(ctr)
+            return n
+        nxt, lock, res, err = [0], threading.Lock(), [], []
 
-            def worker(c):
-                try:
-                    while True:
-                        with lock:
-                            if nxt[0] >= nsteps:
-                                return
-                            nxt[0] += 1
-                        res.append(count_batch(c))
-                except BaseException as e:  # surfaced below
-                    err.append(e)
+        def worker(c):
+            try:
+                while True:
+                    with lock:
+                        if nxt[0] >= nsteps:
+                            return
+                        nxt[0] += 1
+                    res.append(count_batch(c))
+            except BaseException as e:  # surfaced below
+                err.append(e)
 
-            th = [threading.Thread(target=worker, args=(c,), daemon=True) for c in ctrs]
-            for x in th:
-                x.start()
-            for x in th:
-                x.join()
-            if err:
-                raise err[0]
-            return res[-1]
-        if comm is not None:
-            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch_joined(ctrs[j]),
-                                         lambda i, j, n, release: merge_owned(i, ctrs[j], release, n))
-        elif merge_thread:
-            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
-                                         lambda i, j, n, release: exchange_only(ctrs[j], n, release),
-                                         lambda i, m, payload: merge_runs(mergers[m], payload))
-        else:
-            res = okm_dist.run_pipelined(nsteps, lambda i, j: count_batch(ctrs[j]),
-                                         lambda i, j, n, release: exchange_merge(ctrs[j], n, release))
-        return res[-1] if res else 0
+        th = [threading.Thread(target=worker, args=(c,), daemon=True) for c in ctrs]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if err:
+            raise err[0]
+        return res[-1]
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -368,7 +280,8 @@ def main():
         count_batch(c)
     run_steps(args.warmup)
     barrier_sync()
-    xt[0] = xt[1] = 0.0
+    if pipe is not None:
+        pipe.phase_ms.update(exchange=0.0, merge=0.0)
     t_start = time.perf_counter()
     n_owned = run_steps(args.steps)
     barrier_sync()
@@ -451,7 +364,7 @@ def main():
                    "k": K, "reads_per_gpu": args.reads, "read_len": READ_LEN, "genome_bp": GENOME_BP,
                    "distinct_kmers": int(info["distinct"]) if world == 1 else None,
                    "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}",
-                   "batches_in_flight": (3 if merge_thread else 2) if dist_on else S},
+                   "batches_in_flight": 2 if dist_on else S},
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_mt": cpu_mt,
@@ -467,10 +380,9 @@ def main():
     }
     if dist_on:
         out["config"]["owned_distinct_rank0"] = int(n_owned)
-        out["exchange_ms_per_step_rank0"] = {"exchange": round(xt[0] / args.steps * 1e3, 3),
-                                             "merge": round(xt[1] / args.steps * 1e3, 3)}
-        out["exchange_impl"] = ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
-                                if comm is not None else "torch gloo rehearsal (okm/dist.py)")
+        out["exchange_ms_per_step_rank0"] = {"exchange": round(pipe.phase_ms["exchange"] / args.steps, 3),
+                                             "merge": round(pipe.phase_ms["merge"] / args.steps, 3)}
+        out["exchange_impl"] = "okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
     if c3 is not None:
         out["c3"] = ({k: c3[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                          "scaling", "config", "exchange_impl", "phase_ms_per_step_rank0",
@@ -500,23 +412,8 @@ def main_c3(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
-    # product path: the library's own RCCL communicator (okm_comm, okm_merge_owned:
-    # HIP pack/unpack kernels + grouped ncclSend/ncclRecv over xGMI); torch.distributed
-    # (gloo, host) only hands out the communicator id, barriers and the max-time
-    # reduce.  OKM_BENCH_BACKEND=gloo rehearses the exchange through torch on one
-    # GPU instead (RCCL refuses two ranks on one device).
-    backend = os.environ.get("OKM_BENCH_BACKEND", "nccl")
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
-    comm = None
-    if dist_on:
-        dist.init_process_group("gloo")
-        from okm import dist as okm_dist
-        if backend == "nccl":
-            uid = torch.zeros(okm._lib.OKM_COMM_ID_BYTES, dtype=torch.uint8)
-            if rank == 0:
-                uid = torch.frombuffer(bytearray(okm.comm_unique_id()), dtype=torch.uint8)
-            dist.broadcast(uid, 0)
-            comm = okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
+    comm = init_comm(world, rank, device) if dist_on else None
     out = c3_run(args, world, rank, device, comm, dist_on, args.steps, args.warmup, baselines=True)
     if out is not None:
         emit(out)
@@ -530,8 +427,6 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
     """Time `steps` whole C3 jobs (after `warmup` untimed ones) on every rank
     and return rank 0's line (None on the other ranks).  Every rank must call
     it (the merge is collective); it releases its contexts and shard buffer."""
-    if dist_on:
-        from okm import dist as okm_dist
     total = args.c3_reads
     r0, r1 = total * rank // world, total * (rank + 1) // world
     nreads = r1 - r0
@@ -546,7 +441,7 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
         ctr = okm.KmerCounter(K, "count", device)
         # the owner's merge reuses the counting context (okm_merge_owned allows
         # owner == local): one device pool per rank, no cross-context trimming
-        merger = (ctr if comm is not None else okm.KmerCounter(K, "count", device)) if dist_on else None
+        merger = ctr if dist_on else None
     except Exception as e:
         setup_err = e
     if dist_on:  # every rank learns whether all could set up, before any collective of the merge
@@ -555,8 +450,6 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
         if int(bad.item()) and setup_err is None:
             setup_err = RuntimeError(f"C3 setup failed on {int(bad.item())} rank(s)")
     if setup_err is not None:
-        if merger is not None and merger is not ctr:
-            merger.close()
         if ctr is not None:
             ctr.close()
         if dbuf is not None:
@@ -582,45 +475,17 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
         except Exception as e:
             if comm is None:
                 raise
-            # still take part in the merge's collectives: okm_merge_owned agrees
-            # on the failure (status word) and every rank returns an error
-            # instead of the others blocking in a collective this rank never joins
             err = e
         xt[0] += time.perf_counter() - tc
-        if not dist_on:
+        if comm is None:
             return n
-        if comm is not None:
-            try:
-                n_m = comm.merge_owned(ctr, merger)
-            except Exception:
-                if err is None:
-                    raise
-            if err is not None:
-                raise err
-            t = comm.last_times()
-            xt[1] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
-            xt[2] += t["merge_ms"] * 1e-3
-            return n_m
-        tx = time.perf_counter()
-        kp, cp, _ = ctr.result_device()
-        keys = torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda") if n else \
-            torch.empty(0, dtype=torch.int64, device="cuda")
-        counts = torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda") if n else \
-            torch.empty(0, dtype=torch.int64, device="cuda")
-        rk, rc, _, rs = okm_dist.exchange_runs(keys.cpu(), counts.cpu(), K)  # gloo rehearsal
-        rk, rc = rk.cuda(), rc.cuda()
-        torch.cuda.synchronize()
-        xt[1] += time.perf_counter() - tx
-        tm = time.perf_counter()
-        merger.reset()
-        off = 0
-        for sz in rs:
-            if sz:
-                merger.add_sorted_pairs_device(rk.data_ptr() + 8 * off, rc.data_ptr() + 8 * off, sz)
-            off += sz
-        n_m = merger.count()
-        merger.synchronize()
-        xt[2] += time.perf_counter() - tm
+        # every rank learns whether any count failed, and then all stop here
+        # together (okm.pipeline.agree_or_raise) instead of merging alone
+        agree_or_raise(comm, err)
+        n_m = comm.merge_owned(ctr, merger)
+        t = comm.last_times()
+        xt[1] += (t["plan_ms"] + t["exchange_ms"]) * 1e-3
+        xt[2] += t["merge_ms"] * 1e-3
         return n_m
 
     def barrier_sync():
@@ -669,8 +534,6 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
         dbuf.download(host)
         cpu, cpu_mt = cpu_baselines(host, m, min(args.cpu_mt_reads, nreads), device, "the C3 shard")
 
-    if merger is not None and merger is not ctr:
-        merger.close()
     ctr.close()
     dbuf.free()
     if rank != 0:
@@ -711,7 +574,7 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
                             "frac_of_8TBs": round(surv_bytes * steps / dt / 8e12, 4),
                             "input_stream_frac": round(shard_bases * steps / dt / 8e12, 5)},
         "exchange_impl": ("okm_merge_owned (library RCCL communicator, HIP pack/unpack, owner count of sorted slices)"
-                          if comm is not None else ("torch gloo rehearsal" if dist_on else None)),
+                          if comm is not None else None),
         "phase_ms_per_step_rank0": {"count": round(xt[0] / steps * 1e3, 2),
                                     "exchange": round(xt[1] / steps * 1e3, 2),
                                     "merge": round(xt[2] / steps * 1e3, 2)},

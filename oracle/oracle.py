@@ -71,6 +71,8 @@ def load() -> ctypes.CDLL:
     lib.oracle_counter_wide_windows.argtypes = [c_void_p]
     lib.oracle_counter_wide_result.restype = c_uint64
     lib.oracle_counter_wide_result.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]
+    lib.oracle_counter_add_separated_ranges.argtypes = [c_void_p, c_void_p, c_uint64, c_uint8, c_void_p, c_void_p,
+                                                         c_uint32]
     lib.oracle_query_hits.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint8, c_void_p]
     _lib = lib
     return lib
@@ -128,6 +130,16 @@ class OracleCounter:
         offs = np.zeros(len(lens) + 1, dtype=np.uint64)
         offs[1:] = np.cumsum(lens)
         self.add_batch(body, offs, normalized=False)
+
+    def add_separated_ranges(self, data: np.ndarray, ranges, sep: int = ord("\n")) -> None:
+        """Restatement-MT helper (oracle_counter_add_separated_ranges): count
+        only canonical keys inside one of the [lo, hi) `ranges` (rolling
+        encode; every valid window still counts in `windows`)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        lo = np.ascontiguousarray([r[0] for r in ranges], dtype=np.uint64)
+        hi = np.ascontiguousarray([r[1] for r in ranges], dtype=np.uint64)
+        load().oracle_counter_add_separated_ranges(self.h, data.ctypes.data, len(data), sep, lo.ctypes.data,
+                                                   hi.ctypes.data, len(lo))
 
     def add_pairs(self, keys: np.ndarray, counts: np.ndarray) -> None:
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
@@ -309,3 +321,43 @@ def count_separated_wide_ranges(data: np.ndarray, k: int, threads: int, bits: in
     keys = np.concatenate([p[0] for p in parts]) if parts else np.zeros((0, 2), np.uint64)
     counts = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint64)
     return keys, counts, w
+
+
+def count_separated_ranges_mt(chunks, k: int, ranges, threads: int) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Restatement-MT helper for full-size parity (not reference behaviour: a
+    labelled helper): the canonical keys inside `ranges` ([lo, hi) pairs) of
+    every window of the batch chunks yielded by `chunks` (device layout,
+    records joined by '\n', each chunk ending at a record boundary), each
+    chunk split at record boundaries over `threads` counters.  Returns the
+    sorted (keys, counts) restricted to the ranges, and the valid windows of
+    all chunks."""
+    import threading
+
+    load()
+    threads = max(1, int(threads))
+    ctrs = [OracleCounter(k) for _ in range(threads)]
+    for data in chunks:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        cut = np.flatnonzero(data == ord("\n"))
+        ends = [0]
+        for t in range(1, threads):
+            i = int(np.searchsorted(cut, len(data) * t // threads))
+            ends.append(int(cut[i]) + 1 if i < len(cut) else len(data))
+        ends.append(len(data))
+        ths = [threading.Thread(target=ctrs[t].add_separated_ranges, args=(data[ends[t]:ends[t + 1]], ranges))
+               for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    parts = [c.result(1) for c in ctrs]
+    windows = sum(c.windows for c in ctrs)
+    kk = np.concatenate([p[0] for p in parts])
+    cc = np.concatenate([p[1] for p in parts])
+    if len(kk) == 0:
+        return kk.astype(np.uint64), cc.astype(np.uint64), windows
+    order = np.argsort(kk, kind="stable")
+    kk, cc = kk[order], cc[order]
+    first = np.concatenate([[True], kk[1:] != kk[:-1]])
+    starts = np.flatnonzero(first)
+    return kk[starts].astype(np.uint64), np.add.reduceat(cc, starts).astype(np.uint64), windows

@@ -827,6 +827,9 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     constexpr int kHB = sizeof(KT) > 8 ? OKM_FULL_HB_W : kHomeBits;  // full-mode home bits
+    // full_item shifts a key by rem_bits - kHB with rem_bits > kDenseBits: the
+    // shift stays non-negative only while kHB <= kDenseBits + 1
+    static_assert(kHB <= kDenseBits + 1, "full-mode home bits exceed kDenseBits + 1 (OKM_FULL_HB_W vs OKM_COUNT_CB)");
     constexpr int kFull = full_lds_bytes<W, KT, kHB>();
     constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
     constexpr int kBytes = kFull > kDense ? kFull : kDense;

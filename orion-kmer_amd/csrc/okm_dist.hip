@@ -674,8 +674,8 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     {
         okm_status a = OKM_OK;
         for (auto [b, bytes] : {std::pair<DevBuf *, size_t>{&m->starts, nt * (nb + 1) * sizeof(ull)},
-                                {&m->hist, (nb + 2) * sizeof(ull)},
-                                {&m->hsum, (nb + 2) * sizeof(ull)},
+                                {&m->hist, (nb + 3) * sizeof(ull)},
+                                {&m->hsum, (nb + 3) * sizeof(ull)},
                                 {&m->cut, (P + 1) * sizeof(ull)},
                                 {&m->sizes, (3 * P + 1) * sizeof(ull)},
                                 {&m->gsizes, (3 * (size_t)P + 1) * P * sizeof(ull)},
@@ -685,18 +685,22 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
                                 {&m->offs, 4 * (P + 1) * sizeof(ull)},
                                 {&m->flag, 2 * sizeof(ull)}})
             if (a == OKM_OK) a = b->ensure(bytes);
-        if (a == OKM_OK) a = ensure_hpin(m, (nt + 1) * (nb + 2) + (3 * (size_t)P + 1) * P + 64);
+        if (a == OKM_OK) a = ensure_hpin(m, (nt + 1) * (nb + 3) + (3 * (size_t)P + 1) * P + 64);
         if (a != OKM_OK) return broke(m, a);
     }
     // host sources of async copies: live until the sync below
     const ull one = 1;
     const bool wide = ctx_is_wide(tabs[0].local);  // K128 keys (k > 32): u64 word pairs, never deltas
-    const ull wd = want_deltas(P) && !wide ? 1 : 0;  // 1: deltas wanted (forced or auto), agreed below
+    // words nb + 1 / nb + 2 of the all-reduce: ranks that want deltas (forced
+    // or auto) / ranks that FORCE them.  Both must be 0 or P: a forced rank
+    // beside an auto rank would otherwise pick a different format than its peer
+    const int wmode = wide ? 0 : want_deltas(P);
+    const ull wd[2] = {wmode ? 1ull : 0ull, wmode == 1 ? 1ull : 0ull};
     okm_status st = OKM_OK;
     for (size_t i = 0; i < nt && st == OKM_OK; ++i)  // counts the local shards if needed (synchronous)
         st = okm_result_device(tabs[i].local, &tabs[i].dk, &tabs[i].dc, &tabs[i].n);
     HIP_TRY(hipMemsetAsync(m->hist.p, 0, (nb + 1) * sizeof(ull), s));
-    HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb + 1, &wd, sizeof(ull), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb + 1, wd, 2 * sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->starts.p, 0, nt * (nb + 1) * sizeof(ull), s));
     if (st == OKM_OK) {
         for (size_t i = 0; i < nt; ++i) {
@@ -710,21 +714,21 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
         HIP_TRY(hipMemcpyAsync(m->hist.as<ull>() + nb, &one, sizeof(ull), hipMemcpyHostToDevice, s));
     }
     {
-        okm_status c = m->tp->all_reduce_sum(m->hist.as<ull>(), m->hsum.as<ull>(), nb + 2, s);
+        okm_status c = m->tp->all_reduce_sum(m->hist.as<ull>(), m->hsum.as<ull>(), nb + 3, s);
         if (c != OKM_OK) return broke(m, c);
     }
-    ull *h_sum = m->hpin, *h_starts = m->hpin + nb + 2;
-    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, (nb + 2) * sizeof(ull), hipMemcpyDeviceToHost, s));
+    ull *h_sum = m->hpin, *h_starts = m->hpin + nb + 3;
+    HIP_TRY(hipMemcpyAsync(h_sum, m->hsum.p, (nb + 3) * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_starts, m->starts.p, nt * (nb + 1) * sizeof(ull), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (st != OKM_OK) return st;
     if (h_sum[nb]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed before the exchange");
-    if (h_sum[nb + 1] != 0 && h_sum[nb + 1] != P)
+    if ((h_sum[nb + 1] != 0 && h_sum[nb + 1] != P) || (h_sum[nb + 2] != 0 && h_sum[nb + 2] != P))
         return fail(OKM_E_COMM, "okm_merge_owned: ranks disagree on the key wire format (OKM_WIRE_DELTAS)");
     uint64_t pairs = 0;
     for (uint32_t b = 0; b < nb; ++b) pairs += h_sum[b];
     // every rank sees the same sums: the same decision everywhere
-    *deltas = h_sum[nb + 1] == P && (want_deltas(P) == 1 || dense_enough(pairs / P, ctx_k(tabs[0].local)));
+    *deltas = h_sum[nb + 1] == P && (h_sum[nb + 2] == P || dense_enough(pairs / P, ctx_k(tabs[0].local)));
     for (size_t i = 0; i < nt; ++i) tabs[i].starts.assign(h_starts + i * (nb + 1), h_starts + (i + 1) * (nb + 1));
     bounds.assign(P + 1, 0);  // (h_starts stays valid: tabs[i].starts copied above)
     owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());

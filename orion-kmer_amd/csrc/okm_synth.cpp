@@ -185,7 +185,11 @@ extern "C" okm_status okm_synth_long_reads(uint64_t genome_seed, uint64_t genome
             while (j < L) {
                 const uint64_t draw = splitmix64(h + 0x632BE59BD9B4E019ull * (++d));
                 const uint64_t u = draw & 0xFFFFFFFFull;
-                const uint32_t code = g[src++];
+                // a run of deletions can consume more than 2 L source bases
+                // (npos above assumes fewer): wrap instead of reading past the
+                // genome, which leaves every read that stays inside unchanged
+                const uint32_t code = g[src];
+                src = src + 1 == genome_len ? 0 : src + 1;
                 if (u < t1) {
                     o[j++] = (uint8_t)((code + 1 + (uint32_t)((draw >> 32) % 3)) & 3u);
                 } else if (u < t2) {

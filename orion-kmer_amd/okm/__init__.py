@@ -511,6 +511,10 @@ def distributed_compare(comm: "Comm", a: "KmerCounter", b: "KmerCounter", owner_
     (compare.rs:58) and |A|, |B|, |A ∩ B| are summed over the ranks.  Every
     rank returns the global (|A|, |B|, |A ∩ B|); union and Jaccard follow on
     the host (compare.rs:60-66)."""
+    if any(c.wide for c in (a, b, owner_a, owner_b)):
+        # okm_set_intersection_size_device reads plain u64 keys; compare.rs:37-39
+        # only ever sees k <= 32 databases (KmerDbV2 stores u64 keys)
+        raise OkmError(_lib.OKM_E_ARG, "distributed_compare: k > 32 (two-u64) sets are not supported")
     na, nb = comm.merge_owned_n([a, b], [owner_a, owner_b])
     inter = 0
     if na and nb:

@@ -1,26 +1,23 @@
-"""Owner-partitioned merge of per-GPU count tables.
+"""TEST INFRASTRUCTURE (rehearsal only): a torch restatement of the plan of
+the library's owner-partitioned merge, ``okm_merge_owned``
+(orion-kmer_amd/csrc/okm_dist.hip), so that the world-size
+2/3 gloo tests run the N>1 orchestration on CPU processes without a GPU.
+The product path never imports this file: bench.py and the CLI exchange
+through the library's RCCL communicator (okm.Comm).
 
-Reads shard naturally across GPUs (count.rs:23-38 is per record), so every
-rank counts its own shard with no communication.  The only exchange step
-is the merge:
+The plan restated here is the library's:
 
   1. each rank holds its local table, sorted by key (okm_count's output);
-  2. a 2^B-bin histogram of the top key bits is summed over ranks
+  2. a 2^16-bin histogram of the top key bits is summed over ranks
      (all_reduce) and cut into contiguous, count-balanced key ranges, one per
-     rank (value-range ownership: canonical k-mers are skewed ~7:5:3:1 by
-     first base, so equal-width ranges would not balance);
+     rank, by the library's own host split (okm_owner_bounds);
   3. every rank's sorted table splits into contiguous per-owner slices
-     (searchsorted on the range boundaries) and one all_to_all_single moves
-     sizes, then one moves keys and one moves counts;
-  4. each owner adds the received (key, count) runs into a fresh counter
-     (weights add, exactly the AtomicUsize fetch_add of count.rs:31-34) and
-     re-counts, giving its range sorted.  Every rank's slice arrives sorted, so
-     the engine takes them in place (okm_add_sorted_pairs_device: binary-search
-     splits, no partition pass).
+     (searchsorted on the range boundaries) and all_to_all moves sizes, keys
+     and counts (counts as one byte plus escapes, like k_pack_counts);
+  4. each owner adds the received sorted runs into one table (weights add:
+     the AtomicUsize fetch_add of count.rs:31-34).
 
-The global table is the concatenation of the owners' ranges in rank order,
-so no final merge is needed.  The same code runs over gloo with CPU tensors
-(tests) and over RCCL ("nccl") with device tensors (bench.py on MI355X).
+The global table is the concatenation of the owners' ranges in rank order.
 """
 
 from __future__ import annotations
@@ -75,7 +72,7 @@ def owner_ranges(hist: np.ndarray, world: int) -> List[int]:
     bins [b_r, b_{r+1}); cuts where the running total first reaches r/world.
     The library's host split (okm_owner_bounds, the same code okm_merge_owned
     runs), so the gloo tests exercise it."""
-    from . import owner_bounds
+    from okm import owner_bounds
     return owner_bounds(np.asarray(hist, dtype=np.uint64), world)
 
 
@@ -245,95 +242,3 @@ def gather_global(keys: torch.Tensor, counts: torch.Tensor,
     ok = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gk, ns)]).view(np.uint64)
     oc = np.concatenate([g[:int(c.item())].cpu().numpy() for g, c in zip(gc, ns)]).view(np.uint64)
     return ok, oc
-
-
-def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
-                  consume: Callable[[int, int, object, Callable[[], None]], object],
-                  finish: Optional[Callable[[int, int, object], object]] = None) -> List[object]:
-    """Pipelined N>1 step loop (bench.py).  A worker thread counts batch i
-    into table buffer i % 2 (count_into(i, j) -> handle) while this thread
-    consumes the previous one (consume(i, j, handle, release) -> result), so
-    the exchange of batch i overlaps the count of batch i + 1.  consume calls
-    release() once the table has been copied out (the buffer may then count
-    batch i + 2).  Only this thread issues collectives, so every rank issues
-    them in the same order.
-
-    With `finish`, consume's result is a payload handed to a third thread that
-    runs finish(i, m, payload) -> result on merge slot m = i % 2 (the owner's
-    merge, no collectives): the merge of batch i then overlaps the exchange of
-    batch i + 1 and the count of batch i + 2, and the slot is reused by batch
-    i + 2 only after its finish returned.  Results are in step order either
-    way.  An exception in any thread is re-raised here."""
-    import queue
-    import threading
-    free = [threading.Semaphore(1), threading.Semaphore(1)]
-    q: "queue.Queue" = queue.Queue()
-    err: List[BaseException] = []
-    stop = threading.Event()
-
-    def acquire(sem: "threading.Semaphore") -> bool:
-        while not sem.acquire(timeout=0.1):
-            if stop.is_set():
-                return False
-        return True
-
-    def producer():
-        try:
-            for i in range(nsteps):
-                if not acquire(free[i % 2]):
-                    return
-                q.put((i, i % 2, count_into(i, i % 2)))
-        except BaseException as e:  # surfaced on the consuming thread
-            err.append(e)
-            stop.set()
-            q.put(None)
-
-    out: List[object] = [None] * nsteps
-    mfree = [threading.Semaphore(1), threading.Semaphore(1)]
-    mq: "queue.Queue" = queue.Queue()
-
-    def finisher():
-        try:
-            while True:
-                item = mq.get()
-                if item is None:
-                    return
-                i, m, payload = item
-                out[i] = finish(i, m, payload)
-                mfree[m].release()
-        except BaseException as e:
-            err.append(e)
-            stop.set()
-
-    th = threading.Thread(target=producer, daemon=True)
-    th.start()
-    fth = threading.Thread(target=finisher, daemon=True) if finish is not None else None
-    if fth is not None:
-        fth.start()
-    try:
-        for _ in range(nsteps):
-            item = None
-            while item is None and not err:
-                try:
-                    item = q.get(timeout=0.1)
-                except queue.Empty:
-                    continue
-            if err or item is None:
-                break
-            i, j, h = item
-            r = consume(i, j, h, free[j].release)
-            if fth is None:
-                out[i] = r
-                continue
-            if not acquire(mfree[i % 2]):
-                break
-            mq.put((i, i % 2, r))
-    finally:
-        if fth is not None:
-            mq.put(None)
-            fth.join()
-        stop.set()
-        th.join()
-    if err:
-        raise err[0]
-    return out

@@ -1,5 +1,8 @@
-"""Multi-process (gloo, CPU) tests of the owner-partitioned table merge,
-okm/dist.py.
+"""Multi-process (gloo, CPU) tests of the N>1 path: the
+product's step orchestration (okm/pipeline.py: OwnedCountPipeline,
+run_pipelined, the failure agreement) and the owner split of the library
+(okm_owner_bounds), with the exchange restated in torch
+(tests/dist_rehearsal.py, rehearsal only).
 
 Each rank counts its own contiguous shard of reads (count.rs:23-38 is per
 record, so shards need no halo), the ranks exchange (key, count) runs by
@@ -21,7 +24,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import okm
-from okm import dist as okm_dist
+import dist_rehearsal as okm_dist
+from okm.pipeline import OwnedCountPipeline, PeerFailure, run_pipelined
 from oracle import OracleCounter
 
 
@@ -286,10 +290,10 @@ def _pipe_worker(rank, world, port, k, nsteps, out_path, staged=False):
             return r
 
         if staged:
-            merged = okm_dist.run_pipelined(nsteps, count_into, consume, finish)
+            merged = run_pipelined(nsteps, count_into, consume, finish)
             res = [okm_dist.gather_global(mk, mc) for mk, mc in merged]
         else:
-            res = okm_dist.run_pipelined(nsteps, count_into, consume)
+            res = run_pipelined(nsteps, count_into, consume)
         if rank == 0:
             np.savez(out_path, **{f"k{i}": r[0] for i, r in enumerate(res)}, **{f"c{i}": r[1] for i, r in enumerate(res)})
     finally:
@@ -317,7 +321,7 @@ def test_pipelined_worker_error_surfaces():
 
     seen = []
     with pytest.raises(RuntimeError, match="count failed"):
-        okm_dist.run_pipelined(5, count_into, lambda i, j, h, release: (release(), seen.append(h)))
+        run_pipelined(5, count_into, lambda i, j, h, release: (release(), seen.append(h)))
     assert seen == [0, 1]
 
 
@@ -328,10 +332,136 @@ def test_pipelined_finish_error_surfaces():
         return payload
 
     with pytest.raises(RuntimeError, match="merge failed"):
-        okm_dist.run_pipelined(6, lambda i, j: i, lambda i, j, h, release: (release(), h)[1], finish)
+        run_pipelined(6, lambda i, j: i, lambda i, j, h, release: (release(), h)[1], finish)
 
 
 def test_pipelined_finish_results_in_order():
-    out = okm_dist.run_pipelined(7, lambda i, j: i, lambda i, j, h, release: (release(), h * 10)[1],
+    out = run_pipelined(7, lambda i, j: i, lambda i, j, h, release: (release(), h * 10)[1],
                                  lambda i, m, p: (i, m, p))
     assert out == [(i, i % 2, i * 10) for i in range(7)]
+
+
+# ---------------------------------------------------------------------------
+# okm.pipeline.OwnedCountPipeline (bench.py's N>1 step) over gloo processes:
+# the product orchestration with oracle-backed counters and a gloo comm whose
+# merge_owned restates okm_merge_owned's plan (dist_rehearsal)
+# ---------------------------------------------------------------------------
+
+class _OracleCtx:
+    """The KmerCounter surface the pipeline uses, counted by the restatement."""
+
+    def __init__(self, k, fail_at=None):
+        self.k, self.fail_at, self.step = k, fail_at, -1
+        self.oc = OracleCounter(k)
+
+    def reset(self):
+        self.oc = OracleCounter(self.k)
+
+    def add(self, data, step):
+        self.step = step
+        if self.fail_at is not None and step == self.fail_at:
+            raise RuntimeError(f"count failed at step {step}")
+        self.oc.add_separated(data)
+
+    def count(self):
+        return self.oc.distinct
+
+    def result(self, min_count=1):
+        return self.oc.result(min_count)
+
+
+class _GlooComm:
+    """allreduce / merge_owned of okm.Comm over the default gloo group."""
+
+    def __init__(self, k):
+        self.k = k
+        self.merges = 0
+
+    def allreduce(self, values):
+        t = torch.tensor([int(v) for v in values], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return [int(x) for x in t.tolist()]
+
+    def merge_owned(self, local, owner):
+        lk, lc = local.result(1)
+        rk, rc, _, _ = okm_dist.exchange_runs(torch.from_numpy(lk.view(np.int64).copy()),
+                                              torch.from_numpy(lc.view(np.int64).copy()), self.k)
+        owner.reset()
+        if rk.numel():
+            owner.oc.add_pairs(rk.numpy().view(np.uint64), rc.numpy().view(np.uint64))
+        self.merges += 1
+        return owner.count()
+
+
+def _step_reads(i):
+    return _reads(3_000, 150, seed=40 + i).reshape(3_000, 151)
+
+
+def _owned_pipe_worker(rank, world, port, k, nsteps, fail_rank, fail_step, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = _GlooComm(k)
+        fail_at = fail_step if rank == fail_rank else None
+
+        def add(ctx, step):
+            ctx.add(np.ascontiguousarray(np.array_split(_step_reads(step), world)[rank]).reshape(-1), step)
+
+        pipe = OwnedCountPipeline(comm, lambda: _OracleCtx(k, fail_at), add)
+        outcome = "ok"
+        try:
+            res = pipe.run(nsteps)
+        except PeerFailure:
+            outcome = "peer"
+            res = None
+        except RuntimeError as e:
+            outcome = "own" if "count failed" in str(e) else repr(e)
+            res = None
+        mk = mc = None
+        if res is not None:
+            ok, oc_ = pipe.owned().result(1)
+            mk, mc = okm_dist.gather_global(torch.from_numpy(ok.view(np.int64).copy()),
+                                            torch.from_numpy(oc_.view(np.int64).copy()))
+        # one more collective after the failure: every rank is still in step
+        dist.barrier()
+        np.savez(out_path + f".{rank}.npz", outcome=np.array(outcome), merges=np.array(comm.merges),
+                 n=np.array(res if res is not None else [], np.int64),
+                 keys=mk if mk is not None else np.zeros(0, np.uint64),
+                 counts=mc if mc is not None else np.zeros(0, np.uint64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_owned_count_pipeline_steps_equal_global_table(tmp_path):
+    """Every step's owners hold the global table of that step's reads; the
+    last step's ranges in rank order equal the single-process table."""
+    k, world, nsteps = 31, 2, 4
+    out = os.path.join(str(tmp_path), "own")
+    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, -1, -1, out), nprocs=world, join=True)
+    got = [np.load(out + f".{r}.npz") for r in range(world)]
+    assert all(str(g["outcome"]) == "ok" for g in got)
+    oc = OracleCounter(k)
+    oc.add_separated(_step_reads(nsteps - 1).reshape(-1))
+    ek, ec = oc.result(1)
+    assert np.array_equal(got[0]["keys"], ek) and np.array_equal(got[0]["counts"], ec)
+    for i in range(nsteps):  # owned distinct counts sum to each step's distinct keys
+        o = OracleCounter(k)
+        o.add_separated(_step_reads(i).reshape(-1))
+        assert sum(int(g["n"][i]) for g in got) == o.distinct, i
+    assert all(int(g["merges"]) == nsteps for g in got)
+
+
+@pytest.mark.parametrize("fail_rank,fail_step", [(1, 2), (0, 0)])
+def test_owned_count_pipeline_failure_stops_every_rank(tmp_path, fail_rank, fail_step):
+    """a rank whose count fails must not let its peers run the
+    merge alone: every rank raises at that step, before okm_merge_owned, and
+    the process group is still usable (the barrier after the failure)."""
+    k, world, nsteps = 25, 2, 5
+    out = os.path.join(str(tmp_path), "fail")
+    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, fail_rank, fail_step, out),
+             nprocs=world, join=True)
+    got = [np.load(out + f".{r}.npz") for r in range(world)]
+    for r, g in enumerate(got):
+        assert str(g["outcome"]) == ("own" if r == fail_rank else "peer"), (r, str(g["outcome"]))
+        assert int(g["merges"]) == fail_step  # no rank merged the failed step

@@ -17,7 +17,7 @@ import pytest
 import torch
 
 import okm
-from oracle import OracleCounter, count_separated_mt
+from oracle import OracleCounter, count_separated_mt, count_separated_ranges_mt
 
 pytestmark = pytest.mark.gpu
 
@@ -263,6 +263,9 @@ def test_c3_p1_full_size(monkeypatch):
     # ~1.0e9 genomic + ~0.6e9 error k-mers (~1.8e9 expected; measured 1.61e9)
     assert 1.4e9 < nd < 1.9e9
     d1 = _table_digest(keys, counts)
+    # exact parity of the FOLDED table on 12 key ranges against the rolling
+    # range restatement over ALL 167,772,160 reads (count.rs:48,52-89,106-119)
+    _exact_key_ranges(keys, counts, buf, n, stride, k)
     del keys, counts
     ctr.close()
     # the same input folded twice as often: the same table
@@ -285,6 +288,49 @@ def test_c3_p1_full_size(monkeypatch):
         c.add_device_batch(buf.address, m * stride)
         gk, gc = c.result(1)
     buf.free()
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def c3_key_ranges(k, per_quarter=3, width_bits=13):
+    """Key ranges spread over the four first-base quarters of the canonical
+    keys (skewed ~7:5:3:1): `per_quarter` ranges of 1/2^width_bits of
+    the key space at 10 %, 50 % and 90 % of each quarter."""
+    space = 1 << (2 * k)
+    q = space >> 2
+    w = space >> width_bits
+    out = []
+    for a in range(4):
+        for f in ((0.1, 0.5, 0.9) if per_quarter == 3 else np.linspace(0.05, 0.95, per_quarter)):
+            lo = a * q + int(f * q)
+            out.append((lo, lo + w))
+    return out
+
+
+def _exact_key_ranges(keys, counts, buf, n_reads, stride, k, threads=None, chunk_reads=4_194_304):
+    """Compare the device table's entries inside c3_key_ranges() exactly with
+    the restatement over every read of the device batch `buf` (streamed to
+    the host in chunks)."""
+    ranges = c3_key_ranges(k)
+    thr = threads or max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1),
+                                os.cpu_count() or 1))
+    bounds = torch.tensor([v for r in ranges for v in r], dtype=torch.int64, device=keys.device)
+    cut = torch.searchsorted(keys, bounds).cpu().tolist()  # keys < 2^62: signed order is unsigned order
+    gk = np.concatenate([keys[cut[2 * i]:cut[2 * i + 1]].cpu().numpy() for i in range(len(ranges))]).view(np.uint64)
+    gc = np.concatenate([counts[cut[2 * i]:cut[2 * i + 1]].cpu().numpy() for i in range(len(ranges))]).view(np.uint64)
+    host = np.empty(chunk_reads * stride, dtype=np.uint8)
+
+    def chunks():
+        seq = dev_tensor(buf.address, n_reads * stride, "|u1")
+        for r0 in range(0, n_reads, chunk_reads):
+            r1 = min(n_reads, r0 + chunk_reads)
+            nb = (r1 - r0) * stride
+            h = torch.from_numpy(host[:nb])
+            h.copy_(seq[r0 * stride:r1 * stride])
+            yield host[:nb]
+
+    ek, ec, w = count_separated_ranges_mt(chunks(), k, ranges, thr)
+    assert w == int(counts.sum().item())
+    assert len(ek) > 100_000 and all(cut[2 * i + 1] > cut[2 * i] for i in range(len(ranges))), cut
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
 
 

@@ -3,13 +3,15 @@ all 64 WGS-shaped samples (okm.workloads.c5_samples: 64 runs of
 data_metagenome.json.gz, <= 256 Mbases each, 11.19 Gbases in all), then
 compare.rs:51-66 of DB1 (samples 0-31) against DB2 (samples 32-63).
 
-Exact against the restatement on a subset: the sets of the two smallest
-samples of each DB (oracle/okm_oracle.c over the host cores), and their
-unions / intersection (numpy).  For the rest, full-size properties: every
-set strictly increasing and canonical, |A|, |B|, |A ∩ B| equal between the
-one-GPU compare (set unions of sorted runs + device intersection) and the
-distributed compare through the library's exchange at P = 8 virtual ranks
-(okm_merge_owned_n over okm_comm_init_loopback)."""
+Exact against the restatement: the sets of 12 samples of every size class
+(0.1 to 256 Mbases, read lengths 365 to 20,008; oracle/okm_oracle.c over the
+host cores) and the unions / intersection of four of them (numpy).  At the
+full workload: |A|, |B|, |A ∩ B| and the Jaccard f64 of the one-GPU compare
+(set unions of sorted runs + device intersection) equal numpy's union1d /
+intersect1d of all 64 device sets on the host, and the distributed compare
+through the library's exchange at P = 8 virtual ranks (okm_merge_owned_n
+over okm_comm_init_loopback) equals the one-GPU compare.  Every set is
+strictly increasing and canonical."""
 
 import os
 import threading
@@ -47,6 +49,9 @@ def c5_sets():
     plans = [workloads.c5_sample_plan(s) for s in range(64)]
     smallest = sorted(range(32), key=lambda s: plans[s][1])[:2] + \
         sorted(range(32, 64), key=lambda s: plans[s][1])[:2]
+    # + 8 samples across the size classes and read lengths (0.7 to 256 Mbases;
+    # 256 Mbases at 365 bp and at 20,008 bp reads)
+    exact = smallest + [7, 15, 24, 58, 57, 53, 0, 49]
     sets, kept, bases = [], {}, 0
     with okm.KmerCounter(K, "set") as ctx:
         for s in range(64):
@@ -59,14 +64,15 @@ def c5_sets():
             keys, _ = ctx.result(1)
             d.free()
             sets.append(keys)
-            if s in smallest:
+            if s in exact:
                 kept[s] = b
-    return sets, kept, bases
+    return sets, kept, bases, smallest
 
 
 def test_c5_sample_sets_exact_subset_and_properties(c5_sets):
-    sets, kept, bases = c5_sets
+    sets, kept, bases, smallest = c5_sets
     assert 11.0e9 < bases < 11.4e9  # the stated workload: 11.19 Gbases
+    assert len(kept) == 12
     for s, b in kept.items():  # exact sets (build.rs:50-58 DashSet) vs the restatement
         ek, _ = count_separated_mt(b, K, _threads())
         assert np.array_equal(sets[s], ek), s
@@ -77,7 +83,7 @@ def test_c5_sample_sets_exact_subset_and_properties(c5_sets):
         assert int(keys[-1]) < (1 << (2 * K))
         assert _canonical_ok(keys[rng.integers(0, len(keys), 100_000)]), s
     # the subset's unions and intersection on the device vs numpy (compare.rs:51-66)
-    sub = sorted(kept)
+    sub = sorted(smallest)
     a_sets, b_sets = [sets[s] for s in sub if s < 32], [sets[s] for s in sub if s >= 32]
     got = []
     for group in (a_sets, b_sets):
@@ -113,9 +119,45 @@ def _one_gpu_compare(sets):
     return out
 
 
-def test_c5_distributed_compare_p8_equals_one_gpu(c5_sets):
-    sets, _, _ = c5_sets
-    want = _one_gpu_compare(sets)
+def _host_compare(sets, threads):
+    """compare.rs:51-66 on the host: DB1 = union of sets 0-31, DB2 = union of
+    sets 32-63 (np.union1d of sorted unique arrays, key range by key range on
+    `threads` threads), |A ∩ B| by np.intersect1d per range."""
+    from concurrent.futures import ThreadPoolExecutor
+    edges = [int(x) for x in np.linspace(0, 1 << (2 * K), threads + 1)]
+
+    def part(r):
+        lo, hi = np.uint64(edges[r]), np.uint64(edges[r + 1])
+        def sl(x):
+            return x[np.searchsorted(x, lo):np.searchsorted(x, hi)]
+        a = np.unique(np.concatenate([sl(x) for x in sets[:32]]))
+        b = np.unique(np.concatenate([sl(x) for x in sets[32:]]))
+        return len(a), len(b), len(np.intersect1d(a, b, assume_unique=True))
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        parts = list(ex.map(part, range(threads)))
+    return tuple(int(sum(p[i] for p in parts)) for i in range(3))
+
+
+@pytest.fixture(scope="module")
+def c5_compare(c5_sets):
+    return _one_gpu_compare(c5_sets[0])
+
+
+def test_c5_compare_exact_vs_host_unions(c5_sets, c5_compare):
+    """|A|, |B|, |A ∩ B| and the Jaccard f64 (compare.rs:58-66) of the one-GPU
+    compare over all 64 device sets equal numpy's on the host."""
+    na, nb, inter = c5_compare
+    ha, hb, hi = _host_compare(c5_sets[0], _threads())
+    assert (na, nb, inter) == (ha, hb, hi)
+    union = na + nb - inter
+    assert inter / union == hi / (ha + hb - hi)
+    assert 0 < inter < min(na, nb)
+
+
+def test_c5_distributed_compare_p8_equals_one_gpu(c5_sets, c5_compare):
+    sets = c5_sets[0]
+    want = c5_compare
     na, nb, inter = want
     assert 0 < inter < min(na, nb)  # the two halves share half of their genomes
     P = 8

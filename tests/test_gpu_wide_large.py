@@ -17,7 +17,7 @@ import pytest
 import torch
 
 import okm
-from okm.dist import DeviceView
+from dist_rehearsal import DeviceView
 from oracle import count_separated_wide_ranges
 
 pytestmark = pytest.mark.gpu

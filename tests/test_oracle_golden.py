@@ -313,3 +313,32 @@ def test_wide_range_shards_equal_the_restatement(k):
     gk, gc, w = count_separated_wide_ranges(batch, k, threads=5)
     assert w == oc.windows
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+@pytest.mark.parametrize("k", [5, 21, 31, 32])
+def test_u64_range_filter_equals_the_restatement(k):
+    """The rolling key-range helper (count_separated_ranges_mt, used by the
+    full-size C3 and P = 8 rehearsal GPU tests) equals the O(k) restatement
+    restricted to the same ranges, over several chunks and threads."""
+    from oracle import count_separated_ranges_mt
+    import okm
+    batch = okm.synth_reads(4_000, 150, genome_len=50_000, genome_seed=k, seed=k + 3, sub_rate=0.02, n_rate=0.002)
+    batch.reshape(4_000, 151)[::89, :150] = ord("A")  # a hot key (all-A: key 0)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    top = 1 << (2 * k) if k < 32 else 1 << 64
+    rng = np.random.default_rng(k)
+    ranges = [(0, max(1, top >> 12))]  # includes key 0 (poly-A)
+    for _ in range(9):
+        a = int(rng.integers(0, top >> 1)) if k == 32 else int(rng.integers(0, top))
+        ranges.append((a, min(top - 1, a + max(1, top >> int(rng.integers(4, 9))))))
+    ranges.append((top - (top >> 6), top - 1))
+    sel = np.zeros(len(ek), bool)
+    for lo, hi in ranges:
+        sel |= (ek >= np.uint64(lo)) & (ek < np.uint64(hi))
+    half = 2_000 * 151
+    gk, gc, w = count_separated_ranges_mt([batch[:half], batch[half:]], k, ranges, threads=3)
+    assert w == oc.windows
+    assert sel.sum() > 10
+    assert np.array_equal(gk, ek[sel]) and np.array_equal(gc, ec[sel])
