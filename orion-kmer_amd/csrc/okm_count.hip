@@ -44,6 +44,9 @@ namespace okm {
 #ifndef OKM_COUNT_DESC_PF  // tag kernel: load the next item's descriptor while this item is counted
 #define OKM_COUNT_DESC_PF 0
 #endif
+#ifndef OKM_COUNT_LATE_RESET  // tag mode: per-home state reset inside the item's own phases, no trailing barriers
+#define OKM_COUNT_LATE_RESET 1
+#endif
 #ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
 #define OKM_FULL_RANK 1
 #endif
@@ -250,6 +253,7 @@ __device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *
                                                uint32_t *coff) {
     const uint32_t t = threadIdx.x;
     const uint32_t R = __builtin_amdgcn_readfirstlane(it.seg_count);
+    if (OKM_COUNT_LATE_RESET) lds_sync();  // the previous tag item's last step may still read the rest buffer
     if (t < R) {
         const DevSeg s = segs[it.seg_begin + t];
         ck[t] = s.keys;
@@ -551,6 +555,9 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     lds_sync();
     PMARK(2);
     // 2. rest offsets: thread t owns homes [4t, 4t+4) = words 2t, 2t+1
+    //    (late reset: the previous item's home offsets, read by its last step
+    //    before this item's first barrier, are cleared here)
+    if (OKM_COUNT_LATE_RESET) hd[2 * t] = hd[2 * t + 1] = 0;
     {
         const uint32_t w0 = rc[2 * t], w1 = rc[2 * t + 1];
         const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
@@ -606,9 +613,12 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             px[k] = x;
             pc[k] = c;
             if (first) {
-                prange[k] = (hs << 16) | he;
+                // bit 31: the home's tag sorts below x (a rest key never equals its
+                // home's tag), so step 6b need not read the tags again
+                const ull tgh = tag[h];
+                prange[k] = (hs << 16) | he | (tgh < x ? 0x80000000u : 0u);
                 atomicAdd(&hd[h >> 1], 1u << half_shift(h));
-                if (x < tag[h]) atomicAdd(&lt[h >> 1], 1u << half_shift(h));
+                if (x < tgh) atomicAdd(&lt[h >> 1], 1u << half_shift(h));
             }
         }
     }
@@ -618,6 +628,28 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     ull tg[kHomesPer];
     uint32_t ho[kHomesPer];
     uint32_t D;
+    // late reset: this thread's homes are read here for the last time (step 4,
+    // the last reader of other threads' tags and rest offsets, is behind the
+    // barrier above), so they are cleared at once for the next item
+    uint32_t lw0 = 0, lw1 = 0, nw0 = 0, nw1 = 0;  // rest keys below the tag; tag counts (u16 pairs)
+    ull tw[W ? kHomesPer : 1];                     // tag weights (weighted launches)
+    if (OKM_COUNT_LATE_RESET) {
+        lw0 = lt[2 * t];
+        lw1 = lt[2 * t + 1];
+        lt[2 * t] = lt[2 * t + 1] = 0;
+        rc[2 * t] = rc[2 * t + 1] = 0;
+        if (W) {
+#pragma unroll
+            for (int q = 0; q < kHomesPer; ++q) {
+                tw[q] = tc64[kHomesPer * t + q];
+                tc64[kHomesPer * t + q] = 0;
+            }
+        } else {
+            nw0 = tc16[2 * t];
+            nw1 = tc16[2 * t + 1];
+            tc16[2 * t] = tc16[2 * t + 1] = 0;
+        }
+    }
     {
         const uint32_t w0 = hd[2 * t], w1 = hd[2 * t + 1];
         uint32_t dq[kHomesPer] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
@@ -625,6 +657,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 #pragma unroll
         for (int q = 0; q < kHomesPer; ++q) {
             tg[q] = tag[kHomesPer * t + q];
+            if (OKM_COUNT_LATE_RESET) tag[kHomesPer * t + q] = kEmptyKey;
             dq[q] += tg[q] != kEmptyKey;
             ho[q] = d;
             d += dq[q];
@@ -639,11 +672,12 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     PMARK(6);
     // 6a. tags: rank = home offset + rest distinct keys below the tag
     {
-        const uint32_t l0 = lt[2 * t], l1 = lt[2 * t + 1];
+        const uint32_t l0 = OKM_COUNT_LATE_RESET ? lw0 : lt[2 * t], l1 = OKM_COUNT_LATE_RESET ? lw1 : lt[2 * t + 1];
         const uint32_t lq[kHomesPer] = {l0 & 0xFFFFu, l0 >> 16, l1 & 0xFFFFu, l1 >> 16};
         uint32_t nq[kHomesPer];
         if (!W) {
-            const uint32_t n0 = tc16[2 * t], n1 = tc16[2 * t + 1];
+            const uint32_t n0 = OKM_COUNT_LATE_RESET ? nw0 : tc16[2 * t];
+            const uint32_t n1 = OKM_COUNT_LATE_RESET ? nw1 : tc16[2 * t + 1];
             nq[0] = n0 & 0xFFFFu;
             nq[1] = n0 >> 16;
             nq[2] = n1 & 0xFFFFu;
@@ -654,7 +688,9 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             if (!NW && tg[q] != kEmptyKey) {
                 const uint64_t o = out_off + ho[q] + lq[q];
                 out_keys[o] = tg[q];
-                store_count<W>(out_counts, o, W ? (uint64_t)tc64[kHomesPer * t + q] : (uint64_t)nq[q]);
+                const uint64_t cq = W ? (OKM_COUNT_LATE_RESET ? (uint64_t)tw[q] : (uint64_t)tc64[kHomesPer * t + q])
+                                      : (uint64_t)nq[q];
+                store_count<W>(out_counts, o, cq);
             }
         }
     }
@@ -664,16 +700,22 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         if (NW || (uint32_t)k * kCB >= rtot) break;
         if (prange[k]) {
             const ull x = px[k];
-            const uint32_t hs = prange[k] >> 16, he = prange[k] & 0xFFFFu;
+            const uint32_t hs = (prange[k] >> 16) & 0x7FFFu, he = prange[k] & 0xFFFFu;
             uint32_t less = 0;
             for (uint32_t q = hs; q < he; ++q) less += (rf[q] && rk[q] < x) ? 1u : 0u;
             const uint32_t h = home_of(x, r);
-            const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + (tag[h] < x ? 1u : 0u);
+            const uint32_t tag_below = OKM_COUNT_LATE_RESET ? prange[k] >> 31 : (tag[h] < x ? 1u : 0u);
+            const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + tag_below;
             out_keys[o] = x;
             store_count<W>(out_counts, o, (uint64_t)pc[k]);
         }
     }
     PMARK(7);
+    // late reset: everything but the home offsets (hd, cleared in the next
+    // item's step 2) was cleared in step 5, and nothing read here is written
+    // before the next item's first barrier: no trailing barriers, the next
+    // item's loads overlap this step
+    if (OKM_COUNT_LATE_RESET) return __builtin_amdgcn_readfirstlane(D);
     // reset this thread's homes for the next item once every reader is done
     lds_sync();
 #pragma unroll

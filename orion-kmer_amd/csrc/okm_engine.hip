@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 
+#include "okm_arena.h"
 #include "okm_hip_try.h"
 #include "okm_internal.h"
 #include "okm_key.h"
@@ -64,11 +65,31 @@ static double hbm_cap_frac() {
     return frac;
 }
 
+// OKM_POOL=classic: the cache of whole hipMalloc blocks instead of the arena
+// (A/B runs); OKM_ARENA_CHUNK_MB: the arena's physical chunk (default 64 MiB).
+static bool arena_wanted() {
+    static const bool on = [] {
+        const char *e = getenv("OKM_POOL");
+        return !(e && strcmp(e, "classic") == 0);
+    }();
+    return on;
+}
+static size_t arena_chunk_bytes() {
+    static const size_t b = [] {
+        const char *e = getenv("OKM_ARENA_CHUNK_MB");
+        const long mb = e ? atol(e) : 64;
+        return (size_t)(mb > 0 ? mb : 64) << 20;
+    }();
+    return b;
+}
+
 struct DevPool {
     std::multimap<size_t, void *> free_;
     std::map<void *, size_t> size_;
     size_t held = 0;
     int device = 0;
+    int mode = -1;  // -1: undecided (first get), 0: whole-block cache, 1: arena
+    VmmArena arena;
     std::mutex mu;  // the owning context's thread, or another pool trimming this one on OOM
 
     void attach(int dev) {
@@ -80,7 +101,23 @@ struct DevPool {
         std::lock_guard<std::mutex> g(g_pools_mu);
         g_pools.erase(std::remove(g_pools.begin(), g_pools.end(), this), g_pools.end());
     }
+    bool arena_mode() {
+        std::lock_guard<std::mutex> g(mu);
+        return decide();
+    }
+    bool decide() {  // mu held
+        if (mode < 0) mode = arena_wanted() && arena.init(device, arena_chunk_bytes()) ? 1 : 0;
+        return mode == 1;
+    }
+    bool owns(const void *p) const {
+        const char *q = static_cast<const char *>(p);
+        return arena.base && q >= arena.base && q < arena.base + arena.reserved;
+    }
     okm_status get(size_t bytes, void **out) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (decide()) return arena_get(bytes, out);
+        }
         bytes = (bytes + 255) & ~size_t(255);
         if (bytes == 0) bytes = 256;
         if (bytes > (64u << 20)) {  // big buffers: 1/16 size classes, so run-to-run size jitter reuses blocks
@@ -185,6 +222,73 @@ struct DevPool {
                     p);
         return OKM_OK;
     }
+    // Arena allocation (mu held): a best-fit address range, then physical
+    // chunks for the parts of it that are not mapped yet.  Past the soft cap,
+    // idle chunks of this arena (then of the other pools on the device) are
+    // unmapped first — after a device sync, since a freed range's last kernel
+    // may still be in flight.
+    okm_status arena_get(size_t bytes, void **out) {
+        bytes = VmmArena::round_up(std::max<size_t>(bytes, 256), 256);
+        const size_t off = arena.take(bytes);
+        if (off == ~size_t(0))
+            return fail(OKM_E_NOMEM, "device arena: no free range of " + std::to_string(bytes) + " B");
+        const size_t c0 = arena.first_chunk(off), c1 = arena.last_chunk(off, bytes);
+        size_t missing = 0;
+        for (size_t i = c0; i <= c1; ++i) {
+            arena.chunks[i].users++;  // reserved: nobody unmaps them from here on
+            missing += !arena.chunks[i].mapped;
+        }
+        auto undo = [&]() {
+            for (size_t i = c0; i <= c1; ++i) arena.chunks[i].users--;
+            arena.give_back(off);
+        };
+        if (missing) {
+            const size_t need = missing * arena.chunk;
+            if (over_cap(need) && arena.idle()) {
+                (void)hipDeviceSynchronize();
+                arena.unmap_idle(need);
+            }
+            if (over_cap(need)) {  // other contexts' idle chunks (their locks, not ours)
+                mu.unlock();
+                trim_others();
+                mu.lock();
+            }
+            const auto t0 = std::chrono::steady_clock::now();
+            hipError_t e = hipSuccess;
+            for (size_t i = c0; i <= c1 && e == hipSuccess; ++i)
+                if (!arena.chunks[i].mapped) e = arena.map_chunk(i);
+            if (e != hipSuccess) {  // HBM full: give back everything idle and try once more
+                (void)hipGetLastError();
+                (void)hipDeviceSynchronize();
+                arena.unmap_idle(~size_t(0));
+                mu.unlock();
+                trim_others();
+                mu.lock();
+                e = hipSuccess;
+                for (size_t i = c0; i <= c1 && e == hipSuccess; ++i)
+                    if (!arena.chunks[i].mapped) e = arena.map_chunk(i);
+            }
+            held = arena.mapped;
+            if (getenv("OKM_PROFILE_HOST") || pool_trace())
+                fprintf(stderr, "[okm arena] mapped %zu chunks for %zu B in %.3f ms (mapped %.2f GB, in use %.2f GB)\n",
+                        missing, bytes,
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                        arena.mapped / 1e9, arena.in_use / 1e9);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                undo();
+                size_t fr = 0, tot = 0;
+                (void)hipMemGetInfo(&fr, &tot);
+                (void)hipGetLastError();
+                return fail(OKM_E_NOMEM, "device arena: mapping " + std::to_string(bytes) + " B: " +
+                                             hipGetErrorString(e) + " (context maps " + std::to_string(arena.mapped) +
+                                             " B, " + std::to_string(arena.in_use) + " B in use; device free " +
+                                             std::to_string(fr) + " of " + std::to_string(tot) + " B)");
+            }
+        }
+        *out = arena.base + off;
+        return OKM_OK;
+    }
     // Would `bytes` more take the device past the soft cap?
     bool over_cap(size_t bytes) const {
         const double frac = hbm_cap_frac();
@@ -199,19 +303,48 @@ struct DevPool {
     void put(void *p) {
         if (!p) return;
         std::lock_guard<std::mutex> g(mu);
+        if (owns(p)) {
+            const size_t off = static_cast<char *>(p) - arena.base;
+            auto it = arena.live.find(off);
+            if (it == arena.live.end()) return;  // a pointer inside a block (e.g. a table's counts)
+            for (size_t i = arena.first_chunk(off); i <= arena.last_chunk(off, it->second); ++i) arena.chunks[i].users--;
+            arena.give_back(off);
+            return;
+        }
         auto it = size_.find(p);
         if (it == size_.end()) return;
         if (pool_trace()) fprintf(stderr, "[pool] put %zu %p\n", it->second, p);
         free_.emplace(it->second, p);
     }
+    // Arena ranges only: keep the first `bytes` of the allocation at p (its
+    // tail returns to the arena, nothing moves); false when p is not an arena
+    // allocation.
+    bool shrink(void *p, size_t bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!owns(p)) return false;
+        const size_t off = static_cast<char *>(p) - arena.base;
+        if (!arena.live.count(off)) return false;
+        arena.shrink(off, VmmArena::round_up(std::max<size_t>(bytes, 256), 256));
+        return true;
+    }
     size_t size_of(const void *p) {
         std::lock_guard<std::mutex> g(mu);
+        if (owns(p)) {
+            auto it = arena.live.find(static_cast<const char *>(p) - arena.base);
+            return it == arena.live.end() ? 0 : it->second;
+        }
         auto it = size_.find(const_cast<void *>(p));
         return it == size_.end() ? 0 : it->second;
     }
     // OKM_POOL_DUMP=1 (tuning): every block, its size and whether it is cached
     void dump(const char *tag) {
         std::lock_guard<std::mutex> g(mu);
+        if (mode == 1) {
+            fprintf(stderr, "[okm arena %s] mapped %.2f GB, in use %.2f GB in %zu ranges, %zu free ranges, idle %.2f GB\n",
+                    tag, arena.mapped / 1e9, arena.in_use / 1e9, arena.live.size(), arena.free_off.size(),
+                    arena.idle() / 1e9);
+            return;
+        }
         size_t c = 0;
         for (auto &f : free_) c += f.first;
         fprintf(stderr, "[okm pool %s] %zu blocks, held %.2f GB, cached %.2f GB:", tag, size_.size(), held / 1e9, c / 1e9);
@@ -222,16 +355,27 @@ struct DevPool {
         }
         fprintf(stderr, "\n");
     }
+    // Bytes held but not in use (reusable without new device memory).
     size_t cached() {
         std::lock_guard<std::mutex> g(mu);
+        if (mode == 1) return arena.mapped - std::min(arena.mapped, arena.in_use);
         size_t b = 0;
         for (auto &kv : free_) b += kv.first;
         return b;
     }
     // hipFree synchronises the device, so a block freed here is idle even if
-    // its owner put it back while its kernels were still queued
+    // its owner put it back while its kernels were still queued (the arena
+    // synchronises before unmapping for the same reason)
     void trim() {
         std::lock_guard<std::mutex> g(mu);
+        if (mode == 1) {
+            if (arena.idle()) {
+                (void)hipDeviceSynchronize();
+                arena.unmap_idle(~size_t(0));
+                held = arena.mapped;
+            }
+            return;
+        }
         for (auto &kv : free_) {
             (void)hipFree(kv.second);
             held -= size_[kv.second];
@@ -246,6 +390,7 @@ struct DevPool {
     }
     void release_all() {
         std::lock_guard<std::mutex> g(mu);
+        arena.release();
         for (auto &kv : size_) (void)hipFree(kv.first);
         size_.clear();
         free_.clear();
@@ -1152,6 +1297,19 @@ static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, u
     const uint64_t kb = std::max<uint64_t>(n, 1) * 8 * c->kw, cb = std::max<uint64_t>(n, 1) * 8;
     const double held = (double)c->pool.size_of(*keys) + (double)c->pool.size_of(*counts);
     if (held <= slack * (double)(kb + cb) + (64u << 20)) return OKM_OK;
+    // arena: the table stays where it is and the allocations' tails go back
+    // (counts inside the keys' block, as count_and_compact lays a shared
+    // result out, or two allocations of their own)
+    {
+        const size_t kpad = (kb + 255) & ~size_t(255);
+        uint8_t *kbase = reinterpret_cast<uint8_t *>(*keys);
+        if (reinterpret_cast<uint8_t *>(*counts) == kbase + kpad && c->pool.size_of(*keys) >= kpad + cb &&
+            c->pool.shrink(*keys, kpad + cb))
+            return OKM_OK;
+        if (c->pool.size_of(*keys) && c->pool.size_of(*counts) && c->pool.shrink(*keys, kb) &&
+            c->pool.shrink(*counts, cb))
+            return OKM_OK;
+    }
     // keys and counts in ONE block (the counts pointer lies inside it, and the
     // pool ignores it on put): a table kept for long (a folded run, a group's
     // table) then takes one cached block of its total size, where two requests
@@ -2142,7 +2300,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     } else {
         nd = 0;
         for (auto &t : tabs) nd += t.n;
-        c->pool.trim();  // the groups' working buffers make room for the joined table
+        if (!c->pool.arena_mode()) c->pool.trim();  // the groups' working buffers make room for the joined table
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         uint64_t o = 0;

@@ -241,6 +241,170 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
 }
 
 // ---------------------------------------------------------------------------
+// query over a minimizer-bucketed copy of the set
+//
+// The hash set costs one random 128-B line per probed window (one HBM line
+// per window at C2 scale: 0.79 of the random-probe ceiling).
+// Here the set's keys are grouped by the MINIMIZER of each k-mer: the m-mer
+// (m = min(k, 15)) whose canonical value has the smallest hash among the
+// k - m + 1 m-mers of the k-mer.  The canonical m-mers of a k-mer and of its
+// reverse complement are the same set, so a window and the canonical key
+// agree on the minimizer whatever strand the read came from.  Consecutive
+// windows of a read share their minimizer for ~(k - m + 2) / 2 windows on
+// average, so the ~120 windows of a 150-bp read touch ~17 buckets (a
+// directory word pair and a short key run each) instead of ~120 random
+// slots.  The hits are exactly the hash set's (query.rs:86-93: membership of
+// the canonical key); only where the key is looked up changes.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMiniM = 15;        // m-mer length (m = min(k, 15))
+constexpr uint32_t kMiniPerBucket = 4; // average keys per bucket
+constexpr uint32_t kMiniMaxBucket = 256;  // larger buckets (low-complexity key families): the hash path
+
+struct MiniTab {
+    const ull *keys;   // the set's keys grouped by bucket
+    const ull *dir;    // bucket b holds keys[dir[b], dir[b + 1])
+    uint32_t nb;       // buckets
+    uint32_t m;        // m-mer length
+};
+
+__host__ __device__ __forceinline__ uint32_t mini_hash(uint32_t canon_m) {  // murmur3 fmix32, seeded
+    uint32_t h = canon_m ^ 0x9E3779B9u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+__host__ __device__ __forceinline__ uint32_t mini_bucket(uint32_t h, uint32_t nb) {
+    return (uint32_t)(((uint64_t)h * nb) >> 32);
+}
+__host__ __device__ __forceinline__ uint32_t canon_mmer(uint32_t fwd, uint32_t m) {
+    const uint32_t mask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
+    const uint32_t rc = ~rev2(fwd << (32 - 2 * m)) & mask;  // reverse complement of the m bases
+    return fwd < rc ? fwd : rc;
+}
+// Bucket of a canonical k-mer key (2k bits, MSB-first).
+__host__ __device__ __forceinline__ uint32_t key_bucket(uint64_t key, uint32_t k, uint32_t m, uint32_t nb) {
+    const uint32_t mask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
+    uint32_t best = ~0u;
+    for (uint32_t i = 0; i + m <= k; ++i) {
+        const uint32_t f = (uint32_t)(key >> (2 * (k - m - i))) & mask;  // bases i .. i+m-1
+        const uint32_t h = mini_hash(canon_mmer(f, m));
+        best = h < best ? h : best;
+    }
+    return mini_bucket(best, nb);
+}
+
+__global__ __launch_bounds__(kProbeBlock) void k_mini_count(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
+                                                            uint32_t m, uint32_t nb, ull *__restrict__ cnt,
+                                                            ull *__restrict__ maxb) {
+    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
+    ull mx = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
+        const ull x = slots[i];
+        if (x == kEmpty) continue;
+        const ull r = atomicAdd(&cnt[key_bucket(x, k, m, nb)], 1ull) + 1;
+        mx = r > mx ? r : mx;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const ull o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(maxb, mx);
+}
+
+__global__ __launch_bounds__(kProbeBlock) void k_mini_place(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
+                                                            uint32_t m, uint32_t nb, ull *__restrict__ cursor,
+                                                            ull *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
+        const ull x = slots[i];
+        if (x == kEmpty) continue;
+        out[atomicAdd(&cursor[key_bucket(x, k, m, nb)], 1ull)] = x;
+    }
+}
+
+// k_query_hits over the bucketed set: the thread's 16 windows, their keys and
+// validity as in k_query_hits, then the 16 + k - m canonical m-mer hashes
+// they span, each window's minimizer (the minimum over its k - m + 1), and a
+// scan of its bucket; a bucket's directory words are read once per run of
+// windows that share it.
+template <int K>
+__global__ __launch_bounds__(kProbeBlock) void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
+                                                                 const ull *__restrict__ tile_pre, MiniTab t,
+                                                                 uint32_t k_rt, uint32_t *__restrict__ hits,
+                                                                 uint64_t nrec) {
+    __shared__ ull wsum[kProbeBlock / 64];
+    const uint64_t w0 = (uint64_t)blockIdx.x * kQTile + (uint64_t)threadIdx.x * kQSeg;
+    // 64 bytes: the m-mer slices reach one code word past the windows' 48
+    WinWords<kQSeg, 48> ww;
+    load_windows<kQSeg, 48>(seq, n, w0, ww);
+    const uint32_t *w = ww.w;
+    const uint32_t sepm = w0 < n ? sep_mask16(w) : 0u;
+    ull tot;
+    const ull rec0 = tile_pre[blockIdx.x] + block_excl_scan<kProbeBlock>((ull)__popc(sepm), wsum, &tot);
+    if (w0 >= n) return;
+
+    const uint32_t k = K ? (uint32_t)K : k_rt;
+    const uint32_t m = K ? (K < (int)kMiniM ? (uint32_t)K : kMiniM) : t.m;
+    constexpr int NP = WinWords<kQSeg, 48>::kLoad / 16;
+    Codes<NP> c;
+    make_codes<NP, true>(w, c);  // query.rs: raw bytes, U invalid
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int j = 0; j < kQSeg; ++j) {
+        bool valid;
+        (void)window_key(c, j, k, &valid);
+        vmask |= (valid ? 1u : 0u) << j;
+    }
+    // m-mer hashes at bases 0 .. 15 + k - m (<= 32 positions)
+    const uint32_t span = k - m;  // a window's m-mers: j .. j + span
+    const uint32_t mmask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
+    uint32_t h[kQSeg + 17];  // span <= 32 - 15
+#pragma unroll
+    for (int i = 0; i < kQSeg + 17; ++i) {
+        if ((uint32_t)i > kQSeg - 1 + span) break;
+        const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
+        const uint32_t r = rc32(c, 2 * i) & mmask;
+        h[i] = mini_hash(f < r ? f : r);
+    }
+    ull rec = rec0;
+    uint32_t cur = 0;
+    uint32_t pb = ~0u;
+    ull s = 0, e = 0;
+#pragma unroll
+    for (int j = 0; j < kQSeg; ++j) {
+        if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
+            flush_hits(hits, nrec, rec, cur);
+            cur = 0;
+            ++rec;
+        }
+        if ((vmask >> j) & 1u) {
+            uint32_t mn = h[j];
+            if (K) {
+#pragma unroll
+                for (uint32_t d = 1; d <= (K > (int)kMiniM ? (uint32_t)K - kMiniM : 0u); ++d) mn = min(mn, h[j + d]);
+            } else {
+                for (uint32_t d = 1; d <= span; ++d) mn = min(mn, h[j + d]);
+            }
+            const uint32_t b = mini_bucket(mn, t.nb);
+            if (b != pb) {
+                s = t.dir[b];
+                e = t.dir[b + 1];
+                pb = b;
+            }
+            const ull key = window_key_nv(c, j, k);
+            bool hit = false;
+            for (ull q = s; q < e && !hit; ++q) hit = t.keys[q] == key;
+            cur += hit ? 1u : 0u;
+        }
+    }
+    flush_hits(hits, nrec, rec, cur);
+}
+
+// ---------------------------------------------------------------------------
 // classify: map of the filtered input counts, probed by every reference key
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kProbeBlock) void k_map_build(MapTab t, const ull *__restrict__ keys,
@@ -439,8 +603,16 @@ struct okm_kset {
     ull *d_ctr = nullptr;  // [0]: new keys of the last insert
     Scratch keys, batch, tiles, hits;
     std::vector<uint8_t> host_batch;
+    // minimizer-bucketed copy of the keys (query): built at the first query
+    // after an insert; mini_ok false when a bucket is too big for the scan
+    Scratch mini_keys, mini_dir;
+    uint32_t mini_nb = 0;
+    bool mini_built = false, mini_ok = false;
 
     SetTab tab() const { return SetTab{slots, cap - 1, 64u - log2_exact(cap)}; }
+    MiniTab mini() const {
+        return MiniTab{(const ull *)mini_keys.p, (const ull *)mini_dir.p, mini_nb, k < kMiniM ? (uint32_t)k : kMiniM};
+    }
 };
 
 struct okm_classifier {
@@ -489,6 +661,7 @@ okm_status set_reserve(okm_kset *s, uint64_t n) {
 }
 
 okm_status set_insert_device(okm_kset *s, const uint64_t *d_keys, uint64_t n, uint64_t *n_new) {
+    s->mini_built = false;
     PTRY(set_reserve(s, n));
     PHIP(hipMemsetAsync(s->d_ctr, 0, sizeof(ull), s->st));
     hipLaunchKernelGGL(k_set_insert, dim3(grid_for(n)), dim3(kProbeBlock), 0, s->st, s->tab(),
@@ -509,6 +682,56 @@ void launch_query_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pr
                        (uint32_t)s->k, d_hits, nrec);
 }
 
+// OKM_QUERY_MINI=0: the hash-set probe kernel instead of the bucketed copy.
+bool query_mini_wanted() {
+    const char *e = getenv("OKM_QUERY_MINI");
+    return !(e && *e == '0');
+}
+
+// The minimizer-bucketed copy of the set (k_mini_count / scan / k_mini_place).
+okm_status mini_build(okm_kset *s) {
+    s->mini_built = true;
+    s->mini_ok = false;
+    if (s->size == 0) return OKM_OK;
+    const uint32_t m = s->k < kMiniM ? s->k : kMiniM;
+    const uint64_t nb64 = std::max<uint64_t>(1, (s->size + kMiniPerBucket - 1) / kMiniPerBucket);
+    if (nb64 >= 0xFFFFFFFFull) return OKM_OK;
+    const uint32_t nb = (uint32_t)nb64;
+    const size_t tmp = scan_tmp_elems((uint64_t)nb + 1);
+    PTRY(s->mini_dir.ensure(((size_t)nb + 1 + (size_t)nb + 1 + tmp + 1) * sizeof(ull)));
+    PTRY(s->mini_keys.ensure((size_t)s->size * sizeof(ull)));
+    ull *cnt = (ull *)s->mini_dir.p + (nb + 1), *scr = cnt + (nb + 1), *maxb = scr + tmp;
+    ull *dir = (ull *)s->mini_dir.p;
+    PHIP(hipMemsetAsync(cnt, 0, ((size_t)nb + 1) * sizeof(ull), s->st));
+    PHIP(hipMemsetAsync(maxb, 0, sizeof(ull), s->st));
+    hipLaunchKernelGGL(k_mini_count, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
+                       s->cap, (uint32_t)s->k, m, nb, cnt, maxb);
+    PHIP(hipGetLastError());
+    launch_exclusive_scan(s->st, cnt, dir, (uint64_t)nb + 1, scr);
+    PHIP(hipMemcpyAsync(cnt, dir, ((size_t)nb + 1) * sizeof(ull), hipMemcpyDeviceToDevice, s->st));
+    hipLaunchKernelGGL(k_mini_place, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
+                       s->cap, (uint32_t)s->k, m, nb, cnt, (ull *)s->mini_keys.p);
+    PHIP(hipGetLastError());
+    ull h[2] = {0, 0};
+    PHIP(hipMemcpyAsync(&h[0], maxb, sizeof(ull), hipMemcpyDeviceToHost, s->st));
+    PHIP(hipMemcpyAsync(&h[1], dir + nb, sizeof(ull), hipMemcpyDeviceToHost, s->st));
+    PHIP(hipStreamSynchronize(s->st));
+    s->mini_nb = nb;
+    // every key placed (the ~0 key of a database lives in the hash set's flag
+    // word only, and never equals a window's canonical key)
+    const char *mb = getenv("OKM_QUERY_MINI_MAXB");  // tests: force the hash-set fallback
+    const uint64_t maxb_ok = mb && atoll(mb) > 0 ? (uint64_t)atoll(mb) : kMiniMaxBucket;
+    s->mini_ok = h[0] <= maxb_ok && h[1] <= s->size;
+    return OKM_OK;
+}
+
+template <int K>
+void launch_query_mini_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pre, uint32_t *d_hits,
+                         uint64_t nrec, uint32_t ntiles) {
+    hipLaunchKernelGGL(k_query_hits_mini<K>, dim3(ntiles), dim3(kProbeBlock), 0, s->st, d_seq, n, pre, s->mini(),
+                       (uint32_t)s->k, d_hits, nrec);
+}
+
 okm_status query_device(okm_kset *s, const uint8_t *d_seq, uint64_t n, uint64_t nrec, uint32_t *d_hits) {
     PHIP(hipMemsetAsync(d_hits, 0, nrec * sizeof(uint32_t), s->st));
     if (n == 0 || s->size == 0) return OKM_OK;
@@ -519,6 +742,19 @@ okm_status query_device(okm_kset *s, const uint8_t *d_seq, uint64_t n, uint64_t 
     ull *cnt = (ull *)s->tiles.p, *pre = cnt + ntiles, *scr = pre + ntiles;
     hipLaunchKernelGGL(k_sep_count, dim3((uint32_t)ntiles), dim3(kProbeBlock), 0, s->st, d_seq, n, cnt);
     launch_exclusive_scan(s->st, cnt, pre, ntiles, scr);
+    if (query_mini_wanted() && !s->mini_built) PTRY(mini_build(s));
+    if (query_mini_wanted() && s->mini_ok) {
+        switch (s->k) {
+        case 21: launch_query_mini_k<21>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        case 25: launch_query_mini_k<25>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        case 27: launch_query_mini_k<27>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        case 31: launch_query_mini_k<31>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        case 32: launch_query_mini_k<32>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        default: launch_query_mini_k<0>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
+        }
+        PHIP(hipGetLastError());
+        return OKM_OK;
+    }
     switch (s->k) {
     case 21: launch_query_k<21>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
     case 25: launch_query_k<25>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
@@ -569,6 +805,8 @@ void okm_kset_destroy(okm_kset *s) {
     s->batch.release();
     s->tiles.release();
     s->hits.release();
+    s->mini_keys.release();
+    s->mini_dir.release();
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }

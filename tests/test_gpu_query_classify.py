@@ -148,8 +148,10 @@ def _reads(rng, genome, n, lo, hi, noise=0.01, lower=0.0):
     return out
 
 
-@pytest.mark.parametrize("k", [31, 21, 32, 17, 5])
-def test_query_hits_vs_oracle(k):
+@pytest.mark.parametrize("mini", ["1", "0"], ids=["minimizer-index", "hash-set"])
+@pytest.mark.parametrize("k", [31, 21, 32, 17, 5, 15, 16, 27])
+def test_query_hits_vs_oracle(k, mini, monkeypatch):
+    monkeypatch.setenv("OKM_QUERY_MINI", mini)
     rng = np.random.default_rng(100 + k)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000)
     # the DB: the genome's first 60 % as two references
@@ -166,6 +168,37 @@ def test_query_hits_vs_oracle(k):
         got = s.query_hits(reads)
     assert np.array_equal(got, exp)
     assert exp.sum() > 0
+
+
+def _revcomp(b: bytes) -> bytes:
+    return b[::-1].translate(bytes.maketrans(b"ACGTacgt", b"TGCAtgca"))
+
+
+@pytest.mark.parametrize("k", [31, 25, 12])
+def test_query_minimizer_index_strands_and_fallback(k, monkeypatch):
+    """The minimizer-bucketed set (okm_probe.hip k_query_hits_mini) finds a
+    canonical key from either strand of a read; an index whose biggest bucket
+    is past the scan limit (forced here with OKM_QUERY_MINI_MAXB) falls back to
+    the hash-set probe; every path equals the restatement."""
+    rng = np.random.default_rng(k)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=150_000)
+    g = genome.tobytes()
+    fwd = [g[o:o + int(rng.integers(40, 300))] for o in rng.integers(0, 140_000, 3000)]
+    reads = fwd + [_revcomp(r) for r in fwd[:1500]]  # the other strand of half of them
+    oc = OracleCounter(k)
+    oc.add_records([g[:90_000]])
+    db_keys, _ = oc.result(1)
+    exp = oracle.query_hits(reads, db_keys, k)
+    for mini, maxb in (("1", ""), ("1", "2"), ("0", "")):  # index; index forced back to the hash set; hash set
+        monkeypatch.setenv("OKM_QUERY_MINI", mini)
+        monkeypatch.setenv("OKM_QUERY_MINI_MAXB", maxb)
+        with okm.KmerSet(k, 0, len(db_keys)) as s:
+            s.insert(db_keys)
+            got = s.query_hits(reads)
+            s.insert(db_keys[:10])  # an insert drops the index; the next query rebuilds it
+            again = s.query_hits(reads)
+        assert np.array_equal(got, exp) and np.array_equal(again, exp), (mini, maxb)
+    assert exp[1500:3000].sum() > 0 and exp[3000:4500].sum() > 0  # both strands hit
 
 
 def test_query_hits_device_batch_long_records():

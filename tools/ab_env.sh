@@ -1,11 +1,28 @@
 #!/bin/bash
-# A/B timing of environment settings of one build (C2 bench):
-#   tools/ab_env.sh name1 'VAR=val ...' name2 'VAR=val ...' ...
-# one JSON line per setting in gpurun_out/ab/<name>.json and a summary line each
+# Interleaved A/B of environment settings on one build (box-to-box and
+# process-to-process clocks drift): tools/ab_env.sh REPS "NAME=ENV ..." ...
+# e.g. tools/ab_env.sh 3 "classic=OKM_POOL=classic" "arena=" ; one C2 bench per
+# (rep, setting), round-robin; medians per setting at the end.  Extra bench.py
+# arguments in AB_BENCH_ARGS.
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/ab
-while [ $# -ge 2 ]; do
-  n=$1; e=$2; shift 2
-  env $e timeout -k 10 200 python bench.py --c3-steps 0 --steps 10 --warmup 2 --cpu-sample-reads 0 > gpurun_out/ab/$n.json 2> gpurun_out/ab/$n.err || exit 1
-  python3 -c "import json; d=json.load(open('gpurun_out/ab/$n.json')); print('$n', d['ms_per_step'], {k: v['avg_ms'] for k, v in d['kernels'].items() if v['avg_ms'] > 0.03})"
+mkdir -p gpurun_out/abe
+reps=$1; shift
+names=()
+for r in $(seq 1 "$reps"); do
+  for spec in "$@"; do
+    n=${spec%%=*}; envs=${spec#*=}
+    [ "$r" = 1 ] && names+=("$n")
+    env $envs timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-sample-reads 0 --cpu-mt-reads 0 \
+      ${AB_BENCH_ARGS:---c3-steps 0} > gpurun_out/abe/${n}_$r.json 2> gpurun_out/abe/${n}_$r.err || exit 1
+  done
 done
+python3 - "${names[@]}" <<'PY'
+import glob, json, statistics, sys
+for n in sys.argv[1:]:
+    runs = [json.load(open(f)) for f in sorted(glob.glob(f"gpurun_out/abe/{n}_*.json"))]
+    ks = runs[0]["kernels"].keys()
+    med = {k: round(statistics.median(r["kernels"][k]["avg_ms"] for r in runs), 4) for k in ks}
+    c3 = [r["c3"]["ms_per_step"] for r in runs if isinstance(r.get("c3"), dict) and "ms_per_step" in r["c3"]]
+    print(n, "step", round(statistics.median(r["ms_per_step"] for r in runs), 3),
+          [round(r["ms_per_step"], 3) for r in runs], "c3", c3, med)
+PY
