@@ -1,7 +1,7 @@
 // okm_arena.h — a counting context's device memory arena.
 //
 // One reserved virtual address range per context (2x the device's HBM), with
-// physical memory mapped into it in fixed chunks (hipMemCreate / hipMemMap)
+// physical memory mapped into it in fixed chunks (hipMemCreate / hipMemMap; 1 GiB)
 // as allocations need them.  Allocations are best-fit ranges of the address
 // space; freed ranges coalesce with their neighbours, so a 9 GB request is
 // served by any free 9 GB stretch, whatever sizes were freed to make it.

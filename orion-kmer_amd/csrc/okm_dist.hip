@@ -369,11 +369,19 @@ class Transport {
     // after a failure inside a collective: peers blocked in one return an error
     virtual void abort() = 0;
     virtual const char *name() const = 0;
+    // true: send buffers must be plain hipMalloc memory of the communicator
+    // (the counting contexts' tables live in a virtual-memory arena, which
+    // RCCL's peer-to-peer paths are not given to register or map)
+    virtual bool owned_send_buffers() const { return false; }
 };
 
 class RcclTransport final : public Transport {
   public:
     explicit RcclTransport(ncclComm_t nc) : nc_(nc) {}
+    bool owned_send_buffers() const override {
+        const char *e = getenv("OKM_RCCL_SEND_IN_PLACE");  // 1: send the table slices in place (A/B)
+        return !(e && *e == '1');
+    }
     ~RcclTransport() override {
         if (nc_) (void)rccl().CommDestroy(nc_);
     }
@@ -591,6 +599,7 @@ struct okm_comm {
     hipStream_t stream = nullptr;
     DevBuf starts, hist, hsum, cut, sizes, gsizes, low, esc_cnt, esc_cur, esc, rk, rlow, rc, resc, offs, flag;
     DevBuf k5, kesc, kesc_cur, rk5, rkesc, stmp;  // keys as 5-byte deltas (+ key escapes, scan scratch)
+    DevBuf ksend;  // u64 keys sent from communicator memory (Transport::owned_send_buffers)
     ull *hpin = nullptr;  // pinned landing area for the small readbacks
     size_t hpin_cap = 0;
     double last_ms[4] = {0, 0, 0, 0};  // plan, exchange, unpack, merge (host wall, last okm_merge_owned)
@@ -772,6 +781,10 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     okm_status st = OKM_OK;
     if (!set) st = m->low.ensure(std::max<uint64_t>(n, 16));
     if (deltas && st == OKM_OK) st = m->k5.ensure(5 * std::max<uint64_t>(n, 16));
+    // u64 keys go out of communicator memory (owned_send_buffers): staged below,
+    // allocated here so that a failure is still reported to the peers
+    if (!deltas && st == OKM_OK && tp.owned_send_buffers())
+        st = m->ksend.ensure(kw * std::max<uint64_t>(n, 16) * sizeof(uint64_t));
     hs[3 * P] = st != OKM_OK;
     HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), row * sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, 2 * P * sizeof(ull), s));
@@ -883,6 +896,11 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
         if (count) msgs.push_back(Msg{send, (uint8_t *)const_cast<void *>(buf), count, esize, (int)peer});
     };
     uint64_t bytes_out = 0, bytes_in = 0;
+    const uint64_t *ksrc = dk;  // u64 keys: the local table's slices, in place or staged
+    if (!deltas && n && tp.owned_send_buffers()) {
+        HIP_TRY(hipMemcpyAsync(m->ksend.p, dk, kw * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+        ksrc = m->ksend.as<uint64_t>();
+    }
     for (uint32_t r = 0; r < P; ++r) {
         if (deltas) {  // 5 bytes per key + key escapes
             add(true, m->k5.as<uint8_t>() + 5 * cut[r], 5 * ss[r], 1, r);
@@ -890,7 +908,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
             add(true, m->kesc.as<uint64_t>() + 2 * ksoff[r], 2 * ks[r], 8, r);
             add(false, m->rkesc.as<uint64_t>() + 2 * kroff[r], 2 * kr[r], 8, r);
         } else {
-            add(true, dk + kw * cut[r], kw * ss[r], 8, r);
+            add(true, ksrc + kw * cut[r], kw * ss[r], 8, r);
             add(false, m->rk.as<uint64_t>() + kw * roff[r], kw * rs[r], 8, r);
         }
         if (!set) {
@@ -1115,7 +1133,7 @@ void okm_comm_destroy(okm_comm *m) {
     m->tp.reset();
     for (DevBuf *b : {&m->starts, &m->hist, &m->hsum, &m->cut, &m->sizes, &m->gsizes, &m->low, &m->esc_cnt,
                       &m->esc_cur, &m->esc, &m->rk, &m->rlow, &m->rc, &m->resc, &m->offs, &m->flag, &m->k5, &m->kesc,
-                      &m->kesc_cur, &m->rk5, &m->rkesc, &m->stmp})
+                      &m->kesc_cur, &m->rk5, &m->rkesc, &m->stmp, &m->ksend})
         b->release();
     if (m->hpin) (void)hipHostFree(m->hpin);
     if (m->stream) (void)hipStreamDestroy(m->stream);

@@ -256,15 +256,16 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
 // slots.  The hits are exactly the hash set's (query.rs:86-93: membership of
 // the canonical key); only where the key is looked up changes.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kMiniM = 15;        // m-mer length (m = min(k, 15))
-constexpr uint32_t kMiniPerBucket = 4; // average keys per bucket
-constexpr uint32_t kMiniMaxBucket = 256;  // larger buckets (low-complexity key families): the hash path
+constexpr uint32_t kMiniM = 15;     // m-mer length (m = min(k, 15))
+constexpr uint32_t kMiniRow = 4;    // keys a bucket row holds (32 B)
+constexpr uint32_t kMiniPerBucket = 2;  // buckets = keys / 2: rows overflow for ~1 % of the keys
 
 struct MiniTab {
-    const ull *keys;   // the set's keys grouped by bucket
-    const ull *dir;    // bucket b holds keys[dir[b], dir[b + 1])
-    uint32_t nb;       // buckets
-    uint32_t m;        // m-mer length
+    const ull *rows;      // nb rows of kMiniRow keys (~0: empty slot)
+    const uint32_t *ovf;  // bit b: bucket b had more keys than its row holds
+    SetTab spill;         // ... those keys
+    uint32_t nb;          // buckets
+    uint32_t m;           // m-mer length
 };
 
 __host__ __device__ __forceinline__ uint32_t mini_hash(uint32_t canon_m) {  // murmur3 fmix32, seeded
@@ -296,43 +297,42 @@ __host__ __device__ __forceinline__ uint32_t key_bucket(uint64_t key, uint32_t k
     return mini_bucket(best, nb);
 }
 
-__global__ __launch_bounds__(kProbeBlock) void k_mini_count(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
-                                                            uint32_t m, uint32_t nb, ull *__restrict__ cnt,
-                                                            ull *__restrict__ maxb) {
-    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
-    ull mx = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
-        const ull x = slots[i];
-        if (x == kEmpty) continue;
-        const ull r = atomicAdd(&cnt[key_bucket(x, k, m, nb)], 1ull) + 1;
-        mx = r > mx ? r : mx;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const ull o = __shfl_xor(mx, d, 64);
-        mx = o > mx ? o : mx;
-    }
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(maxb, mx);
-}
-
-__global__ __launch_bounds__(kProbeBlock) void k_mini_place(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
-                                                            uint32_t m, uint32_t nb, ull *__restrict__ cursor,
-                                                            ull *__restrict__ out) {
+// Every key of the hash set into its bucket's row; a row's fifth and later
+// keys go to the spill set (ctl[0]: spill inserts, ctl[1]: 1 when the spill
+// set would pass half load -- the index is then not used).
+__global__ __launch_bounds__(kProbeBlock) void k_mini_fill(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
+                                                           uint32_t m, uint32_t nb, ull *__restrict__ rows,
+                                                           uint32_t *__restrict__ cnt, uint32_t *__restrict__ ovf,
+                                                           SetTab spill, ull *__restrict__ ctl) {
     const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
         const ull x = slots[i];
         if (x == kEmpty) continue;
-        out[atomicAdd(&cursor[key_bucket(x, k, m, nb)], 1ull)] = x;
+        const uint32_t b = key_bucket(x, k, m, nb);
+        const uint32_t r = atomicAdd(&cnt[b], 1u);
+        if (r < kMiniRow) {
+            rows[(uint64_t)b * kMiniRow + r] = x;
+            continue;
+        }
+        atomicOr(&ovf[b >> 5], 1u << (b & 31));
+        if (atomicAdd(&ctl[0], 1ull) < (spill.mask + 1) / 2)
+            set_insert(spill, x);
+        else
+            atomicOr(&ctl[1], 1ull);
     }
 }
 
-// k_query_hits over the bucketed set: the thread's 16 windows, their keys and
-// validity as in k_query_hits, then the 16 + k - m canonical m-mer hashes
-// they span, each window's minimizer (the minimum over its k - m + 1), and a
-// scan of its bucket; a bucket's directory words are read once per run of
-// windows that share it.
+// k_query_hits over the bucketed set: the thread's 16 windows, their
+// validity as in k_query_hits, the 16 + k - m canonical m-mer hashes they
+// span and each window's minimizer bucket; then, OKM_QUERY_MINI_GROUP windows at a time, every
+// valid window's 32-B bucket row is loaded (rows of consecutive windows are
+// mostly the same: cache hits) and compared with its canonical key; a key
+// missing from a full row whose bucket overflowed is looked up in the spill set.
+#ifndef OKM_QUERY_MINI_GROUP  // windows whose rows are loaded together
+#define OKM_QUERY_MINI_GROUP 4
+#endif
 template <int K>
-__global__ __launch_bounds__(kProbeBlock) void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
+__global__ __launch_bounds__(kProbeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
                                                                  const ull *__restrict__ tile_pre, MiniTab t,
                                                                  uint32_t k_rt, uint32_t *__restrict__ hits,
                                                                  uint64_t nrec) {
@@ -352,36 +352,22 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits_mini(const uint8_t *
     constexpr int NP = WinWords<kQSeg, 48>::kLoad / 16;
     Codes<NP> c;
     make_codes<NP, true>(w, c);  // query.rs: raw bytes, U invalid
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        bool valid;
-        (void)window_key(c, j, k, &valid);
-        vmask |= (valid ? 1u : 0u) << j;
-    }
-    // m-mer hashes at bases 0 .. 15 + k - m (<= 32 positions)
+    const uint32_t vmask = ~invalid_windows<kQSeg, NP>(c, k) & 0xFFFFu;
+    // minimizer bucket of every window
     const uint32_t span = k - m;  // a window's m-mers: j .. j + span
     const uint32_t mmask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
-    uint32_t h[kQSeg + 17];  // span <= 32 - 15
+    uint32_t bk[kQSeg];
+    {
+        uint32_t h[kQSeg + 17];  // span <= 32 - 15
 #pragma unroll
-    for (int i = 0; i < kQSeg + 17; ++i) {
-        if ((uint32_t)i > kQSeg - 1 + span) break;
-        const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
-        const uint32_t r = rc32(c, 2 * i) & mmask;
-        h[i] = mini_hash(f < r ? f : r);
-    }
-    ull rec = rec0;
-    uint32_t cur = 0;
-    uint32_t pb = ~0u;
-    ull s = 0, e = 0;
-#pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
-            flush_hits(hits, nrec, rec, cur);
-            cur = 0;
-            ++rec;
+        for (int i = 0; i < kQSeg + 17; ++i) {
+            if ((uint32_t)i > kQSeg - 1 + span) break;
+            const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
+            const uint32_t r = rc32(c, 2 * i) & mmask;
+            h[i] = mini_hash(f < r ? f : r);
         }
-        if ((vmask >> j) & 1u) {
+#pragma unroll
+        for (int j = 0; j < kQSeg; ++j) {
             uint32_t mn = h[j];
             if (K) {
 #pragma unroll
@@ -389,17 +375,45 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits_mini(const uint8_t *
             } else {
                 for (uint32_t d = 1; d <= span; ++d) mn = min(mn, h[j + d]);
             }
-            const uint32_t b = mini_bucket(mn, t.nb);
-            if (b != pb) {
-                s = t.dir[b];
-                e = t.dir[b + 1];
-                pb = b;
-            }
-            const ull key = window_key_nv(c, j, k);
-            bool hit = false;
-            for (ull q = s; q < e && !hit; ++q) hit = t.keys[q] == key;
-            cur += hit ? 1u : 0u;
+            bk[j] = mini_bucket(mn, t.nb);
         }
+    }
+    uint32_t hitm = 0;  // bit j: window j's key is in the set
+    constexpr int G = OKM_QUERY_MINI_GROUP;
+#pragma unroll
+    for (int half = 0; half < kQSeg / G; ++half) {
+        ulonglong2 r0[G], r1[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {  // every row load of the group's windows in flight together
+            const int j = G * half + u;
+            if ((vmask >> j) & 1u) {
+                const ulonglong2 *row = reinterpret_cast<const ulonglong2 *>(t.rows + (uint64_t)bk[j] * kMiniRow);
+                r0[u] = row[0];
+                r1[u] = row[1];
+            } else {
+                r0[u] = r1[u] = make_ulonglong2(kEmpty, kEmpty);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int j = G * half + u;
+            if (!((vmask >> j) & 1u)) continue;
+            const ull key = window_key_nv(c, j, k);
+            bool hit = r0[u].x == key || r0[u].y == key || r1[u].x == key || r1[u].y == key;
+            if (!hit && r1[u].y != kEmpty && ((t.ovf[bk[j] >> 5] >> (bk[j] & 31)) & 1u)) hit = set_contains(t.spill, key);
+            hitm |= (hit ? 1u : 0u) << j;
+        }
+    }
+    ull rec = rec0;
+    uint32_t cur = 0;
+#pragma unroll
+    for (int j = 0; j < kQSeg; ++j) {
+        if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
+            flush_hits(hits, nrec, rec, cur);
+            cur = 0;
+            ++rec;
+        }
+        cur += (hitm >> j) & 1u;
     }
     flush_hits(hits, nrec, rec, cur);
 }
@@ -605,13 +619,18 @@ struct okm_kset {
     std::vector<uint8_t> host_batch;
     // minimizer-bucketed copy of the keys (query): built at the first query
     // after an insert; mini_ok false when a bucket is too big for the scan
-    Scratch mini_keys, mini_dir;
+    Scratch mini_rows, mini_aux;  // rows; bucket counts + overflow bits + spill set + ctl
     uint32_t mini_nb = 0;
+    ull *mini_spill = nullptr;
+    uint64_t mini_spill_cap = 0;
+    uint32_t *mini_ovf = nullptr;
     bool mini_built = false, mini_ok = false;
 
     SetTab tab() const { return SetTab{slots, cap - 1, 64u - log2_exact(cap)}; }
     MiniTab mini() const {
-        return MiniTab{(const ull *)mini_keys.p, (const ull *)mini_dir.p, mini_nb, k < kMiniM ? (uint32_t)k : kMiniM};
+        return MiniTab{(const ull *)mini_rows.p, mini_ovf,
+                       SetTab{mini_spill, mini_spill_cap - 1, 64u - log2_exact(mini_spill_cap)}, mini_nb,
+                       k < kMiniM ? (uint32_t)k : kMiniM};
     }
 };
 
@@ -682,13 +701,13 @@ void launch_query_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pr
                        (uint32_t)s->k, d_hits, nrec);
 }
 
-// OKM_QUERY_MINI=0: the hash-set probe kernel instead of the bucketed copy.
+// OKM_QUERY_MINI=1: the bucketed copy instead of the hash-set probe kernel.
 bool query_mini_wanted() {
     const char *e = getenv("OKM_QUERY_MINI");
-    return !(e && *e == '0');
+    return e && *e == '1';
 }
 
-// The minimizer-bucketed copy of the set (k_mini_count / scan / k_mini_place).
+// The minimizer-bucketed copy of the set (k_mini_fill).
 okm_status mini_build(okm_kset *s) {
     s->mini_built = true;
     s->mini_ok = false;
@@ -697,31 +716,34 @@ okm_status mini_build(okm_kset *s) {
     const uint64_t nb64 = std::max<uint64_t>(1, (s->size + kMiniPerBucket - 1) / kMiniPerBucket);
     if (nb64 >= 0xFFFFFFFFull) return OKM_OK;
     const uint32_t nb = (uint32_t)nb64;
-    const size_t tmp = scan_tmp_elems((uint64_t)nb + 1);
-    PTRY(s->mini_dir.ensure(((size_t)nb + 1 + (size_t)nb + 1 + tmp + 1) * sizeof(ull)));
-    PTRY(s->mini_keys.ensure((size_t)s->size * sizeof(ull)));
-    ull *cnt = (ull *)s->mini_dir.p + (nb + 1), *scr = cnt + (nb + 1), *maxb = scr + tmp;
-    ull *dir = (ull *)s->mini_dir.p;
-    PHIP(hipMemsetAsync(cnt, 0, ((size_t)nb + 1) * sizeof(ull), s->st));
-    PHIP(hipMemsetAsync(maxb, 0, sizeof(ull), s->st));
-    hipLaunchKernelGGL(k_mini_count, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
-                       s->cap, (uint32_t)s->k, m, nb, cnt, maxb);
-    PHIP(hipGetLastError());
-    launch_exclusive_scan(s->st, cnt, dir, (uint64_t)nb + 1, scr);
-    PHIP(hipMemcpyAsync(cnt, dir, ((size_t)nb + 1) * sizeof(ull), hipMemcpyDeviceToDevice, s->st));
-    hipLaunchKernelGGL(k_mini_place, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
-                       s->cap, (uint32_t)s->k, m, nb, cnt, (ull *)s->mini_keys.p);
+    const uint64_t spill_cap = pow2_at_least(2 * (s->size / 8 + 1024));  // room for 1/8 of the keys at load 1/2
+    const size_t cnt_b = (size_t)nb * 4, ovf_b = ((size_t)nb + 31) / 32 * 4;
+    const size_t spill_off = (cnt_b + ovf_b + 255) & ~(size_t)255;
+    PTRY(s->mini_rows.ensure((size_t)nb * kMiniRow * sizeof(ull)));
+    PTRY(s->mini_aux.ensure(spill_off + (spill_cap + 1) * sizeof(ull) + 2 * sizeof(ull)));
+    uint8_t *aux = (uint8_t *)s->mini_aux.p;
+    uint32_t *cnt = (uint32_t *)aux;
+    s->mini_ovf = (uint32_t *)(aux + cnt_b);
+    s->mini_spill = (ull *)(aux + spill_off);
+    s->mini_spill_cap = spill_cap;
+    ull *ctl = s->mini_spill + spill_cap + 1;
+    PHIP(hipMemsetAsync(s->mini_rows.p, 0xFF, (size_t)nb * kMiniRow * sizeof(ull), s->st));
+    PHIP(hipMemsetAsync(cnt, 0, cnt_b + ovf_b, s->st));
+    PHIP(hipMemsetAsync(s->mini_spill, 0xFF, spill_cap * sizeof(ull), s->st));
+    PHIP(hipMemsetAsync(s->mini_spill + spill_cap, 0, 3 * sizeof(ull), s->st));  // flag word + ctl
+    s->mini_nb = nb;
+    hipLaunchKernelGGL(k_mini_fill, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots, s->cap,
+                       (uint32_t)s->k, m, nb, (ull *)s->mini_rows.p, cnt, s->mini_ovf, s->mini().spill, ctl);
     PHIP(hipGetLastError());
     ull h[2] = {0, 0};
-    PHIP(hipMemcpyAsync(&h[0], maxb, sizeof(ull), hipMemcpyDeviceToHost, s->st));
-    PHIP(hipMemcpyAsync(&h[1], dir + nb, sizeof(ull), hipMemcpyDeviceToHost, s->st));
+    PHIP(hipMemcpyAsync(h, ctl, 2 * sizeof(ull), hipMemcpyDeviceToHost, s->st));
     PHIP(hipStreamSynchronize(s->st));
-    s->mini_nb = nb;
     // every key placed (the ~0 key of a database lives in the hash set's flag
-    // word only, and never equals a window's canonical key)
-    const char *mb = getenv("OKM_QUERY_MINI_MAXB");  // tests: force the hash-set fallback
-    const uint64_t maxb_ok = mb && atoll(mb) > 0 ? (uint64_t)atoll(mb) : kMiniMaxBucket;
-    s->mini_ok = h[0] <= maxb_ok && h[1] <= s->size;
+    // word only, and never equals a window's canonical key); OKM_QUERY_MINI_MAXB
+    // (tests): treat more spilled keys than that as a failed build
+    const char *mb = getenv("OKM_QUERY_MINI_MAXB");
+    const bool forced = mb && atoll(mb) > 0 && h[0] > (uint64_t)atoll(mb);
+    s->mini_ok = h[1] == 0 && !forced;
     return OKM_OK;
 }
 
@@ -805,8 +827,8 @@ void okm_kset_destroy(okm_kset *s) {
     s->batch.release();
     s->tiles.release();
     s->hits.release();
-    s->mini_keys.release();
-    s->mini_dir.release();
+    s->mini_rows.release();
+    s->mini_aux.release();
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }
