@@ -206,6 +206,29 @@ static bool bgzf_members(const uint8_t *in, size_t n, std::vector<size_t> &mb, s
     return mb.size() > 1;
 }
 
+// A member inflated on the host threads (okm_inflate.cpp): true when that
+// path took it (pos advanced past it, or st set under OKM_GZ_PARALLEL=2, which
+// makes a rejected member an error instead of a serial retry: tests).
+static bool member_parallel(const uint8_t *in, size_t n, size_t &pos, Bytes &out, okm_status &st) {
+    const size_t base = out.size();
+    size_t used = 0;
+    bool applied = false;
+    const okm_status s = gunzip_member_parallel(in + pos, n - pos, out, &used, &applied);
+    if (!applied) return false;
+    if (s == OKM_OK) {
+        pos += used;
+        st = OKM_OK;
+        return true;
+    }
+    out.resize(base);
+    const char *e = getenv("OKM_GZ_PARALLEL");
+    if (e && *e == '2') {
+        st = s;
+        return true;
+    }
+    return false;
+}
+
 static okm_status gunzip_libdeflate(Deflate *D, const uint8_t *in, size_t n, Bytes &out) {
     std::vector<size_t> mb, ob;
     if (bgzf_members(in, n, mb, ob)) {  // members are independent: inflate them in parallel
@@ -233,6 +256,13 @@ static okm_status gunzip_libdeflate(Deflate *D, const uint8_t *in, size_t n, Byt
     size_t pos = 0;
     okm_status st = OKM_OK;
     while (pos < n) {
+        if (member_parallel(in, n, pos, out, st)) {
+            if (st != OKM_OK) break;
+            size_t p = pos;  // trailing zero padding after the last member is tolerated
+            while (p < n && in[p] == 0) ++p;
+            if (p == n) break;
+            continue;
+        }
         // a single-member file's ISIZE (mod 2^32) sizes the output exactly
         size_t cap = std::max<size_t>(n - pos, 1 << 16) * 4;
         const uint8_t *t = in + n - 4;
@@ -271,6 +301,14 @@ static okm_status gunzip(const uint8_t *in, size_t n, Bytes &out) {
     size_t pos = 0;
     Bytes buf(1 << 20);
     while (pos < n) {
+        okm_status pst = OKM_OK;
+        if (member_parallel(in, n, pos, out, pst)) {
+            if (pst != OKM_OK) return pst;
+            size_t p = pos;  // trailing zero padding after the last member is tolerated
+            while (p < n && in[p] == 0) ++p;
+            if (p == n) break;
+            continue;
+        }
         z_stream z;
         memset(&z, 0, sizeof(z));
         if (inflateInit2(&z, 15 + 16) != Z_OK) return fail(OKM_E_IO, "zlib init failed");

@@ -51,6 +51,13 @@ template <typename F> void parallel_for(size_t n, F &&f) {
     for (auto &th : ts) th.join();
 }
 
+// One gzip member (header at in[0]) inflated on the host threads
+// (okm_inflate.cpp), appended to out; *used = the member's bytes.  *applied is
+// false (and nothing done) when the member is too small to split or parallel
+// inflate is off (OKM_GZ_PARALLEL=0); an error leaves out's new tail
+// unspecified (the caller decodes the member serially instead).
+okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_t *used, bool *applied);
+
 std::string lower_extension(const std::string &path);
 okm_status read_whole_file(const std::string &path, Bytes &data);
 // utils.rs:125-152: .gz/.xz/.zst/.zstd by lower-cased last extension.

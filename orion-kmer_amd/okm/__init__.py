@@ -208,6 +208,20 @@ def read_fastx_file(path: str, decompress_by_extension: bool = True) -> List[byt
     return out
 
 
+def read_file(path: str, decompress_by_extension: bool = True) -> bytes:
+    """A whole file through the library's reader (okm_read_file: .gz / .xz /
+    .zst by extension, utils.rs:125-152; single-member gzip inflated on the
+    host threads, okm_inflate.cpp)."""
+    data = c_void_p()
+    n = c_uint64()
+    check(lib().okm_read_file(path.encode(), 1 if decompress_by_extension else 0, byref(data), byref(n)),
+          f"okm_read_file({path})")
+    try:
+        return ctypes.string_at(data, n.value) if n.value else b""
+    finally:
+        lib().okm_free_result(data)
+
+
 def write_counts_tsv(path: str, k: int, keys: np.ndarray, counts: np.ndarray) -> None:
     """keys: uint64 (k <= 32) or (n, 2) [lo, hi] (k in 33..64)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
