@@ -183,6 +183,15 @@ __device__ __forceinline__ void flush_hits(uint32_t *hits, uint64_t nrec, ull re
     if (cur && rec < nrec) atomicAdd(&hits[rec], cur);
 }
 
+// The compiler may not keep values derived from the codes alive across the
+// probe loads (it would: they are cheaper to keep than to recompute, and they
+// cost the occupancy): the codes are "changed" here, so they are recomputed.
+template <int NP>
+__device__ __forceinline__ void opaque_codes(Codes<NP> &c) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) asm volatile("" : "+v"(c.p[i]), "+v"(c.q[i]));
+}
+
 // Keys of the thread's SEG windows stay in registers and their home-slot
 // loads are all in flight together.  K > 0: k known at compile time; K = 0:
 // runtime k.
@@ -205,22 +214,16 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
     constexpr int NP = WinWords<kQSeg>::kLoad / 16;
     Codes<NP> c;
     make_codes<NP, true>(w, c);  // query.rs: raw bytes, U invalid
-    ull key[kQSeg];
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        bool valid;
-        key[j] = window_key(c, j, k, &valid);
-        vmask |= (valid ? 1u : 0u) << j;
-    }
-    // every valid window's home slot load in flight before any is consumed
+    const uint32_t vmask = ~invalid_windows<kQSeg, NP>(c, k) & 0xFFFFu;
+    // every valid window's home slot load in flight before any is consumed;
+    // only the loaded words stay live across the loads (keys and homes are
+    // recomputed from the codes afterwards), so 8 waves fit a SIMD and twice
+    // the probes are in flight per CU
     ull first[kQSeg];
-    uint64_t home[kQSeg];
 #pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        home[j] = home_slot(key[j], t.shift);
-        first[j] = (vmask >> j) & 1u ? t.slots[home[j]] : kEmpty;
-    }
+    for (int j = 0; j < kQSeg; ++j)
+        first[j] = (vmask >> j) & 1u ? t.slots[home_slot(window_key_nv(c, j, k), t.shift)] : kEmpty;
+    opaque_codes(c);
     ull rec = rec0;
     uint32_t cur = 0;
 #pragma unroll
@@ -230,10 +233,9 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
             cur = 0;
             ++rec;
         }
-        if ((vmask >> j) & 1u) {
-            const bool hit = first[j] == key[j] ? true
-                             : first[j] == kEmpty ? false
-                                                  : set_probe_rest(t, key[j], home[j]);
+        if (first[j] != kEmpty) {  // a valid window whose home slot holds a key
+            const ull key = window_key_nv(c, j, k);
+            const bool hit = first[j] == key || set_probe_rest(t, key, home_slot(key, t.shift));
             cur += hit ? 1u : 0u;
         }
     }
@@ -243,29 +245,35 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
 // ---------------------------------------------------------------------------
 // query over a minimizer-bucketed copy of the set
 //
-// The hash set costs one random 128-B line per probed window (one HBM line
-// per window at C2 scale: 0.79 of the random-probe ceiling).
+// The hash set costs one random 128-B line per probed window, and at C2 scale
+// every one is an HBM miss (0.79 of the random-probe ceiling).
 // Here the set's keys are grouped by the MINIMIZER of each k-mer: the m-mer
 // (m = min(k, 15)) whose canonical value has the smallest hash among the
 // k - m + 1 m-mers of the k-mer.  The canonical m-mers of a k-mer and of its
 // reverse complement are the same set, so a window and the canonical key
 // agree on the minimizer whatever strand the read came from.  Consecutive
-// windows of a read share their minimizer for ~(k - m + 2) / 2 windows on
-// average, so the ~120 windows of a 150-bp read touch ~17 buckets (a
-// directory word pair and a short key run each) instead of ~120 random
-// slots.  The hits are exactly the hash set's (query.rs:86-93: membership of
-// the canonical key); only where the key is looked up changes.
+// k-mers share their minimizer for ~(k - m + 2) / 2 windows on average.
+// Each bucket (a hash of the minimizer) is a small open-addressing table of
+// kMiniSlots keys (four 128-B lines): a window probes ONE slot of its bucket,
+// and the windows of a read that share the bucket probe the same four lines,
+// so a 150-bp read misses on ~15 buckets' lines instead of ~120 random slots.
+// A bucket given more than kMiniSlots / 2 keys is marked overflowed (every
+// slot kMiniOvf, a value no canonical key takes) and its windows probe the
+// hash set instead.  The hits are exactly the hash set's (query.rs:86-93:
+// membership of the canonical key); only where the key is looked up changes.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kMiniM = 15;     // m-mer length (m = min(k, 15))
-constexpr uint32_t kMiniRow = 4;    // keys a bucket row holds (32 B)
-constexpr uint32_t kMiniPerBucket = 2;  // buckets = keys / 2: rows overflow for ~1 % of the keys
+constexpr uint32_t kMiniM = 15;        // m-mer length (m = min(k, 15))
+constexpr uint32_t kMiniSlots = 64;    // slots per bucket (512 B)
+constexpr uint32_t kMiniKeysPerBucket = 4;  // buckets = keys / 4; ~8 % of the keys sit in overflowed buckets
+// ~1: TTT...TG for k = 32 (its reverse complement CAA...A is smaller), and
+// more than 2k bits for k < 32 -- never a canonical key
+constexpr ull kMiniOvf = ~1ull;
 
 struct MiniTab {
-    const ull *rows;      // nb rows of kMiniRow keys (~0: empty slot)
-    const uint32_t *ovf;  // bit b: bucket b had more keys than its row holds
-    SetTab spill;         // ... those keys
-    uint32_t nb;          // buckets
-    uint32_t m;           // m-mer length
+    const ull *tab;  // nb buckets of kMiniSlots keys (kEmpty: free, kMiniOvf: bucket overflowed)
+    SetTab set;      // the hash set (overflowed buckets)
+    uint32_t nb;     // buckets
+    uint32_t m;      // m-mer length
 };
 
 __host__ __device__ __forceinline__ uint32_t mini_hash(uint32_t canon_m) {  // murmur3 fmix32, seeded
@@ -277,13 +285,25 @@ __host__ __device__ __forceinline__ uint32_t mini_hash(uint32_t canon_m) {  // m
     h ^= h >> 16;
     return h;
 }
+// The minimum of k - m + 1 hashes is skewed towards 0: mixed again before it
+// picks a bucket, or the low buckets would take every key.
 __host__ __device__ __forceinline__ uint32_t mini_bucket(uint32_t h, uint32_t nb) {
+    h ^= 0x7F4A7C15u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
     return (uint32_t)(((uint64_t)h * nb) >> 32);
 }
 __host__ __device__ __forceinline__ uint32_t canon_mmer(uint32_t fwd, uint32_t m) {
     const uint32_t mask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
     const uint32_t rc = ~rev2(fwd << (32 - 2 * m)) & mask;  // reverse complement of the m bases
     return fwd < rc ? fwd : rc;
+}
+// A key's home slot inside its bucket.
+__device__ __forceinline__ uint32_t mini_slot(ull key) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 58);  // top 6 bits (kMiniSlots = 64)
 }
 // Bucket of a canonical k-mer key (2k bits, MSB-first).
 __host__ __device__ __forceinline__ uint32_t key_bucket(uint64_t key, uint32_t k, uint32_t m, uint32_t nb) {
@@ -297,42 +317,65 @@ __host__ __device__ __forceinline__ uint32_t key_bucket(uint64_t key, uint32_t k
     return mini_bucket(best, nb);
 }
 
-// Every key of the hash set into its bucket's row; a row's fifth and later
-// keys go to the spill set (ctl[0]: spill inserts, ctl[1]: 1 when the spill
-// set would pass half load -- the index is then not used).
+// Build pass 1: keys per bucket.
+__global__ __launch_bounds__(kProbeBlock) void k_mini_count(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
+                                                            uint32_t m, uint32_t nb, uint32_t *__restrict__ cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
+        const ull x = slots[i];
+        if (x != kEmpty) atomicAdd(&cnt[key_bucket(x, k, m, nb)], 1u);
+    }
+}
+// Build pass 2: every bucket's slots: kMiniOvf when it has too many keys, else empty.
+__global__ __launch_bounds__(kProbeBlock) void k_mini_clear(const uint32_t *__restrict__ cnt, uint32_t nb,
+                                                            ull *__restrict__ tab) {
+    const uint64_t n = (uint64_t)nb * kMiniSlots;
+    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < n; i += stride)
+        tab[i] = cnt[i / kMiniSlots] > kMiniSlots / 2 ? kMiniOvf : kEmpty;
+}
+// Build pass 3: every key of a bucket that did not overflow into its table.
 __global__ __launch_bounds__(kProbeBlock) void k_mini_fill(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
-                                                           uint32_t m, uint32_t nb, ull *__restrict__ rows,
-                                                           uint32_t *__restrict__ cnt, uint32_t *__restrict__ ovf,
-                                                           SetTab spill, ull *__restrict__ ctl) {
+                                                           uint32_t m, uint32_t nb, const uint32_t *__restrict__ cnt,
+                                                           ull *__restrict__ tab) {
     const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
         const ull x = slots[i];
         if (x == kEmpty) continue;
         const uint32_t b = key_bucket(x, k, m, nb);
-        const uint32_t r = atomicAdd(&cnt[b], 1u);
-        if (r < kMiniRow) {
-            rows[(uint64_t)b * kMiniRow + r] = x;
-            continue;
-        }
-        atomicOr(&ovf[b >> 5], 1u << (b & 31));
-        if (atomicAdd(&ctl[0], 1ull) < (spill.mask + 1) / 2)
-            set_insert(spill, x);
-        else
-            atomicOr(&ctl[1], 1ull);
+        if (cnt[b] > kMiniSlots / 2) continue;
+        ull *bt = tab + (uint64_t)b * kMiniSlots;
+        for (uint32_t s = mini_slot(x);; s = (s + 1) & (kMiniSlots - 1))
+            if (atomicCAS(&bt[s], kEmpty, x) == kEmpty) break;  // distinct keys, load <= 1/2: a slot is free
     }
 }
 
-// k_query_hits over the bucketed set: the thread's 16 windows, their
-// validity as in k_query_hits, the 16 + k - m canonical m-mer hashes they
-// span and each window's minimizer bucket; then, OKM_QUERY_MINI_GROUP windows at a time, every
-// valid window's 32-B bucket row is loaded (rows of consecutive windows are
-// mostly the same: cache hits) and compared with its canonical key; a key
-// missing from a full row whose bucket overflowed is looked up in the spill set.
-#ifndef OKM_QUERY_MINI_GROUP  // windows whose rows are loaded together
-#define OKM_QUERY_MINI_GROUP 4
+// Continue a bucket probe whose home slot held neither the key nor a free slot.
+__device__ __noinline__ bool mini_probe_rest(const ull *__restrict__ bt, ull key, uint32_t s) {
+    for (uint32_t i = 1; i < kMiniSlots; ++i) {
+        const ull v = bt[(s + i) & (kMiniSlots - 1)];
+        if (v == key) return true;
+        if (v == kEmpty) return false;
+    }
+    return false;
+}
+
+// k_query_hits over the bucketed set: the thread's 16 windows, their validity
+// as in k_query_hits, the 16 + k - m canonical m-mer hashes they span and each
+// window's minimizer bucket; then every valid window's home slot in its bucket
+// is loaded together (windows of one bucket hit the same two lines), a collision
+// continues inside the bucket, and an overflowed bucket sends the window to
+// the hash set.
+#ifndef OKM_QUERY_MINI_WAVES  // experiment builds: a waves-per-SIMD target for k_query_hits_mini
+#define OKM_QUERY_MINI_WAVES 0
+#endif
+#if OKM_QUERY_MINI_WAVES
+#define OKM_MINI_ATTR __attribute__((amdgpu_waves_per_eu(OKM_QUERY_MINI_WAVES)))
+#else
+#define OKM_MINI_ATTR
 #endif
 template <int K>
-__global__ __launch_bounds__(kProbeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
+__global__ __launch_bounds__(kProbeBlock) OKM_MINI_ATTR void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
                                                                  const ull *__restrict__ tile_pre, MiniTab t,
                                                                  uint32_t k_rt, uint32_t *__restrict__ hits,
                                                                  uint64_t nrec) {
@@ -356,53 +399,74 @@ __global__ __launch_bounds__(kProbeBlock) __attribute__((amdgpu_waves_per_eu(4))
     // minimizer bucket of every window
     const uint32_t span = k - m;  // a window's m-mers: j .. j + span
     const uint32_t mmask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
-    uint32_t bk[kQSeg];
-    {
-        uint32_t h[kQSeg + 17];  // span <= 32 - 15
+    auto mmer_hash = [&](int i) {  // hash of the canonical m-mer at base i
+        const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
+        const uint32_t r = rc32(c, 2 * i) & mmask;
+        return mini_hash(f < r ? f : r);
+    };
+    ull first[kQSeg];
+    if constexpr (K >= 30) {
+        // window j's minimizer is the least of m-mers j .. j + SP (SP >= 15):
+        // suffix minima S of m-mers 0 .. SP and a running minimum P of
+        // SP + 1 .. SP + j, so each window's bucket -- and its slot load -- is
+        // ready in order while only S stays live (the loads of the first
+        // windows are in flight while the later buckets are computed)
+        constexpr int SP = K - (int)kMiniM;
+        uint32_t S[SP + 1];
 #pragma unroll
-        for (int i = 0; i < kQSeg + 17; ++i) {
-            if ((uint32_t)i > kQSeg - 1 + span) break;
-            const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
-            const uint32_t r = rc32(c, 2 * i) & mmask;
-            h[i] = mini_hash(f < r ? f : r);
-        }
+        for (int i = 0; i <= SP; ++i) S[i] = mmer_hash(i);
+#pragma unroll
+        for (int i = SP - 1; i >= 0; --i) S[i] = min(S[i], S[i + 1]);
+        uint32_t P = ~0u;
 #pragma unroll
         for (int j = 0; j < kQSeg; ++j) {
-            uint32_t mn = h[j];
-            if (K) {
-#pragma unroll
-                for (uint32_t d = 1; d <= (K > (int)kMiniM ? (uint32_t)K - kMiniM : 0u); ++d) mn = min(mn, h[j + d]);
-            } else {
-                for (uint32_t d = 1; d <= span; ++d) mn = min(mn, h[j + d]);
-            }
-            bk[j] = mini_bucket(mn, t.nb);
+            if (j > 0) P = min(P, mmer_hash(SP + j));
+            const uint32_t b = mini_bucket(min(S[j], P), t.nb);
+            first[j] = (vmask >> j) & 1u ? t.tab[(uint64_t)b * kMiniSlots + mini_slot(window_key_nv(c, j, k))] : kEmpty;
         }
+    } else {
+        uint32_t bk[kQSeg];
+        {
+            uint32_t h[kQSeg + 17];  // span <= 32 - 15
+#pragma unroll
+            for (int i = 0; i < kQSeg + 17; ++i) {
+                if ((uint32_t)i > kQSeg - 1 + span) break;
+                h[i] = mmer_hash(i);
+            }
+#pragma unroll
+            for (int j = 0; j < kQSeg; ++j) {
+                uint32_t mn = h[j];
+                if (K) {
+#pragma unroll
+                    for (uint32_t d = 1; d <= (K > (int)kMiniM ? (uint32_t)K - kMiniM : 0u); ++d) mn = min(mn, h[j + d]);
+                } else {
+                    for (uint32_t d = 1; d <= span; ++d) mn = min(mn, h[j + d]);
+                }
+                bk[j] = mini_bucket(mn, t.nb);
+            }
+        }
+        // every valid window's home slot load in flight together (only the
+        // loaded words stay live: keys are recomputed, buckets too on the rare
+        // collision)
+#pragma unroll
+        for (int j = 0; j < kQSeg; ++j)
+            first[j] = (vmask >> j) & 1u ? t.tab[(uint64_t)bk[j] * kMiniSlots + mini_slot(window_key_nv(c, j, k))]
+                                         : kEmpty;
     }
+    opaque_codes(c);
     uint32_t hitm = 0;  // bit j: window j's key is in the set
-    constexpr int G = OKM_QUERY_MINI_GROUP;
 #pragma unroll
-    for (int half = 0; half < kQSeg / G; ++half) {
-        ulonglong2 r0[G], r1[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) {  // every row load of the group's windows in flight together
-            const int j = G * half + u;
-            if ((vmask >> j) & 1u) {
-                const ulonglong2 *row = reinterpret_cast<const ulonglong2 *>(t.rows + (uint64_t)bk[j] * kMiniRow);
-                r0[u] = row[0];
-                r1[u] = row[1];
-            } else {
-                r0[u] = r1[u] = make_ulonglong2(kEmpty, kEmpty);
-            }
+    for (int j = 0; j < kQSeg; ++j) {
+        if (first[j] == kEmpty) continue;  // invalid window, or a free home slot
+        const ull key = window_key_nv(c, j, k);
+        bool hit = first[j] == key;
+        if (!hit) {
+            if (first[j] == kMiniOvf)
+                hit = set_contains(t.set, key);
+            else
+                hit = mini_probe_rest(t.tab + (uint64_t)key_bucket(key, k, m, t.nb) * kMiniSlots, key, mini_slot(key));
         }
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-            const int j = G * half + u;
-            if (!((vmask >> j) & 1u)) continue;
-            const ull key = window_key_nv(c, j, k);
-            bool hit = r0[u].x == key || r0[u].y == key || r1[u].x == key || r1[u].y == key;
-            if (!hit && r1[u].y != kEmpty && ((t.ovf[bk[j] >> 5] >> (bk[j] & 31)) & 1u)) hit = set_contains(t.spill, key);
-            hitm |= (hit ? 1u : 0u) << j;
-        }
+        hitm |= (hit ? 1u : 0u) << j;
     }
     ull rec = rec0;
     uint32_t cur = 0;
@@ -618,19 +682,14 @@ struct okm_kset {
     Scratch keys, batch, tiles, hits;
     std::vector<uint8_t> host_batch;
     // minimizer-bucketed copy of the keys (query): built at the first query
-    // after an insert; mini_ok false when a bucket is too big for the scan
-    Scratch mini_rows, mini_aux;  // rows; bucket counts + overflow bits + spill set + ctl
+    // after an insert; mini_ok false when there is none (no keys, >= 2^32 keys)
+    Scratch mini_tab, mini_cnt;  // the bucket tables; keys per bucket (build)
     uint32_t mini_nb = 0;
-    ull *mini_spill = nullptr;
-    uint64_t mini_spill_cap = 0;
-    uint32_t *mini_ovf = nullptr;
     bool mini_built = false, mini_ok = false;
 
     SetTab tab() const { return SetTab{slots, cap - 1, 64u - log2_exact(cap)}; }
     MiniTab mini() const {
-        return MiniTab{(const ull *)mini_rows.p, mini_ovf,
-                       SetTab{mini_spill, mini_spill_cap - 1, 64u - log2_exact(mini_spill_cap)}, mini_nb,
-                       k < kMiniM ? (uint32_t)k : kMiniM};
+        return MiniTab{(const ull *)mini_tab.p, tab(), mini_nb, k < kMiniM ? (uint32_t)k : kMiniM};
     }
 };
 
@@ -701,49 +760,43 @@ void launch_query_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pr
                        (uint32_t)s->k, d_hits, nrec);
 }
 
-// OKM_QUERY_MINI=1: the bucketed copy instead of the hash-set probe kernel.
-bool query_mini_wanted() {
+// OKM_QUERY_MINI: 0 (default) the hash-set probe kernel, 1 the bucketed copy,
+// 2 the bucketed copy or an error (tests: the index path must be the one run).
+// The bucketed copy halves the HBM lines a C2 query fetches but runs no faster
+// (9.46 vs 8.91 ms: at 91 VGPRs, 5 waves per SIMD, it is bound by the probes
+// in flight, where the hash kernel at 64 VGPRs is bound by HBM lines).
+int query_mini_mode() {
     const char *e = getenv("OKM_QUERY_MINI");
-    return e && *e == '1';
+    return e && *e ? atoi(e) : 0;
 }
 
-// The minimizer-bucketed copy of the set (k_mini_fill).
+// The minimizer-bucketed copy of the set: keys per bucket, the buckets'
+// tables cleared (or marked overflowed), every key inserted into its bucket.
+// OKM_QUERY_MINI_KPB (tests): keys per bucket on average (more: overflows).
 okm_status mini_build(okm_kset *s) {
     s->mini_built = true;
     s->mini_ok = false;
     if (s->size == 0) return OKM_OK;
+    const char *e = getenv("OKM_QUERY_MINI_KPB");
+    const uint64_t kpb = e && atoi(e) > 0 ? (uint64_t)atoi(e) : kMiniKeysPerBucket;
     const uint32_t m = s->k < kMiniM ? s->k : kMiniM;
-    const uint64_t nb64 = std::max<uint64_t>(1, (s->size + kMiniPerBucket - 1) / kMiniPerBucket);
+    const uint64_t nb64 = std::max<uint64_t>(1, (s->size + kpb - 1) / kpb);
     if (nb64 >= 0xFFFFFFFFull) return OKM_OK;
     const uint32_t nb = (uint32_t)nb64;
-    const uint64_t spill_cap = pow2_at_least(2 * (s->size / 8 + 1024));  // room for 1/8 of the keys at load 1/2
-    const size_t cnt_b = (size_t)nb * 4, ovf_b = ((size_t)nb + 31) / 32 * 4;
-    const size_t spill_off = (cnt_b + ovf_b + 255) & ~(size_t)255;
-    PTRY(s->mini_rows.ensure((size_t)nb * kMiniRow * sizeof(ull)));
-    PTRY(s->mini_aux.ensure(spill_off + (spill_cap + 1) * sizeof(ull) + 2 * sizeof(ull)));
-    uint8_t *aux = (uint8_t *)s->mini_aux.p;
-    uint32_t *cnt = (uint32_t *)aux;
-    s->mini_ovf = (uint32_t *)(aux + cnt_b);
-    s->mini_spill = (ull *)(aux + spill_off);
-    s->mini_spill_cap = spill_cap;
-    ull *ctl = s->mini_spill + spill_cap + 1;
-    PHIP(hipMemsetAsync(s->mini_rows.p, 0xFF, (size_t)nb * kMiniRow * sizeof(ull), s->st));
-    PHIP(hipMemsetAsync(cnt, 0, cnt_b + ovf_b, s->st));
-    PHIP(hipMemsetAsync(s->mini_spill, 0xFF, spill_cap * sizeof(ull), s->st));
-    PHIP(hipMemsetAsync(s->mini_spill + spill_cap, 0, 3 * sizeof(ull), s->st));  // flag word + ctl
-    s->mini_nb = nb;
-    hipLaunchKernelGGL(k_mini_fill, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots, s->cap,
-                       (uint32_t)s->k, m, nb, (ull *)s->mini_rows.p, cnt, s->mini_ovf, s->mini().spill, ctl);
+    PTRY(s->mini_tab.ensure((size_t)nb * kMiniSlots * sizeof(ull)));
+    PTRY(s->mini_cnt.ensure((size_t)nb * sizeof(uint32_t)));
+    uint32_t *cnt = (uint32_t *)s->mini_cnt.p;
+    ull *tab = (ull *)s->mini_tab.p;
+    PHIP(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(uint32_t), s->st));
+    hipLaunchKernelGGL(k_mini_count, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
+                       s->cap, (uint32_t)s->k, m, nb, cnt);
+    hipLaunchKernelGGL(k_mini_clear, dim3(grid_for((uint64_t)nb * kMiniSlots)), dim3(kProbeBlock), 0, s->st,
+                       (const uint32_t *)cnt, nb, tab);
+    hipLaunchKernelGGL(k_mini_fill, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
+                       s->cap, (uint32_t)s->k, m, nb, (const uint32_t *)cnt, tab);
     PHIP(hipGetLastError());
-    ull h[2] = {0, 0};
-    PHIP(hipMemcpyAsync(h, ctl, 2 * sizeof(ull), hipMemcpyDeviceToHost, s->st));
-    PHIP(hipStreamSynchronize(s->st));
-    // every key placed (the ~0 key of a database lives in the hash set's flag
-    // word only, and never equals a window's canonical key); OKM_QUERY_MINI_MAXB
-    // (tests): treat more spilled keys than that as a failed build
-    const char *mb = getenv("OKM_QUERY_MINI_MAXB");
-    const bool forced = mb && atoll(mb) > 0 && h[0] > (uint64_t)atoll(mb);
-    s->mini_ok = h[1] == 0 && !forced;
+    s->mini_nb = nb;
+    s->mini_ok = true;
     return OKM_OK;
 }
 
@@ -764,8 +817,10 @@ okm_status query_device(okm_kset *s, const uint8_t *d_seq, uint64_t n, uint64_t 
     ull *cnt = (ull *)s->tiles.p, *pre = cnt + ntiles, *scr = pre + ntiles;
     hipLaunchKernelGGL(k_sep_count, dim3((uint32_t)ntiles), dim3(kProbeBlock), 0, s->st, d_seq, n, cnt);
     launch_exclusive_scan(s->st, cnt, pre, ntiles, scr);
-    if (query_mini_wanted() && !s->mini_built) PTRY(mini_build(s));
-    if (query_mini_wanted() && s->mini_ok) {
+    const int mode = query_mini_mode();
+    if (mode && !s->mini_built) PTRY(mini_build(s));
+    if (mode == 2 && !s->mini_ok) return fail(OKM_E_STATE, "okm_query_hits: no minimizer index (OKM_QUERY_MINI=2)");
+    if (mode && s->mini_ok) {
         switch (s->k) {
         case 21: launch_query_mini_k<21>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
         case 25: launch_query_mini_k<25>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
@@ -827,8 +882,8 @@ void okm_kset_destroy(okm_kset *s) {
     s->batch.release();
     s->tiles.release();
     s->hits.release();
-    s->mini_rows.release();
-    s->mini_aux.release();
+    s->mini_tab.release();
+    s->mini_cnt.release();
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }

@@ -148,7 +148,7 @@ def _reads(rng, genome, n, lo, hi, noise=0.01, lower=0.0):
     return out
 
 
-@pytest.mark.parametrize("mini", ["1", "0"], ids=["minimizer-index", "hash-set"])
+@pytest.mark.parametrize("mini", ["2", "0"], ids=["minimizer-index", "hash-set"])
 @pytest.mark.parametrize("k", [31, 21, 32, 17, 5, 15, 16, 27])
 def test_query_hits_vs_oracle(k, mini, monkeypatch):
     monkeypatch.setenv("OKM_QUERY_MINI", mini)
@@ -176,10 +176,12 @@ def _revcomp(b: bytes) -> bytes:
 
 @pytest.mark.parametrize("k", [31, 25, 12])
 def test_query_minimizer_index_strands_and_fallback(k, monkeypatch):
-    """The minimizer-bucketed set (okm_probe.hip k_query_hits_mini) finds a
-    canonical key from either strand of a read; an index whose biggest bucket
-    is past the scan limit (forced here with OKM_QUERY_MINI_MAXB) falls back to
-    the hash-set probe; every path equals the restatement."""
+    """The minimizer-bucketed set (okm_probe.hip k_query_hits_mini; OKM_QUERY_MINI=2
+    fails instead of falling back, so the index is what ran) finds a canonical
+    key from either strand of a read; windows whose bucket overflowed (forced
+    here with OKM_QUERY_MINI_KPB, keys per bucket: 32 = many buckets past their
+    32-key limit, 256 = all) probe the hash set instead; every path equals the
+    restatement."""
     rng = np.random.default_rng(k)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=150_000)
     g = genome.tobytes()
@@ -189,15 +191,15 @@ def test_query_minimizer_index_strands_and_fallback(k, monkeypatch):
     oc.add_records([g[:90_000]])
     db_keys, _ = oc.result(1)
     exp = oracle.query_hits(reads, db_keys, k)
-    for mini, maxb in (("1", ""), ("1", "2"), ("0", "")):  # index; index forced back to the hash set; hash set
+    for mini, kpb in (("2", ""), ("2", "32"), ("2", "256"), ("0", "")):  # index; mixed; all via the hash set; hash set
         monkeypatch.setenv("OKM_QUERY_MINI", mini)
-        monkeypatch.setenv("OKM_QUERY_MINI_MAXB", maxb)
+        monkeypatch.setenv("OKM_QUERY_MINI_KPB", kpb)
         with okm.KmerSet(k, 0, len(db_keys)) as s:
             s.insert(db_keys)
             got = s.query_hits(reads)
             s.insert(db_keys[:10])  # an insert drops the index; the next query rebuilds it
             again = s.query_hits(reads)
-        assert np.array_equal(got, exp) and np.array_equal(again, exp), (mini, maxb)
+        assert np.array_equal(got, exp) and np.array_equal(again, exp), (mini, kpb)
     assert exp[1500:3000].sum() > 0 and exp[3000:4500].sum() > 0  # both strands hit
 
 

@@ -94,7 +94,7 @@ def wl_query(args):
     s = okm.KmerSet(k, 0, len(db_keys))
     s.insert(db_keys)
     windows = valid_windows(batch, k)
-    mini = os.environ.get("OKM_QUERY_MINI", "1") != "0"
+    mini = os.environ.get("OKM_QUERY_MINI", "0") != "0"
     t_first = time.perf_counter()  # the first query after the inserts builds the minimizer index
     s.query_hits_device(dbuf.address, len(batch), READS, hbuf.address)
     t_first = time.perf_counter() - t_first
@@ -119,7 +119,7 @@ def wl_query(args):
         "config": {"workload": "query: 3,355,443 x 150 bp reads vs the k-mer set of the first half of them",
                    "k": k, "db_unique_kmers": int(len(db_keys)), "valid_windows": windows,
                    "reads_with_hits": int((hits > 0).sum()), "hits": int(hits.sum(dtype=np.uint64)),
-                   "index": ("minimizer-bucketed copy of the set (m = 15, ~4 keys a bucket)" if mini
+                   "index": ("minimizer-bucketed copy of the set (m = 15, keys / 8 buckets of 32 slots; buckets past 16 keys probe the hash set)" if mini
                              else "hash set (one slot per probe)"),
                    "first_query_ms_incl_index_build": round(t_first * 1e3, 2)},
         "roofline": {"bound": "hbm", "kernel": ("k_query_hits_mini<31>" if mini else "k_query_hits<31>")
