@@ -553,6 +553,7 @@ struct okm_ctx {
     okm_mode mode = OKM_MODE_COUNT;
     hipStream_t stream = nullptr;
     uint32_t l1_bits = 0, nbins = 1, shift1 = 64;
+    bool l1_fold = false;  // extract with the folding geometry (extract_l1_bits): set by the first fold, kept by reset
     bool wide = false;   // k > 32: K128 keys (two u64 per key)
     uint32_t kw = 1;     // u64 words per key
 
@@ -838,6 +839,12 @@ static okm_status do_count(okm_ctx *c);
 static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, uint64_t n, double slack);
 static okm_status count_general(okm_ctx *c);
 
+static void set_l1_geometry(okm_ctx *c) {
+    c->l1_bits = std::min<uint32_t>(extract_l1_bits(c->wide, c->l1_fold), 2u * c->k);
+    c->nbins = 1u << c->l1_bits;
+    c->shift1 = 2u * c->k - c->l1_bits;
+}
+
 // L1 bin bounds of a sorted run by binary search (a sorted table is already
 // partitioned by key range: nothing moves).
 static okm_status sorted_run_bins(okm_ctx *c, Run &run) {
@@ -926,6 +933,15 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
     return OKM_OK;
 }
 
+// OKM_L1_FOLD=0: a folding context keeps the batch-by-batch geometry (A/B).
+static bool fold_geometry_wanted() {
+    static const bool on = [] {
+        const char *e = getenv("OKM_L1_FOLD");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 // Fold (memory bounded by distinct keys, not by input): the batches added
 // since the last fold are counted into a sorted (key, count) table that
 // replaces their L1 runs; every kFoldMergeRuns tables are merged into one
@@ -936,6 +952,22 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
 static okm_status fold(okm_ctx *c) {
     OKM_TRY(count_unsorted_to_table(c));
     c->folds += 1;
+    // A context that folds takes 10 L1 bits from here on (and after okm_reset):
+    // a fold counts ~3.6 G instances, whose 9-bit parts are too big for one
+    // 2048-child pass and go through the fan-out split; 10-bit parts do not
+    // (C3 on one GPU: 414 vs 461 ms; a batch-by-batch C2 count stays at 9 bits,
+    // its extraction writes longer runs: 5.23 vs 5.44 ms).  Only sorted runs
+    // (tables) are left here, and their bins come from a binary search.
+    if (!c->l1_fold && !c->wide && fold_geometry_wanted()) {
+        bool all_sorted = true;
+        for (auto &r : c->runs) all_sorted &= r.sorted;
+        if (all_sorted) {
+            c->l1_fold = true;
+            set_l1_geometry(c);
+            for (auto &r : c->runs)
+                if (r.n) OKM_TRY(sorted_run_bins(c, r));
+        }
+    }
     static const uint32_t merge_runs = [] {
         const char *e = getenv("OKM_FOLD_MERGE_RUNS");
         return e ? std::max(2, atoi(e)) : 4;
@@ -2414,7 +2446,6 @@ static hipError_t create_ctx_stream(int device, hipStream_t *st) {
 }
 
 okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint) {
-    (void)distinct_hint;
     if (!out) return fail(OKM_E_ARG, "okm_create: out is NULL");
     *out = nullptr;
     const bool wide_ok = (mode & OKM_MODE_WIDE) != 0;  // opt-in two-u64 extension (k <= 64)
@@ -2434,9 +2465,8 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->mode = mode;
     c->wide = k > 32;
     c->kw = c->wide ? 2 : 1;
-    c->l1_bits = std::min<uint32_t>(log2_floor(extract_max_bins(k > 32)), 2u * k);
-    c->nbins = 1u << c->l1_bits;
-    c->shift1 = 2u * k - c->l1_bits;
+    c->l1_fold = !c->wide && distinct_hint >= (1ull << 30);  // a table this big is built by folding
+    set_l1_geometry(c);
     {
         // fold threshold: OKM_FOLD_BYTES (tests), else 10 % of the device's memory
         // (the count of the folded runs needs ~4.5x their bytes of working set;
@@ -2449,8 +2479,9 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     }
     if (create_ctx_stream(device, &c->stream) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->l1cap, (2 * (size_t)c->nbins + 2) * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->curpad, (size_t)c->nbins * OKM_L1_CUR_STRIDE * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->l1cap, (2 * (size_t)extract_max_bins(c->wide) + 2) * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->curpad, (size_t)extract_max_bins(c->wide) * OKM_L1_CUR_STRIDE * sizeof(unsigned long long)) !=
+            hipSuccess ||
         hipHostMalloc(&c->hpin, kHpinBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->hres, kHresWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();

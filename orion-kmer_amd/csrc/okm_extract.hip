@@ -32,7 +32,7 @@ namespace okm {
 __device__ __forceinline__ uint32_t bin_of(uint64_t key, uint32_t shift) {
     return shift >= 64 ? 0u : (uint32_t)(key >> shift);
 }
-// K >= 21 (compile time): shift = 2K - l1_bits lies in [33, 55] (l1_bits <= 9),
+// K >= 21 (compile time): shift = 2K - l1_bits lies in [32, 55] (l1_bits <= 10),
 // so the bin is a 32-bit shift of the key's high word
 template <int K>
 __device__ __forceinline__ uint32_t bin_k(uint64_t key, uint32_t shift) {
@@ -73,8 +73,12 @@ static_assert(kHTile % kTile == 0, "scatter tile must divide the hist tile");
 #ifndef OKM_L1_BITS  // first-level key-range bins of the k <= 32 extraction (2^bits <= kScatBlock)
 #define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
 #endif
-constexpr int kMaxL1Bins = 1 << OKM_L1_BITS;  // k <= 32 kernels
-static_assert(2 * 21 - OKM_L1_BITS >= 32, "bin_k: the L1 shift of k >= 21 lies in the key's high word");
+#ifndef OKM_L1_BITS_FOLD  // ... for a context that folds (okm_engine.hip fold(): C3 414 vs 461 ms, C2 5.44 vs 5.23)
+#define OKM_L1_BITS_FOLD 10
+#endif
+constexpr int kMaxL1Bins = 1 << (OKM_L1_BITS_FOLD > OKM_L1_BITS ? OKM_L1_BITS_FOLD : OKM_L1_BITS);  // k <= 32 kernels
+static_assert(2 * 21 - (OKM_L1_BITS_FOLD > OKM_L1_BITS ? OKM_L1_BITS_FOLD : OKM_L1_BITS) >= 32,
+              "bin_k: the L1 shift of k >= 21 lies in the key's high word");
 #ifndef OKM_L1_BITS_W  // first-level bins of the k in 33..64 extraction (2^bits <= OKM_WIDE_SCAT_BLOCK)
 #define OKM_L1_BITS_W 9  // 8: k=63 1 Gbases 39.3 vs 34.8 ms (children past one fan-out job), C4 248 vs 237 ms
 #endif
@@ -84,6 +88,9 @@ static_assert(kMaxL1Bins <= kScatBlock, "one bin per scatter thread");
 constexpr uint32_t gcd_u32(uint32_t a, uint32_t b) { return b ? gcd_u32(b, a % b) : a; }
 constexpr uint32_t lcm_u32(uint32_t a, uint32_t b) { return a / gcd_u32(a, b) * b; }
 uint32_t extract_max_bins(bool wide) { return (uint32_t)(wide ? kMaxL1BinsW : kMaxL1Bins); }
+uint32_t extract_l1_bits(bool wide, bool folding) {
+    return wide ? (uint32_t)OKM_L1_BITS_W : (uint32_t)(folding ? OKM_L1_BITS_FOLD : OKM_L1_BITS);
+}
 
 template <int K>
 __global__ __launch_bounds__(kExtractBlock) void k_extract_hist(const uint8_t *__restrict__ seq, ExtractGeom g,

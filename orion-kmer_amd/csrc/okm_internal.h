@@ -127,6 +127,9 @@ void launch_fill_line_tails(void *stream, const unsigned long long *end, uint32_
                             const unsigned long long *cap = nullptr);
 uint32_t extract_tile();
 uint32_t extract_max_bins(bool wide);  // L1 bins: k <= 32 kernels vs k in 33..64
+// L1 key bits a context extracts with: wide keys, or k <= 32 counting batch by
+// batch (9) vs folding many batches into one table (10)
+uint32_t extract_l1_bits(bool wide, bool folding);
 uint32_t part_max_bins(bool weighted, bool wide);
 
 // Exclusive scan of n u64 values (in -> out, out may equal in); tmp >= scan_tmp_elems(n).
