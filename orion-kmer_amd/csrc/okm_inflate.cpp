@@ -517,9 +517,6 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
             pc.ok = find_and_decode(p, nbytes, cut[i], to, cut[i + 1], *scratch, pc);
         }
         delete scratch;
-        if (prof)
-            fprintf(stderr, "[okm gz] chunk %zu: %.1f ms, start %zu (cut %zu), out %zu\n", i, (now() - t0) * 1e3,
-                    pc.start, cut[i], pc.out.n);
     });
     if (broken) return fail(OKM_E_IO, "invalid gzip data");
     const double t1 = now();
