@@ -266,7 +266,7 @@ def main():
             x.join()
         if err:
             raise err[0]
-        return res[-1]
+        return res[-1] if res else 0
 
     def barrier_sync():
         torch.cuda.synchronize()
