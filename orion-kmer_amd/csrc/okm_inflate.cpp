@@ -39,7 +39,6 @@
 #include <chrono>
 #include <cstdio>
 #include <atomic>
-#include <deque>
 #include <vector>
 
 #include "okm_internal.h"
@@ -497,135 +496,148 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
     std::vector<size_t> cut(nch + 1);
     for (size_t i = 0; i <= nch; ++i) cut[i] = 8 * (nbytes * i / nch);
     cut[nch] = SIZE_MAX;
-    std::vector<Piece> pcs(nch);
-    std::atomic<int> broken{0};
+    // rounds of R chunks: the 16-bit pieces of one round at a time (host memory
+    // stays ~R x 4 MiB x 12 B whatever the member's size)
+    const size_t R = std::max<size_t>(2, env_size("OKM_GZ_ROUND_CHUNKS", 2 * (size_t)nt, 1));
     const bool prof = getenv("OKM_GZ_PROF") != nullptr;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    const double t0 = now();
-    parallel_for(nch, [&](size_t i) {
-        Codes *scratch = new Codes;
-        Piece &pc = pcs[i];
-        pc.out.v.resize(std::max<size_t>(1 << 16, (size_t)(nbytes / nch) * 6));
-        if (i == 0) {
-            pc.ok = decode_run(p, nbytes, 0, cut[1], false, *scratch, pc);
-            if (!pc.ok) broken = 1;
-        } else {
-            // a block start within the chunk's first MiB (dynamic blocks are far
-            // smaller; a stored-block stretch without one is decoded again from
-            // the true boundary instead of searched bit by bit)
-            const size_t to = std::min({cut[i + 1], 8 * nbytes, cut[i] + (size_t(8) << 20)});
-            pc.ok = find_and_decode(p, nbytes, cut[i], to, cut[i + 1], *scratch, pc);
-        }
-        delete scratch;
-    });
-    if (broken) return fail(OKM_E_IO, "invalid gzip data");
-    const double t1 = now();
-    // stitch: a chunk is used where it starts at the previous one's stop
-    std::vector<Piece *> seq;
-    std::deque<Piece> redo;
-    seq.push_back(&pcs[0]);
-    size_t pos = pcs[0].stop;
-    bool fin = pcs[0].final;
-    for (size_t j = 1; !fin; ++j) {
-        if (j < nch && pcs[j].ok && pcs[j].start == pos) {
-            seq.push_back(&pcs[j]);
-        } else {
-            redo.emplace_back();
-            Piece &r = redo.back();
-            Codes *scratch = new Codes;
-            r.out.v.resize(1 << 20);
-            const bool good = decode_run(p, nbytes, pos, j + 1 <= nch ? cut[j + 1] : SIZE_MAX, true, *scratch, r);
-            delete scratch;
-            if (!good) return fail(OKM_E_IO, "invalid gzip data");
-            seq.push_back(&r);
-        }
-        pos = seq.back()->stop;
-        fin = seq.back()->final;
-        if (j > nch + 1 && !fin) return fail(OKM_E_IO, "invalid gzip data");
-    }
-    const double t2 = now();
-    // placement
+    double t_dec = 0, t_res = 0, t_crc = 0;
+    size_t rounds = 0, used_pieces = 0, dropped = 0;
     const size_t base = out.size();
-    std::vector<size_t> at(seq.size() + 1, base);
-    for (size_t i = 0; i < seq.size(); ++i) at[i + 1] = at[i] + seq[i]->out.n;
-    out.resize(at.back());
-    uint8_t *o = out.data();
-    std::atomic<int> bad{0};
-    auto resolve = [&](size_t i, size_t a, size_t b) {  // piece i's outputs [a, b)
-        const uint16_t *s = seq[i]->out.v.data();
-        uint8_t *d = o + at[i];
-        const int64_t wbase = (int64_t)(at[i] - base) - (int64_t)kWin;  // member offset of window byte 0
-        for (size_t x = a; x < b; ++x) {
-            if ((x & 31) == 0 && x + 32 <= b) {  // a run of 32 literals narrows in one vector pass
-                uint16_t any = 0;
-                for (int u = 0; u < 32; ++u) any |= s[x + u];
-                if (!(any & 0xFF00)) {
-                    for (int u = 0; u < 32; ++u) d[x + u] = (uint8_t)s[x + u];
-                    x += 31;
+    {
+        const uint8_t *t4 = in + n - 4;  // a single member's ISIZE (mod 2^32) as a size hint
+        const size_t isz = t4[0] | (t4[1] << 8) | (t4[2] << 16) | ((size_t)t4[3] << 24);
+        out.reserve(base + std::max(isz, nbytes * 4));
+    }
+    uLong crc = crc32(0L, Z_NULL, 0);
+    size_t pos = 0;  // bit position of the next block header (a true boundary)
+    bool fin = false;
+    size_t misses = 0;  // consecutive rounds that used only their first chunk
+    while (!fin) {
+        size_t j0 = 0;  // the chunk whose region holds pos
+        while (j0 + 1 < nch && cut[j0 + 1] <= pos) ++j0;
+        // a stretch with no dynamic blocks to find (stored blocks: incompressible
+        // input) is decoded one chunk at a time, with a parallel try every 8 rounds
+        const size_t nr = std::min(misses >= 2 && (rounds & 7) ? 1 : R, nch - j0);
+        std::vector<Piece> pcs(nr);
+        std::atomic<int> broken{0};
+        double t0 = now();
+        parallel_for(nr, [&](size_t q) {
+            const size_t i = j0 + q;
+            Codes *scratch = new Codes;
+            Piece &pc = pcs[q];
+            pc.out.v.resize(std::max<size_t>(1 << 16, (size_t)(nbytes / nch) * 6));
+            if (q == 0) {  // from the true boundary; copies before it are markers (unless the stream starts here)
+                pc.ok = decode_run(p, nbytes, pos, cut[i + 1], pos != 0, *scratch, pc);
+                if (!pc.ok) broken = 1;
+            } else {
+                // a block start within the chunk's first MiB (dynamic blocks are
+                // far smaller; a stored-block stretch without one is decoded from
+                // the true boundary by a later round instead of searched bit by bit)
+                const size_t to = std::min({cut[i + 1], 8 * nbytes, cut[i] + (size_t(8) << 20)});
+                pc.ok = find_and_decode(p, nbytes, cut[i], to, cut[i + 1], *scratch, pc);
+            }
+            delete scratch;
+        });
+        t_dec += now() - t0;
+        if (broken) return fail(OKM_E_IO, "invalid gzip data");
+        // stitch: a chunk is used where it starts at the previous one's stop;
+        // the round ends at the first that does not (the next round decodes
+        // from that true boundary)
+        size_t ns = 1;
+        pos = pcs[0].stop;
+        fin = pcs[0].final;
+        while (!fin && ns < nr && pcs[ns].ok && pcs[ns].start == pos) {
+            pos = pcs[ns].stop;
+            fin = pcs[ns].final;
+            ++ns;
+        }
+        dropped += nr - ns;
+        if (nr > 1) misses = ns == 1 ? misses + 1 : 0;
+        used_pieces += ns;
+        ++rounds;
+        // place and resolve: markers name bytes of the 32 KiB before their piece
+        t0 = now();
+        const size_t rbase = out.size();
+        std::vector<size_t> at(ns + 1, rbase);
+        for (size_t q = 0; q < ns; ++q) at[q + 1] = at[q] + pcs[q].out.n;
+        out.resize(at[ns]);
+        uint8_t *o = out.data();
+        std::atomic<int> bad{0};
+        auto resolve = [&](size_t q, size_t a, size_t b) {  // piece q's outputs [a, b)
+            const uint16_t *sv = pcs[q].out.v.data();
+            uint8_t *d = o + at[q];
+            const int64_t wbase = (int64_t)(at[q] - base) - (int64_t)kWin;  // member offset of window byte 0
+            for (size_t x = a; x < b; ++x) {
+                if ((x & 31) == 0 && x + 32 <= b) {  // a run of 32 literals narrows in one vector pass
+                    uint16_t any = 0;
+                    for (int u = 0; u < 32; ++u) any |= sv[x + u];
+                    if (!(any & 0xFF00)) {
+                        for (int u = 0; u < 32; ++u) d[x + u] = (uint8_t)sv[x + u];
+                        x += 31;
+                        continue;
+                    }
+                }
+                const uint16_t v = sv[x];
+                if (v < 256) {
+                    d[x] = (uint8_t)v;
                     continue;
                 }
+                const int64_t src = wbase + (int64_t)(v & (kWin - 1));
+                if (src < 0) {
+                    bad = 1;
+                    return;
+                }
+                d[x] = o[base + src];
             }
-            const uint16_t v = s[x];
-            if (v < 256) {
-                d[x] = (uint8_t)v;
-                continue;
-            }
-            const int64_t src = wbase + (int64_t)(v & (kWin - 1));
-            if (src < 0) {
-                bad = 1;
-                return;
-            }
-            d[x] = o[base + src];
+        };
+        // the tail (last 32 KiB) of every piece in order, then the rest in parallel
+        for (size_t q = 0; q < ns; ++q) {
+            const size_t len = pcs[q].out.n;
+            resolve(q, len > kWin ? len - kWin : 0, len);
+            if (bad) return fail(OKM_E_IO, "invalid gzip data");
         }
-    };
-    const double t3 = now();
-    // the tail (last 32 KiB) of every piece in order, then the rest in parallel
-    for (size_t i = 0; i < seq.size(); ++i) {
-        const size_t len = seq[i]->out.n;
-        resolve(i, len > kWin ? len - kWin : 0, len);
+        constexpr size_t kSlice = 1 << 20;
+        std::vector<std::pair<size_t, size_t>> jobs;
+        for (size_t q = 0; q < ns; ++q) {
+            const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
+            for (size_t a = 0; a < head; a += kSlice) jobs.emplace_back(q, a);
+        }
+        parallel_for(jobs.size(), [&](size_t j) {
+            const size_t q = jobs[j].first, a = jobs[j].second;
+            const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
+            resolve(q, a, std::min(head, a + kSlice));
+        });
         if (bad) return fail(OKM_E_IO, "invalid gzip data");
+        t_res += now() - t0;
+        // CRC-32 of this round's bytes: per-slice CRCs, combined in order
+        t0 = now();
+        const size_t len = at[ns] - rbase;
+        const size_t nsl = std::max<size_t>(1, (len + (4u << 20) - 1) / (4u << 20));
+        std::vector<uLong> sc(nsl);
+        parallel_for(nsl, [&](size_t sl) {
+            const size_t a = len * sl / nsl, b = len * (sl + 1) / nsl;
+            sc[sl] = crc32(crc32(0L, Z_NULL, 0), o + rbase + a, (uInt)(b - a));  // slices < 4 GiB
+        });
+        for (size_t sl = 0; sl < nsl; ++sl)
+            crc = crc32_combine(crc, sc[sl], (z_off_t)(len * (sl + 1) / nsl - len * sl / nsl));
+        t_crc += now() - t0;
+        if (rounds > 4 * nch + 4) return fail(OKM_E_IO, "invalid gzip data");  // no progress (cannot happen)
     }
-    constexpr size_t kSlice = 1 << 20;
-    std::vector<std::pair<size_t, size_t>> jobs;
-    for (size_t i = 0; i < seq.size(); ++i) {
-        const size_t len = seq[i]->out.n, head = len > kWin ? len - kWin : 0;
-        for (size_t a = 0; a < head; a += kSlice) jobs.emplace_back(i, a);
-    }
-    parallel_for(jobs.size(), [&](size_t j) {
-        const size_t i = jobs[j].first, a = jobs[j].second;
-        const size_t len = seq[i]->out.n, head = len > kWin ? len - kWin : 0;
-        resolve(i, a, std::min(head, a + kSlice));
-    });
-    if (bad) return fail(OKM_E_IO, "invalid gzip data");
-    const double t4 = now();
     // trailer: CRC-32 and ISIZE of this member
     const size_t tb = (pos + 7) >> 3;
     if (tb + 8 > nbytes) return fail(OKM_E_IO, "truncated gzip data");
     const uint8_t *t = p + tb;
     const uint32_t crc_want = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
     const uint32_t isz = t[4] | (t[5] << 8) | (t[6] << 16) | ((uint32_t)t[7] << 24);
-    const size_t total = at.back() - base;
-    if ((uint32_t)total != isz) return fail(OKM_E_IO, "invalid gzip data");
-    const size_t ns = std::max<size_t>(1, (total + (4u << 20) - 1) / (4u << 20));
-    std::vector<uLong> crc(ns);
-    parallel_for(ns, [&](size_t s) {
-        const size_t a = total * s / ns, b = total * (s + 1) / ns;
-        uLong c = crc32(0L, Z_NULL, 0);
-        for (size_t x = a; x < b;) {
-            const size_t m = std::min<size_t>(b - x, 1u << 30);
-            c = crc32(c, o + base + x, (uInt)m);
-            x += m;
-        }
-        crc[s] = c;
-    });
-    uLong c = crc[0];
-    for (size_t s = 1; s < ns; ++s) c = crc32_combine(c, crc[s], (z_off_t)(total * (s + 1) / ns - total * s / ns));
-    if ((uint32_t)c != crc_want) return fail(OKM_E_IO, "invalid gzip data");
+    const size_t total = out.size() - base;
+    if ((uint32_t)total != isz || (uint32_t)crc != crc_want) return fail(OKM_E_IO, "invalid gzip data");
     *used = h + tb + 8;
     if (prof)
-        fprintf(stderr, "[okm gz] %zu chunks, %zu pieces (%zu redone), %.1f MB -> %.1f MB: decode %.1f ms, stitch %.1f, place %.1f, resolve %.1f, crc %.1f\n",
-                nch, seq.size(), redo.size(), nbytes / 1e6, total / 1e6, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
-                (t4 - t3) * 1e3, (now() - t4) * 1e3);
+        fprintf(stderr,
+                "[okm gz] %zu chunks in %zu rounds (%zu pieces used, %zu dropped), %.1f MB -> %.1f MB: decode %.1f ms, "
+                "resolve %.1f, crc %.1f\n",
+                nch, rounds, used_pieces, dropped, nbytes / 1e6, total / 1e6, t_dec * 1e3, t_res * 1e3, t_crc * 1e3);
     return OKM_OK;
 }
 
