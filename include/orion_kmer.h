@@ -101,7 +101,8 @@ const char *okm_last_error(void);
  * ---------------------------------------------------------------------- */
 
 /* device: HIP ordinal.  distinct_hint: expected distinct k-mers (0 = unknown);
- * sizing only, never correctness. */
+ * sizing only, never correctness (>= 2^30: the context starts with the
+ * folding geometry it would otherwise take at its first fold). */
 okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint);
 void okm_destroy(okm_ctx *ctx);
 /* Forget all input and results; keep device allocations for reuse. */
