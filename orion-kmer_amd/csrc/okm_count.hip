@@ -804,9 +804,16 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                    ull *__restrict__ ctl, uint32_t *__restrict__ defer, const ull *__restrict__ guard,
-                   const ull *__restrict__ d_nitems) {
+                   const ull *__restrict__ d_nitems, uint32_t chunked) {
     if (guard && (guard[0] | guard[1])) return;  // speculative launch whose items were not valid
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
+    // items dealt by stride (item = block + k * grid), or (chunked) as one
+    // contiguous range per block: neighbouring items, whose keys and output
+    // slots share lines at their boundaries, then run on one CU in turn
+    const uint32_t per = chunked ? (nitems + gridDim.x - 1) / gridDim.x : 1u;
+    const uint32_t ibeg = chunked ? blockIdx.x * per : blockIdx.x;
+    const uint32_t iend = chunked ? min(nitems, ibeg + per) : nitems;
+    const uint32_t istep = chunked ? 1u : gridDim.x;
     __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     // multi-segment items: their descriptors are staged in the rest buffer,
@@ -821,11 +828,11 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     // Block-uniform values that steer code containing barriers come from
     // blockIdx / scalar loads (see DESIGN.md on the structuriser).
     DevItem nxt{};
-    if (OKM_COUNT_DESC_PF && blockIdx.x < nitems) nxt = items[blockIdx.x];
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    if (OKM_COUNT_DESC_PF && ibeg < iend) nxt = items[ibeg];
+    for (uint32_t item = ibeg; item < iend; item += istep) {
         PMARK(0);
         const DevItem it = OKM_COUNT_DESC_PF ? nxt : items[item];
-        if (OKM_COUNT_DESC_PF && item + gridDim.x < nitems) nxt = items[item + gridDim.x];
+        if (OKM_COUNT_DESC_PF && item + istep < iend) nxt = items[item + istep];
         const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
         if (total == 0) {  // an empty fan-out slot (block-uniform)
             if (t == 0) n_out[item] = 0;
@@ -969,20 +976,35 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                                out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
         return;
     }
-    const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
+    // OKM_COUNT_GRID: workgroups of the unweighted tag kernel (odd, so fan-out
+    // slots spread over blocks).  16383 (~11 C2 items each, 16 generations of
+    // the 1024 resident workgroups) against 4095: count_items 1.550 vs 1.590-1.600
+    // ms; 2047 1.653, 8191 1.568, 32767 1.563, 65535 1.589, one per item 1.802
+    // (profiles/r04_ab_count_grid.txt).  OKM_COUNT_CHUNKED=1: contiguous item
+    // ranges per workgroup instead of a stride (slower: 1.63 ms at 4095).
+    static const uint32_t grid_env = [] {
+        const char *e = getenv("OKM_COUNT_GRID");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 16383u;
+    }();
+    static const uint32_t chunked = [] {
+        const char *e = getenv("OKM_COUNT_CHUNKED");
+        return e && *e == '1' ? 1u : 0u;
+    }();
+    const uint32_t grid = nitems < grid_env ? nitems : grid_env;
+    const uint32_t wgrid = nitems < 4095u ? nitems : 4095u;  // weighted: one workgroup per CU resident
     const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
         if (nowrite)
-            hipLaunchKernelGGL((k_count_items<true, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
+            hipLaunchKernelGGL((k_count_items<true, true>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
         else
-            hipLaunchKernelGGL((k_count_items<true, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
+            hipLaunchKernelGGL((k_count_items<true, false>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer, guard, d_nitems);
+                           out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     }

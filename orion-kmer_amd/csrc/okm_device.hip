@@ -729,7 +729,11 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *err, const unsigned long long *d_nitems) {
     if (!nitems) return;
 #if OKM_COMPACT_WAVE
-    const dim3 g(nitems / 4u + 1u < 4096u ? nitems / 4u + 1u : 4096u), b(256);  // one wave per item
+    static const uint32_t cap = [] {  // OKM_COMPACT_GRID: A/B runs
+        const char *e = getenv("OKM_COMPACT_GRID");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4096u;
+    }();
+    const dim3 g(nitems / 4u + 1u < cap ? nitems / 4u + 1u : cap), b(256);  // one wave per item
 #else
     const dim3 g(nitems < 8191u ? nitems : 8191u), b(256);  // odd: fan-out slots spread over blocks
 #endif

@@ -1035,7 +1035,14 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     c->hprof.mark("idle");
     const uint64_t tile = extract_tile();
     uint64_t tiles = (n + tile - 1) / tile;
-    uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, 2048);
+    // extraction workgroups: 8192 (C2: ~4 tiles each) against 2048: extract_scatter
+    // 1.438 vs 1.484 ms over 4 interleaved runs, 4096 1.447 (profiles/r04_ab_extract_blocks.txt);
+    // OKM_EXTRACT_BLOCKS overrides
+    static const uint64_t max_blocks = [] {
+        const char *e = getenv("OKM_EXTRACT_BLOCKS");
+        return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 8192ull;
+    }();
+    uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, max_blocks);
     uint64_t chunk = ((tiles + nblocks - 1) / nblocks) * tile;
     nblocks = (uint32_t)((n + chunk - 1) / chunk);
     ExtractGeom g{n, c->k, c->shift1, c->nbins, nblocks, chunk, 1};

@@ -376,7 +376,14 @@ void k_part_scatter_tile(
     }
 }
 
-static uint32_t part_grid(uint32_t nchunks) { return nchunks < 4096u ? nchunks : 4096u; }
+// OKM_PART_GRID: cap on the partition kernels' workgroups (A/B runs)
+static uint32_t part_grid(uint32_t nchunks) {
+    static const uint32_t cap = [] {
+        const char *e = getenv("OKM_PART_GRID");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4096u;
+    }();
+    return nchunks < cap ? nchunks : cap;
+}
 
 void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                       uint32_t max_local, uint32_t *HC, unsigned long long *Hg, bool wide) {
