@@ -966,8 +966,19 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                         const unsigned long long *guard, const unsigned long long *d_nitems, bool nowrite) {
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
+    // wide (full-mode) count: 8191 workgroups against 4095, k=63 at 1 Gbases
+    // count_items 8.61-8.62 vs 8.75-8.78 ms over 3 interleaved runs (16383: 8.60-8.65);
+    // the weighted tag kernel (C3's merges) showed no difference at 1023 / 16383
+    static const uint32_t wide_cap = [] {  // OKM_COUNT_WIDE_GRID: A/B runs
+        const char *e = getenv("OKM_COUNT_WIDE_GRID");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 8191u;
+    }();
+    static const uint32_t weighted_cap = [] {  // OKM_COUNT_W_GRID: A/B runs
+        const char *e = getenv("OKM_COUNT_W_GRID");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4095u;
+    }();
     if (wide) {  // every item through the full / dense modes
-        const uint32_t grid = nitems < 4095u ? nitems : 4095u;  // odd: fan-out slots spread over blocks
+        const uint32_t grid = nitems < wide_cap ? nitems : wide_cap;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                                out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
@@ -991,7 +1002,7 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
         return e && *e == '1' ? 1u : 0u;
     }();
     const uint32_t grid = nitems < grid_env ? nitems : grid_env;
-    const uint32_t wgrid = nitems < 4095u ? nitems : 4095u;  // weighted: one workgroup per CU resident
+    const uint32_t wgrid = nitems < weighted_cap ? nitems : weighted_cap;  // weighted: one workgroup per CU resident
     const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
         if (nowrite)
