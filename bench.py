@@ -154,6 +154,9 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--streams", type=int, default=3,
                     help="N=1: batches in flight (engine contexts / HIP streams, one host thread each)")
+    ap.add_argument("--dist-workers", type=int, default=2,
+                    help="N>1: threads counting the next batches (each into its own context) while the "
+                         "exchange + merge of the current one runs")
     ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
                     help="c2: BASELINE configs[1] (1 GiB per GPU, weak scaling; default); c3: BASELINE configs[2] "
                          "(50 GiB of reads from a 1 Gbp genome sharded 1/N over the ranks) as the line's value")
@@ -214,10 +217,10 @@ def main():
     # Batches in flight: at N=1, S contexts (each its own HIP stream and result
     # table) driven by S host threads count whole batches concurrently, so one
     # batch's host syncs and latency-bound phases overlap another's streaming
-    # kernels.  At N>1 (okm.pipeline.OwnedCountPipeline) a worker thread counts
-    # batch i+1 into two contexts in turn while this thread runs the step's
-    # failure agreement and okm_merge_owned of batch i (RCCL on the library's
-    # own stream) into one of two owner contexts.
+    # kernels.  At N>1 (okm.pipeline.OwnedCountPipeline) --dist-workers threads
+    # count the next batches into their own contexts while this thread runs the
+    # step's failure agreement and okm_merge_owned of batch i (RCCL on the
+    # library's own stream) into one of two owner contexts.
     S = max(1, args.streams)
 
     def count_batch(c):
@@ -228,7 +231,8 @@ def main():
     pipe = None
     if dist_on:
         pipe = OwnedCountPipeline(comm, lambda: okm.KmerCounter(K, "count", device),
-                                  lambda c, i: c.add_device_batch(dbuf.address, len(batch)))
+                                  lambda c, i: c.add_device_batch(dbuf.address, len(batch)),
+                                  workers=max(1, args.dist_workers))
         ctrs, mergers = list(pipe.local), list(pipe.owners)
     else:
         ctrs, mergers = [okm.KmerCounter(K, "count", device) for _ in range(S)], []

@@ -8,10 +8,10 @@ HIP histogram / pack / unpack kernels, grouped ncclSend/ncclRecv over xGMI,
 the owner's count of the received sorted slices).  This module is the host
 orchestration around it that ``bench.py`` runs at N>1:
 
-* :func:`run_pipelined` overlaps the count of batch i+1 (a worker thread,
-  two local contexts in turn) with the exchange + merge of batch i (this
-  thread, the only one that issues collectives, so every rank issues them in
-  one order);
+* :func:`run_pipelined` overlaps the counts of the next batches (worker
+  threads, one local context each plus one spare, taken in turn) with the
+  exchange + merge of batch i (this thread, the only one that issues
+  collectives, so every rank issues them in one order);
 * :class:`OwnedCountPipeline` is that loop over ``okm.Comm`` and
   ``okm.KmerCounter`` objects, with the failure agreement the merge needs:
   a rank whose count failed still joins the step's one-word all-reduce, and
@@ -40,13 +40,16 @@ class PeerFailure(RuntimeError):
 
 def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
                   consume: Callable[[int, int, object, Callable[[], None]], object],
-                  finish: Optional[Callable[[int, int, object], object]] = None) -> List[object]:
-    """Pipelined step loop.  A worker thread counts batch i into table buffer
-    i % 2 (count_into(i, j) -> handle) while this thread consumes the previous
-    one (consume(i, j, handle, release) -> result), so the exchange of batch i
-    overlaps the count of batch i + 1.  consume calls release() once the
-    table may be reused (the buffer may then count batch i + 2).  Only this
+                  finish: Optional[Callable[[int, int, object], object]] = None,
+                  workers: int = 1, nbuf: int = 2) -> List[object]:
+    """Pipelined step loop.  `workers` threads count batches (count_into(i, j)
+    -> handle, batch i into table buffer j = i % nbuf; steps are taken in
+    order, and a buffer is reused only after consume released it) while this
+    thread consumes them in step order (consume(i, j, handle, release) ->
+    result), so the exchange of batch i overlaps the counts of the next
+    batches.  consume calls release() once the table may be reused.  Only this
     thread issues collectives, so every rank issues them in the same order.
+    workers <= nbuf - 1 keeps one buffer for the batch being consumed.
 
     With `finish`, consume's result is a payload handed to a third thread that
     runs finish(i, m, payload) -> result on merge slot m = i % 2 (no
@@ -54,8 +57,11 @@ def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
     batch i + 1 and the count of batch i + 2, and the slot is reused by batch
     i + 2 only after its finish returned.  Results are in step order either
     way.  An exception in any thread is re-raised here."""
-    free = [threading.Semaphore(1), threading.Semaphore(1)]
-    q: "queue.Queue" = queue.Queue()
+    workers = max(1, min(workers, max(1, nbuf - 1)))
+    free = [threading.Semaphore(1) for _ in range(nbuf)]
+    done: dict = {}
+    cv = threading.Condition()
+    nxt = [0]
     err: List[BaseException] = []
     stop = threading.Event()
 
@@ -67,14 +73,23 @@ def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
 
     def producer():
         try:
-            for i in range(nsteps):
-                if not acquire(free[i % 2]):
+            while not stop.is_set():
+                with cv:
+                    i = nxt[0]
+                    if i >= nsteps:
+                        return
+                    nxt[0] += 1
+                if not acquire(free[i % nbuf]):
                     return
-                q.put((i, i % 2, count_into(i, i % 2)))
+                h = count_into(i, i % nbuf)
+                with cv:
+                    done[i] = h
+                    cv.notify_all()
         except BaseException as e:  # surfaced on the consuming thread
-            err.append(e)
-            stop.set()
-            q.put(None)
+            with cv:
+                err.append(e)
+                stop.set()
+                cv.notify_all()
 
     out: List[object] = [None] * nsteps
     mfree = [threading.Semaphore(1), threading.Semaphore(1)]
@@ -93,22 +108,21 @@ def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
             err.append(e)
             stop.set()
 
-    th = threading.Thread(target=producer, daemon=True)
-    th.start()
+    ths = [threading.Thread(target=producer, daemon=True) for _ in range(workers)]
+    for th in ths:
+        th.start()
     fth = threading.Thread(target=finisher, daemon=True) if finish is not None else None
     if fth is not None:
         fth.start()
     try:
-        for _ in range(nsteps):
-            item = None
-            while item is None and not err:
-                try:
-                    item = q.get(timeout=0.1)
-                except queue.Empty:
-                    continue
-            if err or item is None:
-                break
-            i, j, h = item
+        for i in range(nsteps):
+            with cv:
+                while i not in done and not err:
+                    cv.wait(timeout=0.1)
+                if err:
+                    break
+                h = done.pop(i)
+            j = i % nbuf
             r = consume(i, j, h, free[j].release)
             if fth is None:
                 out[i] = r
@@ -121,7 +135,8 @@ def run_pipelined(nsteps: int, count_into: Callable[[int, int], object],
             mq.put(None)
             fth.join()
         stop.set()
-        th.join()
+        for th in ths:
+            th.join()
     if err:
         raise err[0]
     return out
@@ -141,10 +156,11 @@ def agree_or_raise(comm, failure: Optional[BaseException], what: str = "count") 
 
 class OwnedCountPipeline:
     """bench.py's N>1 step loop: per step, reset + add this
-    rank's batch (``add_batch(counter, step)``) + ``okm_count`` into one of two
-    local contexts, then ``okm_merge_owned`` of that table into one of two
-    owner contexts.  The count of step i+1 overlaps the exchange + merge of
-    step i (:func:`run_pipelined`).  Each step returns this rank's owned
+    rank's batch (``add_batch(counter, step)``) + ``okm_count`` into one of
+    workers + 1 local contexts (`workers` counting threads, each context its
+    own HIP stream), then ``okm_merge_owned`` of that table into one of two
+    owner contexts.  The counts of the next steps overlap the exchange + merge
+    of step i (:func:`run_pipelined`).  Each step returns this rank's owned
     distinct count; after :meth:`run` the owner context of the last step
     (:meth:`owned`) holds this rank's key range of the global table, and the
     ranks' ranges in rank order ARE the sorted table of every rank's batch.
@@ -153,10 +169,12 @@ class OwnedCountPipeline:
     device)``); `comm` is an ``okm.Comm`` (RCCL or loopback) or anything with
     ``allreduce`` and ``merge_owned``."""
 
-    def __init__(self, comm, counter: Callable[[], object], add_batch: Callable[[object, int], None]):
+    def __init__(self, comm, counter: Callable[[], object], add_batch: Callable[[object, int], None],
+                 workers: int = 1):
         self.comm = comm
         self.add_batch = add_batch
-        self.local = [counter(), counter()]
+        self.workers = max(1, workers)
+        self.local = [counter() for _ in range(self.workers + 1)]  # one more than the counting threads
         self.owners = [counter(), counter()]
         self.phase_ms = {"exchange": 0.0, "merge": 0.0}  # okm_comm_last_times, summed over steps
         self._last = 0
@@ -193,7 +211,7 @@ class OwnedCountPipeline:
                 self.phase_ms["merge"] += t["merge_ms"]
             return n
 
-        return run_pipelined(nsteps, count_into, consume)
+        return run_pipelined(nsteps, count_into, consume, workers=self.workers, nbuf=len(self.local))
 
     def owned(self):
         """The owner context of the last merged step."""

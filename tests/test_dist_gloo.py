@@ -397,7 +397,7 @@ def _step_reads(i):
     return _reads(3_000, 150, seed=40 + i).reshape(3_000, 151)
 
 
-def _owned_pipe_worker(rank, world, port, k, nsteps, fail_rank, fail_step, out_path):
+def _owned_pipe_worker(rank, world, port, k, nsteps, fail_rank, fail_step, out_path, workers=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -408,7 +408,7 @@ def _owned_pipe_worker(rank, world, port, k, nsteps, fail_rank, fail_step, out_p
         def add(ctx, step):
             ctx.add(np.ascontiguousarray(np.array_split(_step_reads(step), world)[rank]).reshape(-1), step)
 
-        pipe = OwnedCountPipeline(comm, lambda: _OracleCtx(k, fail_at), add)
+        pipe = OwnedCountPipeline(comm, lambda: _OracleCtx(k, fail_at), add, workers=workers)
         outcome = "ok"
         try:
             res = pipe.run(nsteps)
@@ -433,12 +433,15 @@ def _owned_pipe_worker(rank, world, port, k, nsteps, fail_rank, fail_step, out_p
         dist.destroy_process_group()
 
 
-def test_owned_count_pipeline_steps_equal_global_table(tmp_path):
+@pytest.mark.parametrize("workers", [1, 3])
+def test_owned_count_pipeline_steps_equal_global_table(tmp_path, workers):
     """Every step's owners hold the global table of that step's reads; the
-    last step's ranges in rank order equal the single-process table."""
-    k, world, nsteps = 31, 2, 4
+    last step's ranges in rank order equal the single-process table (one
+    counting thread, and three counting the next steps concurrently)."""
+    k, world, nsteps = 31, 2, 5
     out = os.path.join(str(tmp_path), "own")
-    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, -1, -1, out), nprocs=world, join=True)
+    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, -1, -1, out, workers), nprocs=world,
+             join=True)
     got = [np.load(out + f".{r}.npz") for r in range(world)]
     assert all(str(g["outcome"]) == "ok" for g in got)
     oc = OracleCounter(k)
@@ -452,14 +455,14 @@ def test_owned_count_pipeline_steps_equal_global_table(tmp_path):
     assert all(int(g["merges"]) == nsteps for g in got)
 
 
-@pytest.mark.parametrize("fail_rank,fail_step", [(1, 2), (0, 0)])
-def test_owned_count_pipeline_failure_stops_every_rank(tmp_path, fail_rank, fail_step):
+@pytest.mark.parametrize("fail_rank,fail_step,workers", [(1, 2, 1), (0, 0, 1), (1, 3, 2)])
+def test_owned_count_pipeline_failure_stops_every_rank(tmp_path, fail_rank, fail_step, workers):
     """a rank whose count fails must not let its peers run the
     merge alone: every rank raises at that step, before okm_merge_owned, and
     the process group is still usable (the barrier after the failure)."""
     k, world, nsteps = 25, 2, 5
     out = os.path.join(str(tmp_path), "fail")
-    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, fail_rank, fail_step, out),
+    mp.spawn(_owned_pipe_worker, args=(world, _free_port(), k, nsteps, fail_rank, fail_step, out, workers),
              nprocs=world, join=True)
     got = [np.load(out + f".{r}.npz") for r in range(world)]
     for r, g in enumerate(got):

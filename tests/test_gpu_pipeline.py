@@ -3,9 +3,10 @@
 pack / unpack kernels and owner merge run, the transport is device copies).
 
 * okm.pipeline.OwnedCountPipeline — bench.py's N>1 step loop: every rank
-  counts its batch into one of two contexts while the previous batch's table
-  goes through the step's failure agreement and okm_merge_owned — at P = 2
-  and P = 8, every step's owned ranges (rank order) exact against the
+  counts its next batches (one to three counting threads, a context each)
+  while the previous batch's table goes through the step's failure agreement
+  and okm_merge_owned — at P = 2, 3 and 8, every step's owned ranges (rank
+  order) exact against the
   restatement of all ranks' reads (count.rs:48: one map over all input,
   :106-119 drained and sorted once);
 * the failure agreement: a rank whose count fails stops every rank at that
@@ -84,9 +85,9 @@ class _Counting:
         return self.comm.last_times()
 
 
-@pytest.mark.parametrize("P", [2, 8])
-def test_owned_count_pipeline_loopback_exact(P):
-    nsteps, rpr = 3, 40_000
+@pytest.mark.parametrize("P,workers", [(2, 1), (8, 1), (2, 2), (3, 3)])
+def test_owned_count_pipeline_loopback_exact(P, workers):
+    nsteps, rpr = 4, 40_000
     batches = [[_step_batch(i, r, P, rpr) for i in range(nsteps)] for r in range(P)]
     bufs = [[okm.DeviceBuffer(len(b)) for b in row] for row in batches]
     for row, brow in zip(bufs, batches):
@@ -94,7 +95,8 @@ def test_owned_count_pipeline_loopback_exact(P):
             d.upload(b)
     comms = okm.Comm.init_loopback(P, 0)
     pipes = [OwnedCountPipeline(_Counting(comms[r]), lambda: okm.KmerCounter(K, "count", 0),
-                                lambda c, i, r=r: c.add_device_batch(bufs[r][i].address, len(batches[r][i])))
+                                lambda c, i, r=r: c.add_device_batch(bufs[r][i].address, len(batches[r][i])),
+                                workers=workers)
              for r in range(P)]
 
     def body(r):
