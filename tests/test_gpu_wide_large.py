@@ -93,7 +93,7 @@ def _rc128(lo, hi, k):
     return rlo, rhi
 
 
-def test_k63_c4_size_properties_memory_and_two_exact_ranges():
+def test_k63_c4_size_properties_memory_and_exact_ranges():
     batch, lens = ont_batch(5.36, seed=44, genome_len=1_000_000_000)
     buf = okm.DeviceBuffer(len(batch))
     buf.upload(batch)
@@ -119,8 +119,10 @@ def test_k63_c4_size_properties_memory_and_two_exact_ranges():
         lo, hi = keys[idx, 0], keys[idx, 1]
         rlo, rhi = _rc128(lo, hi, K)
         assert not bool(_u128_lt(rlo, rhi, lo, hi).any()), "a key above its reverse complement"
-        # exact on two key ranges (a dense low one and a sparse high one)
-        ranges = [(3, 4), (200, 201)]
+        # exact on six key ranges of 1/256 of the key space each, spread over the
+        # first-base quarters (canonical keys are dense in the low ones, sparse
+        # in the last), each against a range-filtered restatement of every read
+        ranges = [(3, 4), (45, 46), (90, 91), (130, 131), (170, 171), (200, 201)]
         def below(bin_):  # keys whose top 8 bits are < bin_ (they are sorted)
             return sum(int(((keys[a:a + step, 1] >> (2 * K - 64 - 8)) < bin_).sum().item()) for a in range(0, n, step))
 
