@@ -228,21 +228,22 @@ struct Out16 {
 bool decode_huff(Bits &br, const Codes &c, Out16 &o, bool spec) {
     const uint32_t wmin = spec ? kWin : 0;  // how far before the chunk a copy may reach
     // bits in a register: buf holds `left` (>= 56 after a refill) unread bits
-    const uint8_t *const p = br.p, *const end = br.p + br.nbytes;
-    const uint8_t *in = p + (br.pos >> 3);
+    const uint8_t *const p = br.p;
+    const size_t nb = br.nbytes;
+    size_t ip = br.pos >> 3;  // next byte to load (may count past nb: those bits are zeros)
     uint64_t buf = 0;
     unsigned left = 0;
     auto refill = [&]() {
-        if (in + 8 <= end) {
+        if (ip + 8 <= nb) {
             uint64_t w;
-            memcpy(&w, in, 8);
+            memcpy(&w, p + ip, 8);
             buf |= w << left;
-            in += (63 - left) >> 3;
+            ip += (63 - left) >> 3;
             left |= 56;
         } else {
-            while (left <= 56) {  // past the end: zero bits (in keeps counting, so the overrun shows)
-                buf |= (uint64_t)(in < end ? *in : 0) << left;
-                ++in;
+            while (left <= 56) {  // past the end: zero bits (ip keeps counting, so the overrun shows)
+                buf |= (uint64_t)(ip < nb ? p[ip] : 0) << left;
+                ++ip;
                 left += 8;
             }
         }
@@ -250,7 +251,7 @@ bool decode_huff(Bits &br, const Codes &c, Out16 &o, bool spec) {
     refill();
     buf >>= br.pos & 7;
     left -= br.pos & 7;
-    auto pos_now = [&]() { return (size_t)(in - p) * 8 - left; };
+    auto pos_now = [&]() { return ip * 8 - left; };
     const uint32_t *lt = c.lit.t, *dt = c.dist.t;
     auto look = [](const uint32_t *t, uint64_t v) {
         uint32_t e = t[v & ((1u << Huff::kPri) - 1)];
@@ -339,7 +340,7 @@ bool decode_huff(Bits &br, const Codes &c, Out16 &o, bool spec) {
             }
         }
         o.n = n;
-        if (in > end + 8) return false;  // ran far past the input
+        if (ip > nb + 8) return false;  // ran far past the input
     }
 }
 
