@@ -9,8 +9,9 @@
 #   tools/gpu_lease.sh bench [bench.py args]    one bench line -> gpurun_out/bench/line.json
 #   tools/gpu_lease.sh exchange [args]          bench.py's N>1 path at world 1 (torchrun, RCCL self-send)
 #   tools/gpu_lease.sh profile <round>          kernel trace + stats + PMC traffic (tools/profile_round.sh)
-#   tools/gpu_lease.sh lds <round>              LDS / SQ counters of the C2 kernels -> profiles/<round>_lds_counters.json
-#   tools/gpu_lease.sh sq <round>               SQ wait / issue counters of the C2 kernels
+#   tools/gpu_lease.sh lds <round>              LDS / SQ counters of the C2 kernels -> gpurun_out/lds/<round>_lds_counters.json
+#   tools/gpu_lease.sh sq <round>               SQ wait / issue counters -> gpurun_out/sq/<round>_sq_stalls.json
+# (only gpurun_out/ comes back from the box: copy what is judged into profiles/)
 #   tools/gpu_lease.sh paths <workload> [args]  tools/bench_paths.py --workload <workload>
 #   tools/gpu_lease.sh ab <reps> <builds...>    interleaved A/B of in-tree builds (tools/ab_interleave.sh)
 set -o pipefail
@@ -83,13 +84,13 @@ lds)
     R=${1:?round}
     sq_pass "$OUT/a" SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU \
         SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES &&
-    sq_sum "profiles/${R}_lds_counters.json" "$OUT/a/p_counter_collection.csv"
+    sq_sum "$OUT/${R}_lds_counters.json" "$OUT/a/p_counter_collection.csv"  # copy into profiles/ after the call
     ;;
 sq)
     R=${1:?round}
     sq_pass "$OUT/a" SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
         SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS &&
-    sq_sum "profiles/${R}_sq_stalls.json" "$OUT/a/p_counter_collection.csv"
+    sq_sum "$OUT/${R}_sq_stalls.json" "$OUT/a/p_counter_collection.csv"  # copy into profiles/ after the call
     ;;
 paths)
     W=${1:?workload}
