@@ -33,6 +33,7 @@
 // decoder, which produces the error the reference reports.
 #include <stdint.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -446,6 +447,14 @@ bool find_and_decode(const uint8_t *p, size_t nbytes, size_t from, size_t to, si
     return false;
 }
 
+// Transparent huge pages for a large buffer about to be written (fewer page
+// faults on first touch: the output of a 1 GiB member is 262 K small pages).
+void huge_pages(void *p, size_t bytes) {
+    const uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095;
+    const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)4095;
+    if (bytes >= (8u << 20) && e > a) (void)madvise((void *)a, e - a, MADV_HUGEPAGE);
+}
+
 size_t gzip_header_len(const uint8_t *in, size_t n) {
     if (n < 18 || in[0] != 0x1f || in[1] != 0x8b || in[2] != 8) return 0;
     const uint8_t flg = in[3];
@@ -509,7 +518,9 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
         const uint8_t *t4 = in + n - 4;  // a single member's ISIZE (mod 2^32) as a size hint
         const size_t isz = t4[0] | (t4[1] << 8) | (t4[2] << 16) | ((size_t)t4[3] << 24);
         out.reserve(base + std::max(isz, nbytes * 4));
+        huge_pages(out.data() + base, out.capacity() - base);
     }
+    std::vector<Piece> pool(R);  // 16-bit piece buffers, reused round to round (their pages stay faulted in)
     uLong crc = crc32(0L, Z_NULL, 0);
     size_t pos = 0;  // bit position of the next block header (a true boundary)
     bool fin = false;
@@ -520,14 +531,20 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
         // a stretch with no dynamic blocks to find (stored blocks: incompressible
         // input) is decoded one chunk at a time, with a parallel try every 8 rounds
         const size_t nr = std::min(misses >= 2 && (rounds & 7) ? 1 : R, nch - j0);
-        std::vector<Piece> pcs(nr);
+        std::vector<Piece> &pcs = pool;
         std::atomic<int> broken{0};
         double t0 = now();
         parallel_for(nr, [&](size_t q) {
             const size_t i = j0 + q;
             Codes *scratch = new Codes;
             Piece &pc = pcs[q];
-            pc.out.v.resize(std::max<size_t>(1 << 16, (size_t)(nbytes / nch) * 6));
+            pc.ok = pc.final = false;
+            pc.out.n = 0;
+            const size_t want = std::max<size_t>(1 << 16, (size_t)(nbytes / nch) * 6);
+            if (pc.out.v.size() < want) {
+                pc.out.v.resize(want);
+                huge_pages(pc.out.v.data(), pc.out.v.size() * sizeof(uint16_t));
+            }
             if (q == 0) {  // from the true boundary; copies before it are markers (unless the stream starts here)
                 pc.ok = decode_run(p, nbytes, pos, cut[i + 1], pos != 0, *scratch, pc);
                 if (!pc.ok) broken = 1;
@@ -592,11 +609,16 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
                 d[x] = o[base + src];
             }
         };
-        // the tail (last 32 KiB) of every piece in order, then the rest in parallel
+        // the tail (last 32 KiB) of every piece in order, then the rest in
+        // parallel; each stretch's CRC-32 is taken right after it is resolved
+        // (while it is in cache) and the CRCs are combined in output order
+        const uLong crc0 = crc32(0L, Z_NULL, 0);
+        std::vector<uLong> tail_crc(ns);
         for (size_t q = 0; q < ns; ++q) {
-            const size_t len = pcs[q].out.n;
-            resolve(q, len > kWin ? len - kWin : 0, len);
+            const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
+            resolve(q, head, len);
             if (bad) return fail(OKM_E_IO, "invalid gzip data");
+            tail_crc[q] = crc32(crc0, o + at[q] + head, (uInt)(len - head));
         }
         constexpr size_t kSlice = 1 << 20;
         std::vector<std::pair<size_t, size_t>> jobs;
@@ -604,24 +626,23 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
             const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
             for (size_t a = 0; a < head; a += kSlice) jobs.emplace_back(q, a);
         }
+        std::vector<uLong> job_crc(jobs.size());
         parallel_for(jobs.size(), [&](size_t j) {
             const size_t q = jobs[j].first, a = jobs[j].second;
             const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
-            resolve(q, a, std::min(head, a + kSlice));
+            const size_t b = std::min(head, a + kSlice);
+            resolve(q, a, b);
+            job_crc[j] = crc32(crc0, o + at[q] + a, (uInt)(b - a));
         });
         if (bad) return fail(OKM_E_IO, "invalid gzip data");
         t_res += now() - t0;
-        // CRC-32 of this round's bytes: per-slice CRCs, combined in order
         t0 = now();
-        const size_t len = at[ns] - rbase;
-        const size_t nsl = std::max<size_t>(1, (len + (4u << 20) - 1) / (4u << 20));
-        std::vector<uLong> sc(nsl);
-        parallel_for(nsl, [&](size_t sl) {
-            const size_t a = len * sl / nsl, b = len * (sl + 1) / nsl;
-            sc[sl] = crc32(crc32(0L, Z_NULL, 0), o + rbase + a, (uInt)(b - a));  // slices < 4 GiB
-        });
-        for (size_t sl = 0; sl < nsl; ++sl)
-            crc = crc32_combine(crc, sc[sl], (z_off_t)(len * (sl + 1) / nsl - len * sl / nsl));
+        for (size_t q = 0, j = 0; q < ns; ++q) {  // jobs are in piece order, then offset order
+            const size_t len = pcs[q].out.n, head = len > kWin ? len - kWin : 0;
+            for (; j < jobs.size() && jobs[j].first == q; ++j)
+                crc = crc32_combine(crc, job_crc[j], (z_off_t)(std::min(head, jobs[j].second + kSlice) - jobs[j].second));
+            crc = crc32_combine(crc, tail_crc[q], (z_off_t)(len - head));
+        }
         t_crc += now() - t0;
         if (rounds > 4 * nch + 4) return fail(OKM_E_IO, "invalid gzip data");  // no progress (cannot happen)
     }
