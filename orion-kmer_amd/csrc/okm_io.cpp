@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -640,6 +642,32 @@ static int gz_level() {
     return lvl;
 }
 
+bool OutWriter::parallel_gzip() const { return p_->f && p_->kind == 4; }
+void *OutWriter::new_compressor() {
+    Deflate *D = deflate_lib();
+    return D ? D->alloc_compressor(gz_level()) : nullptr;
+}
+void OutWriter::free_compressor(void *comp) {
+    if (comp) deflate_lib()->free_compressor(comp);
+}
+okm_status OutWriter::gzip_member(void *comp, const uint8_t *data, size_t n, Bytes &out) {
+    Deflate *D = deflate_lib();
+    if (!D || !comp) return fail(OKM_E_IO, "gzip compression failed");
+    out.resize(D->gzip_compress_bound(comp, n));
+    const size_t m = D->gzip_compress(comp, data, n, out.data(), out.size());
+    if (!m) return fail(OKM_E_IO, "gzip compression failed");
+    out.resize(m);
+    return OKM_OK;
+}
+okm_status OutWriter::write_raw(const uint8_t *data, size_t n) {
+    Impl &I = *p_;
+    if (!I.f) return fail(OKM_E_STATE, "writer not open");
+    if (!n) return OKM_OK;
+    if (fwrite(data, 1, n, I.f) != n) return fail(OKM_E_IO, "write failed");
+    I.wrote = true;
+    return OKM_OK;
+}
+
 okm_status OutWriter::write_blocks(const std::vector<std::pair<const uint8_t *, size_t>> &blocks) {
     Impl &I = *p_;
     if (!I.f) return fail(OKM_E_STATE, "writer not open");
@@ -930,6 +958,49 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
                 break;
             }
             at_byte += off[nb];
+        } else if (w.parallel_gzip()) {
+            // .gz: every block formatted and compressed into its own gzip member
+            // by one thread while it is in cache, and the members appended in
+            // order by a writer thread, so the file writes overlap the next
+            // blocks' compression (the members decompress to the text in order)
+            const size_t nt = std::min<size_t>(nb, (size_t)host_threads());
+            std::vector<Bytes> mem(nb);
+            std::vector<uint64_t> cnt(nb, 0);
+            std::vector<std::atomic<int>> ready(nb);
+            for (auto &r : ready) r = 0;
+            std::atomic<int> cbad{0};
+            std::thread writer([&]() {  // in order, as members complete
+                for (size_t b = 0; b < nb; ++b) {
+                    while (!ready[b].load(std::memory_order_acquire) && !cbad)
+                        std::this_thread::sleep_for(std::chrono::microseconds(50));
+                    if (cbad) return;
+                    if (w.write_raw(mem[b].data(), mem[b].size()) != OKM_OK) {
+                        cbad = 1;
+                        return;
+                    }
+                    Bytes().swap(mem[b]);
+                }
+            });
+            std::atomic<size_t> next{0};
+            parallel_for(nt, [&](size_t) {
+                void *comp = OutWriter::new_compressor();
+                std::string buf;
+                std::vector<uint64_t> fk, fc;
+                for (size_t b; !cbad && (b = next.fetch_add(1)) < nb;) {  // blocks in order, so the writer never waits long
+                    const uint64_t a = b * step, m = std::min<uint64_t>(step, n - a);
+                    format_filtered(k, keys + a * kw, counts + a, m, min_count, buf, fk, fc);
+                    cnt[b] = (uint64_t)std::count(buf.begin(), buf.end(), '\n');
+                    if (OutWriter::gzip_member(comp, (const uint8_t *)buf.data(), buf.size(), mem[b]) != OKM_OK) {
+                        cbad = 1;
+                        break;
+                    }
+                    ready[b].store(1, std::memory_order_release);
+                }
+                OutWriter::free_compressor(comp);
+            });
+            writer.join();
+            if (cbad) return fail(OKM_E_IO, std::string("write failed: ") + path);
+            for (size_t b = 0; b < nb; ++b) lines += cnt[b];
         } else {
             const size_t per_round = 2 * (size_t)host_threads();
             std::vector<std::string> buf(per_round);

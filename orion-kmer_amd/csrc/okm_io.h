@@ -87,6 +87,16 @@ class OutWriter {
     okm_status write(const void *data, size_t n);
     // Several blocks at once (.gz: compressed in parallel, one member each).
     okm_status write_blocks(const std::vector<std::pair<const uint8_t *, size_t>> &blocks);
+    // .gz written as parallel-compressed members: true when gzip_member() /
+    // write_raw() may be used (the caller compresses on its own threads).
+    bool parallel_gzip() const;
+    // One block as a complete gzip member (level OKM_GZ_LEVEL; `comp` is a
+    // compressor from new_compressor()), into out.
+    static okm_status gzip_member(void *comp, const uint8_t *data, size_t n, Bytes &out);
+    static void *new_compressor();
+    static void free_compressor(void *comp);
+    // Bytes already in the output format (compressed members), appended.
+    okm_status write_raw(const uint8_t *data, size_t n);
     okm_status close();
 
   private:
