@@ -47,6 +47,26 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "orion-kmer_amd"))
 
+
+def _launch_ranks_if_asked():
+    """`python3 bench.py --gpus N` with no WORLD_SIZE in the environment runs
+    N rank processes itself (okm.launch: device count probed in a child, so
+    this process makes no HIP call before it starts them; rank 0's line is
+    relayed; any failing rank fails the run), or exits 2 when fewer devices
+    are visible than ranks asked for.  Under torch.distributed.run (WORLD_SIZE
+    set) this is a no-op."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    from okm.launch import launch_or_none
+    rc = launch_or_none(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+
+
+if __name__ == "__main__":
+    _launch_ranks_if_asked()
+
 import numpy as np  # noqa: E402
 
 import okm  # noqa: E402
@@ -186,18 +206,30 @@ def init_comm(world, rank, device):
     return okm.Comm(world, rank, bytes(uid.numpy().tobytes()), device)
 
 
-def main():
-    args = parse()
+def rank_device(args):
+    """(world, rank, device) of this process: one rank per GPU, LOCAL_RANK's
+    device.  A --gpus that disagrees with WORLD_SIZE, or a rank without a
+    device of its own, is an error (RCCL refuses two ranks on one GPU, and a
+    line must never report GPUs it did not use)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.workload == "c3":
-        return main_c3(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    # one rank per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
-    device = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(device)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU, "
+                         f"or run `python3 bench.py --gpus N` without WORLD_SIZE)")
+    ndev = okm.device_count()
+    if local >= ndev:
+        raise SystemExit(f"bench.py: {world} ranks, {ndev} device{'' if ndev == 1 else 's'} visible: "
+                         f"LOCAL_RANK {local} has no GPU of its own")
+    torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def main():
+    args = parse()
+    if args.workload == "c3":
+        return main_c3(args)
+    world, rank, device = rank_device(args)
     # OKM_BENCH_EXCHANGE=1 runs the N>1 exchange + merge path at world size 1
     # too (torchrun --nproc-per-node 1): its cost on one GPU, RCCL self-send
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
@@ -368,7 +400,7 @@ def main():
                    "k": K, "reads_per_gpu": args.reads, "read_len": READ_LEN, "genome_bp": GENOME_BP,
                    "distinct_kmers": int(info["distinct"]) if world == 1 else None,
                    "kmer_instances_per_gpu": int(kmers), "parallelism": f"reads sharded x{world}",
-                   "batches_in_flight": 2 if dist_on else S},
+                   "batches_in_flight": len(pipe.local) if dist_on else S},
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_mt": cpu_mt,
@@ -411,11 +443,7 @@ def main_c3(args):
     they pass 8 % of HBM into sorted tables merged k-way, so memory grows with distinct keys), then at N>1
     the tables merge by key-range owner over RCCL.  Strong scaling: the total
     work is fixed, `value` = all ranks' bases / the slowest rank's time."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(device)
+    world, rank, device = rank_device(args)
     dist_on = world > 1 or os.environ.get("OKM_BENCH_EXCHANGE") == "1"
     comm = init_comm(world, rank, device) if dist_on else None
     out = c3_run(args, world, rank, device, comm, dist_on, args.steps, args.warmup, baselines=True)

@@ -114,13 +114,21 @@ okm_status okm_group_create(okm_group **out, uint8_t k, okm_mode mode, int n_gpu
     const int n = n_gpus <= 0 ? avail : n_gpus;
     if (n > avail)
         return okm::fail(OKM_E_ARG, "okm_group_create: " + std::to_string(n) + " GPUs asked, " + std::to_string(avail) +
-                                        " visible");
+                                        " visible (one context per GPU)");
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+        devs[i] = devices ? devices[i] : i;
+        if (devs[i] < 0 || devs[i] >= avail)
+            return okm::fail(OKM_E_ARG, "okm_group_create: device " + std::to_string(devs[i]) + " of " +
+                                            std::to_string(n) + " GPUs asked, " + std::to_string(avail) + " visible");
+        for (int j = 0; j < i; ++j)
+            if (devs[j] == devs[i])
+                return okm::fail(OKM_E_ARG, "okm_group_create: device " + std::to_string(devs[i]) + " named twice");
+    }
     okm_group *g = new okm_group();
     g->k = k;
     g->mode = mode;
     g->w.resize(n);
-    std::vector<int> devs(n);
-    for (int i = 0; i < n; ++i) devs[i] = devices ? devices[i] : i;
     for (int i = 0; i < n; ++i) {
         okm_status s = okm_create(&g->w[i].ctx, k, mode, devs[i], distinct_hint);
         if (s != OKM_OK) {

@@ -497,11 +497,14 @@ def _table_digest(kp: int, cp: int, n: int, pos0: int, chunk: int = 1 << 26):
     (wrapping), positions counted from pos0: the owners' tables, concatenated
     in rank order, digest like the one-GPU table."""
     import torch
-    from okm import dist as okm_dist
+    tests_dir = os.path.join(ROOT, "tests")
+    if tests_dir not in sys.path:
+        sys.path.insert(0, tests_dir)
+    from dist_rehearsal import DeviceView  # rehearsal-only helper (a torch view of device memory)
     if not n:
         return [0, 0, 0, 0]
-    keys = torch.as_tensor(okm_dist.DeviceView(kp, n), device="cuda")
-    counts = torch.as_tensor(okm_dist.DeviceView(cp, n), device="cuda")
+    keys = torch.as_tensor(DeviceView(kp, n), device="cuda")
+    counts = torch.as_tensor(DeviceView(cp, n), device="cuda")
     d = [n, 0, 0, 0]
     for o in range(0, n, chunk):
         kk, cc = keys[o:o + chunk], counts[o:o + chunk]
