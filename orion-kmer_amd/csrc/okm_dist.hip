@@ -579,7 +579,15 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         const size_t want = std::max<size_t>(bytes + bytes / 8, 4096);
-        HIP_TRY(hipMalloc(&p, want));
+        if (hipMalloc(&p, want) != hipSuccess) {
+            // HBM held by the contexts' cached (idle) arena chunks: give it back, once
+            (void)hipGetLastError();
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            trim_device_pools(dev);
+            p = nullptr;
+            HIP_TRY(hipMalloc(&p, want));
+        }
         cap = want;
         return OKM_OK;
     }
@@ -781,10 +789,12 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     okm_status st = OKM_OK;
     if (!set) st = m->low.ensure(std::max<uint64_t>(n, 16));
     if (deltas && st == OKM_OK) st = m->k5.ensure(5 * std::max<uint64_t>(n, 16));
-    // u64 keys go out of communicator memory (owned_send_buffers): staged below,
+    // u64 keys go out of communicator memory (owned_send_buffers): the slices
+    // that cross the transport (not the borrowed self slice) are staged below,
     // allocated here so that a failure is still reported to the peers
+    const uint64_t n_sent = n - (self_borrow ? skip1 - skip0 : 0);
     if (!deltas && st == OKM_OK && tp.owned_send_buffers())
-        st = m->ksend.ensure(kw * std::max<uint64_t>(n, 16) * sizeof(uint64_t));
+        st = m->ksend.ensure(kw * std::max<uint64_t>(n_sent, 16) * sizeof(uint64_t));
     hs[3 * P] = st != OKM_OK;
     HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), row * sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, 2 * P * sizeof(ull), s));
@@ -896,10 +906,24 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
         if (count) msgs.push_back(Msg{send, (uint8_t *)const_cast<void *>(buf), count, esize, (int)peer});
     };
     uint64_t bytes_out = 0, bytes_in = 0;
-    const uint64_t *ksrc = dk;  // u64 keys: the local table's slices, in place or staged
-    if (!deltas && n && tp.owned_send_buffers()) {
-        HIP_TRY(hipMemcpyAsync(m->ksend.p, dk, kw * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    // u64 keys: the local table's slices in place, or (owned_send_buffers) each
+    // sent slice staged at sst[r] of the communicator's buffer -- only what
+    // crosses the transport: nothing at one rank, (P-1)/P of the table at P
+    std::vector<uint64_t> sst(P, 0);
+    const uint64_t *ksrc = dk;
+    const bool staged = !deltas && tp.owned_send_buffers();
+    if (staged) {
+        uint64_t at = 0;
+        for (uint32_t r = 0; r < P; ++r) {
+            sst[r] = at;
+            if (ss[r])
+                HIP_TRY(hipMemcpyAsync(m->ksend.as<uint64_t>() + kw * at, dk + kw * cut[r], kw * ss[r] * sizeof(uint64_t),
+                                       hipMemcpyDeviceToDevice, s));
+            at += ss[r];
+        }
         ksrc = m->ksend.as<uint64_t>();
+    } else {
+        for (uint32_t r = 0; r < P; ++r) sst[r] = cut[r];
     }
     for (uint32_t r = 0; r < P; ++r) {
         if (deltas) {  // 5 bytes per key + key escapes
@@ -908,7 +932,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
             add(true, m->kesc.as<uint64_t>() + 2 * ksoff[r], 2 * ks[r], 8, r);
             add(false, m->rkesc.as<uint64_t>() + 2 * kroff[r], 2 * kr[r], 8, r);
         } else {
-            add(true, ksrc + kw * cut[r], kw * ss[r], 8, r);
+            add(true, ksrc + kw * sst[r], kw * ss[r], 8, r);
             add(false, m->rk.as<uint64_t>() + kw * roff[r], kw * rs[r], 8, r);
         }
         if (!set) {

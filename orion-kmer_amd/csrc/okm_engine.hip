@@ -400,6 +400,12 @@ struct DevPool {
     }
 };
 
+void trim_device_pools(int device) {
+    std::lock_guard<std::mutex> g(g_pools_mu);
+    for (DevPool *o : g_pools)
+        if (o->device == device) o->trim();
+}
+
 template <typename T>
 static okm_status pool_get(DevPool &pool, size_t n, T **out) {
     void *p = nullptr;

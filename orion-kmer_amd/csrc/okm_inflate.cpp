@@ -517,8 +517,11 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
     {
         const uint8_t *t4 = in + n - 4;  // a single member's ISIZE (mod 2^32) as a size hint
         const size_t isz = t4[0] | (t4[1] << 8) | (t4[2] << 16) | ((size_t)t4[3] << 24);
-        out.reserve(base + std::max(isz, nbytes * 4));
-        huge_pages(out.data() + base, out.capacity() - base);
+        const size_t need = base + std::max(isz, nbytes * 4);
+        if (need > out.capacity()) {  // geometric: a file of many members is not copied once per member
+            out.reserve(std::max(need, 2 * out.capacity()));
+            huge_pages(out.data() + base, out.capacity() - base);
+        }
     }
     std::vector<Piece> pool(R);  // 16-bit piece buffers, reused round to round (their pages stay faulted in)
     uLong crc = crc32(0L, Z_NULL, 0);

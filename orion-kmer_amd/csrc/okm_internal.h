@@ -24,6 +24,9 @@ void host_pinned_free(void *p);
 // Device-to-host copy issued on `device` (this thread's current device is set
 // to it first, so the copy does not queue behind device 0's null stream).
 okm_status memcpy_d2h_on(int device, void *dst, const void *src, size_t bytes);
+// Give back the idle device memory every context's pool on `device` caches
+// (a hipMalloc outside the pools, e.g. a communicator buffer, retries after it).
+void trim_device_pools(int device);
 
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);

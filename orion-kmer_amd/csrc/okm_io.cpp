@@ -257,9 +257,15 @@ static okm_status gunzip_libdeflate(Deflate *D, const uint8_t *in, size_t n, Byt
     out.clear();
     size_t pos = 0;
     okm_status st = OKM_OK;
+    // the parallel inflater cuts the rest of the FILE into chunks: once a member
+    // ends within the first half of what was left (many concatenated members),
+    // the remaining members are inflated one by one instead
+    bool par = true;
     while (pos < n) {
-        if (member_parallel(in, n, pos, out, st)) {
+        const size_t pos0 = pos;
+        if (par && member_parallel(in, n, pos, out, st)) {
             if (st != OKM_OK) break;
+            if (2 * (pos - pos0) < n - pos0) par = false;
             size_t p = pos;  // trailing zero padding after the last member is tolerated
             while (p < n && in[p] == 0) ++p;
             if (p == n) break;
@@ -990,7 +996,10 @@ okm_status write_counts_tsv_chunks(const char *path, uint8_t k, uint64_t min_cou
                     const uint64_t a = b * step, m = std::min<uint64_t>(step, n - a);
                     format_filtered(k, keys + a * kw, counts + a, m, min_count, buf, fk, fc);
                     cnt[b] = (uint64_t)std::count(buf.begin(), buf.end(), '\n');
-                    if (OutWriter::gzip_member(comp, (const uint8_t *)buf.data(), buf.size(), mem[b]) != OKM_OK) {
+                    // a block min_count filtered to nothing adds no member (as write_blocks);
+                    // close() still writes the one empty member of an empty output
+                    if (!buf.empty() &&
+                        OutWriter::gzip_member(comp, (const uint8_t *)buf.data(), buf.size(), mem[b]) != OKM_OK) {
                         cbad = 1;
                         break;
                     }
