@@ -263,8 +263,8 @@ okm_status okm_comm_init_all(okm_comm **out, int n, const int *devices);
 /* n virtual ranks in THIS process on ONE device, without RCCL: the same owner
  * plan, pack / widen / escape kernels, message pieces and owner merge as an
  * RCCL communicator, with every collective done by device copies between the
- * ranks' buffers (host threads meet at a barrier; a rank missing for
- * OKM_LOOPBACK_TIMEOUT_S seconds, default 300, aborts it).  RCCL refuses two
+ * ranks' buffers (host threads meet at a barrier; a rank missing for 300 s
+ * aborts it).  RCCL refuses two
  * ranks on one GPU: this is how the P > 1 merge runs on one device (tests,
  * rehearsals).  out has n entries; each rank's okm_merge_owned runs on a host
  * thread of its own. */
@@ -359,9 +359,13 @@ typedef struct okm_engine_info {
     uint32_t levels;         /* partition passes over keys */
     uint32_t work_items;     /* partitions counted in LDS */
     uint64_t max_partition;  /* largest partition (instances) */
-    uint64_t device_bytes;   /* device memory held */
+    uint64_t device_bytes;   /* device memory held (mapped, including idle cached chunks) */
     uint32_t groups;         /* key-range groups counted one after the other (0/1 = one) */
     uint32_t folds;          /* times the uncounted batches were folded into a sorted table */
+    uint64_t device_peak_bytes;  /* high-water mark of live device allocations since okm_create / okm_reset */
+    uint64_t host_bytes;     /* sorted tables this context keeps in host memory (moved off a full device) */
+    uint32_t spills;         /* tables moved to host memory since okm_create / okm_reset */
+    uint32_t pad;
 } okm_engine_info;
 okm_status okm_engine_info_get(okm_ctx *ctx, okm_engine_info *info);
 

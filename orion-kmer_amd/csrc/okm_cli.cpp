@@ -25,9 +25,12 @@
 
 static int g_verbose = 0;
 
-// OKM_CLI_TIMES=1: wall time of each phase of a run on stderr (tools/e2e_cli.sh)
+// OKM_PROFILE_HOST=1: wall time of each phase of a run on stderr (tools/e2e_cli.sh)
 static void phase(const char *what) {
-    static const bool on = getenv("OKM_CLI_TIMES") != nullptr;
+    static const bool on = [] {
+        const char *e = getenv("OKM_PROFILE_HOST");
+        return e && *e && *e != '0';
+    }();
     if (!on) return;
     static struct timespec t0 = [] {
         struct timespec t;

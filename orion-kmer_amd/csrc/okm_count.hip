@@ -32,48 +32,12 @@
 
 namespace okm {
 
-#ifndef OKM_COUNT_WPE
-#define OKM_COUNT_WPE 8  // waves per EU floor of the unweighted kernel: 4 blocks/CU (64 VGPRs)
-#endif
-#ifndef OKM_COUNT_PREFETCH  // full/dense kernel: load the next item's keys during this one
-#define OKM_COUNT_PREFETCH 0  // measured slower on K128: the extra registers spill (k=63: 22.2 vs 17.2 ms)
-#endif
-#ifndef OKM_COUNT_PROF
-#define OKM_COUNT_PROF 0
-#endif
-#ifndef OKM_COUNT_DESC_PF  // tag kernel: load the next item's descriptor while this item is counted
-#define OKM_COUNT_DESC_PF 0
-#endif
-#ifndef OKM_COUNT_LATE_RESET  // tag mode: per-home state reset inside the item's own phases, no trailing barriers
-#define OKM_COUNT_LATE_RESET 1
-#endif
-#ifndef OKM_FULL_RANK  // full mode: rank inside the home (1) or insertion-sort each thread's slice (0)
-#define OKM_FULL_RANK 1
-#endif
-#ifndef OKM_FULL_HB_W  // full mode, K128 keys: home bits (12: 4096 homes, ~1 key each at 4096 instances)
-#define OKM_FULL_HB_W 12
-#endif
-#ifndef OKM_FULL_FLAG_ROWS  // full mode: run-start flags from lane-contiguous rows + ballots (1)
-#define OKM_FULL_FLAG_ROWS 1
-#endif
-// OKM_COUNT_PROF=1 builds: thread 0 of every block accumulates clock64()
-// deltas between phase marks (debug/tuning only; okm_debug_count_prof()).
-__device__ unsigned long long g_count_prof[16];
-__shared__ unsigned long long g_prof_last;
-#define PMARK(i)                                                        \
-    do {                                                                \
-        if (OKM_COUNT_PROF && threadIdx.x == 0) {                       \
-            const unsigned long long now_ = clock64();                  \
-            atomicAdd(&g_count_prof[i], now_ - g_prof_last);            \
-            g_prof_last = now_;                                         \
-        }                                                               \
-    } while (0)
+constexpr int kCountWpe = 8;  // waves per EU floor of the unweighted tag kernel: 4 blocks/CU (64 VGPRs)
+constexpr int kFullHomeBitsW = 12;  // full mode, K128 keys: 4096 homes (~1 key each at 4096 instances)
 
-#ifndef OKM_COUNT_CB  // threads per counting workgroup (512: 4096-instance items; 256: 2048)
-#define OKM_COUNT_CB 512
-#endif
-constexpr int kCB = OKM_COUNT_CB;         // threads per workgroup
-static_assert(kCB == 512 || kCB == 256, "four homes per thread at 2048 / 1024 homes");
+// Threads per counting workgroup: 512, 4096-instance items (256 threads and
+// 1024 homes measured count -9 % but partition +8 %, profiles/AB_LOG.md)
+constexpr int kCB = 512;
 constexpr int kPer = 8;                   // instances per thread (tag / full modes)
 constexpr int kCapI = kCB * kPer;         // instances per tag/full-mode item (4096)
 constexpr int kHomeBits = kCB == 512 ? 11 : 10;
@@ -253,7 +217,7 @@ __device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *
                                                uint32_t *coff) {
     const uint32_t t = threadIdx.x;
     const uint32_t R = __builtin_amdgcn_readfirstlane(it.seg_count);
-    if (OKM_COUNT_LATE_RESET) lds_sync();  // the previous tag item's last step may still read the rest buffer
+    lds_sync();  // the previous tag item's last step may still read the rest buffer
     if (t < R) {
         const DevSeg s = segs[it.seg_begin + t];
         ck[t] = s.keys;
@@ -281,23 +245,6 @@ __device__ __forceinline__ void load_item_segs(const DevItem &it, const DevSeg *
             kk[u] = gload(reinterpret_cast<const KT *>(ck[lo]) + p);
             if (W && cc[lo]) ww[u] = gload(cc[lo] + p);
         }
-    }
-}
-
-// Insertion sort of sk[a, a + n) (+ weights), n small.
-template <bool W, typename KT>
-__device__ __forceinline__ void slice_sort(KT *sk, ull *sw, uint32_t a, uint32_t n) {
-    for (uint32_t i = a + 1; i < a + n; ++i) {
-        const KT x = sk[i];
-        const ull xw = W ? sw[i] : 0ull;
-        uint32_t j = i;
-        while (j > a && KeyOps<KT>::lt(x, sk[j - 1])) {
-            sk[j] = sk[j - 1];
-            if (W) sw[j] = sw[j - 1];
-            --j;
-        }
-        sk[j] = x;
-        if (W) sw[j] = xw;
     }
 }
 
@@ -377,7 +324,6 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         }
     }
     lds_sync();
-    PMARK(11);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         if ((uint32_t)u >= nrows) break;
@@ -389,96 +335,60 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         }
     }
     lds_sync();
-    PMARK(12);
     uint32_t m = 0;  // run-start flags of positions p0 .. p0 + 7 (p0 = 8t)
     constexpr int kPerT = kCapI / kCB;  // 8 positions per thread
     static_assert(kPerT == 8, "8 flag bits per thread");
     const uint32_t p0 = t * kPerT;
-    if (OKM_FULL_RANK) {
-        // every instance ranks itself inside its home (keys below it, and equal
-        // keys at earlier positions) and moves there: homes are key ranges in
-        // order, so this sorts the item; loops run over one home's keys (~2 at
-        // k=63, whose keys are ~98 % distinct) instead of a thread's whole slice
-        uint32_t dst[kPer];
+    // every instance ranks itself inside its home (keys below it, and equal
+    // keys at earlier positions) and moves there: homes are key ranges in
+    // order, so this sorts the item; loops run over one home's keys (~2 at
+    // k=63, whose keys are ~98 % distinct) instead of a thread's whole slice
+    uint32_t dst[kPer];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            dst[u] = ~0u;
-            if ((uint32_t)u >= nrows) break;
-            if (!KeyOps<KT>::is_empty(kk[u])) {
-                const uint32_t h = hp[u] >> 16;
-                const uint32_t hs = half_of(hc[h >> 1], h);
-                const uint32_t he = h + 1 < kH ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
-                const uint32_t me = hs + (hp[u] & 0xFFFFu);
-                uint32_t rank = hs;
-                for (uint32_t q = hs; q < he; ++q) {
-                    const KT y = sk[q];
-                    rank += (KeyOps<KT>::lt(y, kk[u]) || (q < me && KeyOps<KT>::eq(y, kk[u]))) ? 1u : 0u;
-                }
-                dst[u] = rank;
+    for (int u = 0; u < kPer; ++u) {
+        dst[u] = ~0u;
+        if ((uint32_t)u >= nrows) break;
+        if (!KeyOps<KT>::is_empty(kk[u])) {
+            const uint32_t h = hp[u] >> 16;
+            const uint32_t hs = half_of(hc[h >> 1], h);
+            const uint32_t he = h + 1 < kH ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
+            const uint32_t me = hs + (hp[u] & 0xFFFFu);
+            uint32_t rank = hs;
+            for (uint32_t q = hs; q < he; ++q) {
+                const KT y = sk[q];
+                rank += (KeyOps<KT>::lt(y, kk[u]) || (q < me && KeyOps<KT>::eq(y, kk[u]))) ? 1u : 0u;
             }
+            dst[u] = rank;
         }
-        lds_sync();  // every read of the home-ordered keys is done
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            if ((uint32_t)u >= nrows) break;
-            if (dst[u] != ~0u) {
-                sk[dst[u]] = kk[u];
-                if (W) sw[dst[u]] = ww[u];
-            }
-        }
-        lds_sync();
-        PMARK(13);
-        // count.rs:33: a key's count = its run's length (weight); flag run starts.
-        // The flags are taken in rows of lane-contiguous positions (conflict-free
-        // LDS reads; a thread's own 8 consecutive keys sit 128 B apart from its
-        // neighbours' and read 8-way bank-conflicted as K128) into one ballot
-        // word per wave and row, in the dead home counters
-        if (OKM_FULL_FLAG_ROWS) {
-            uint64_t *fm = reinterpret_cast<uint64_t *>(hc);  // [kCapI / 64] run-start masks
-            static_assert(kCapI / 64 * 8 <= (int)kH * 2, "run-start masks fit the home counters");
-#pragma unroll
-            for (int i = 0; i < kPer; ++i) {
-                const uint32_t p = (uint32_t)i * kCB + t;
-                bool f = false;
-                if (p < ntot) f = p == 0 || !KeyOps<KT>::eq(sk[p], sk[p - 1]);
-                const uint64_t b = __ballot(f);
-                if ((t & 63u) == 0) fm[(uint32_t)i * (kCB / 64) + (t >> 6)] = b;
-            }
-            lds_sync();
-            const uint32_t r = p0 % kCB;
-            m = (uint32_t)(fm[(p0 / kCB) * (kCB / 64) + r / 64] >> (r % 64)) & 0xFFu;
-        } else {
-            KT prev = p0 > 0 && p0 <= ntot ? sk[p0 - 1] : KeyOps<KT>::empty();
-#pragma unroll
-            for (int j = 0; j < kPerT; ++j) {
-                if (p0 + j >= ntot) break;
-                const KT x = sk[p0 + j];
-                m |= KeyOps<KT>::eq(x, prev) ? 0u : 1u << j;
-                prev = x;
-            }
-        }
-    } else {
-        // each thread's 4 homes are one slice of sk: sort it and flag the first
-        // key of every run (count.rs:33: a key's count = its run's length/weight);
-        // the flags of the dead home counters' bytes (hc) are then compacted into
-        // run starts by the whole block, so the emit below is coalesced
-        slice_sort<W>(sk, sw, a, n);
-        PMARK(13);
-        uint8_t *rf = reinterpret_cast<uint8_t *>(hc);  // [kCapI] run-start flags
-        {
-            KT prev = KeyOps<KT>::empty();
-            for (uint32_t i = a; i < a + n; ++i) {
-                const KT x = sk[i];
-                rf[i] = KeyOps<KT>::eq(x, prev) ? 0 : 1;
-                prev = x;
-            }
-        }
-        lds_sync();
-        const uint32_t *rw = reinterpret_cast<const uint32_t *>(rf);
-        const uint64_t fw = (uint64_t)rw[2 * t] | ((uint64_t)rw[2 * t + 1] << 32);
-#pragma unroll
-        for (int j = 0; j < kPerT; ++j) m |= ((fw >> (8 * j)) & 1u) && p0 + j < ntot ? 1u << j : 0u;
     }
+    lds_sync();  // every read of the home-ordered keys is done
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if ((uint32_t)u >= nrows) break;
+        if (dst[u] != ~0u) {
+            sk[dst[u]] = kk[u];
+            if (W) sw[dst[u]] = ww[u];
+        }
+    }
+    lds_sync();
+    // count.rs:33: a key's count = its run's length (weight); flag run starts.
+    // The flags are taken in rows of lane-contiguous positions (conflict-free
+    // LDS reads; a thread's own 8 consecutive keys sit 128 B apart from its
+    // neighbours' and read 8-way bank-conflicted as K128) into one ballot
+    // word per wave and row, in the dead home counters
+    uint64_t *fm = reinterpret_cast<uint64_t *>(hc);  // [kCapI / 64] run-start masks
+    static_assert(kCapI / 64 * 8 <= (int)kH * 2, "run-start masks fit the home counters");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const uint32_t p = (uint32_t)i * kCB + t;
+        bool f = false;
+        if (p < ntot) f = p == 0 || !KeyOps<KT>::eq(sk[p], sk[p - 1]);
+        const uint64_t b = __ballot(f);
+        if ((t & 63u) == 0) fm[(uint32_t)i * (kCB / 64) + (t >> 6)] = b;
+    }
+    lds_sync();
+    const uint32_t rp = p0 % kCB;
+    m = (uint32_t)(fm[(p0 / kCB) * (kCB / 64) + rp / 64] >> (rp % 64)) & 0xFFu;
     uint32_t D;
     {
         uint32_t q = block_excl_scan32((uint32_t)__builtin_popcount(m), wsum, &D);
@@ -488,7 +398,6 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         if (t == 0) first[D] = (uint16_t)ntot;  // ntot <= kCapI fits u16
     }
     lds_sync();
-    PMARK(14);
     for (uint32_t p = t; p < (nowrite ? 0u : D); p += kCB) {
         const uint32_t b = first[p], e = first[p + 1];
         out_keys[out_off + p] = sk[b];
@@ -499,7 +408,6 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             c = e - b;
         store_count<W>(out_counts, out_off + p, c);
     }
-    PMARK(15);
     return __builtin_amdgcn_readfirstlane(D);
 }
 
@@ -553,11 +461,10 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         }
     }
     lds_sync();
-    PMARK(2);
     // 2. rest offsets: thread t owns homes [4t, 4t+4) = words 2t, 2t+1
     //    (late reset: the previous item's home offsets, read by its last step
     //    before this item's first barrier, are cleared here)
-    if (OKM_COUNT_LATE_RESET) hd[2 * t] = hd[2 * t + 1] = 0;
+    hd[2 * t] = hd[2 * t + 1] = 0;
     {
         const uint32_t w0 = rc[2 * t], w1 = rc[2 * t + 1];
         const uint32_t c0 = w0 & 0xFFFFu, c1 = w0 >> 16, c2 = w1 & 0xFFFFu;
@@ -572,7 +479,6 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         if (t == 0) wsum[kCB / 64] = rtot;  // rest total, read by every rest position below
     }
     lds_sync();
-    PMARK(3);
     // 3. scatter rest instances into home order
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -585,7 +491,6 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         }
     }
     lds_sync();
-    PMARK(4);
     // 4. rest positions, one per lane: count, first occurrence in the home's
     //    run, and what the home's distinct count / tag rank must include
     const uint32_t rtot = __builtin_amdgcn_readfirstlane(wsum[kCB / 64]);
@@ -623,7 +528,6 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         }
     }
     lds_sync();
-    PMARK(5);
     // 5. output offsets per home: [tag] + rest distinct keys
     ull tg[kHomesPer];
     uint32_t ho[kHomesPer];
@@ -631,24 +535,21 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
     // late reset: this thread's homes are read here for the last time (step 4,
     // the last reader of other threads' tags and rest offsets, is behind the
     // barrier above), so they are cleared at once for the next item
-    uint32_t lw0 = 0, lw1 = 0, nw0 = 0, nw1 = 0;  // rest keys below the tag; tag counts (u16 pairs)
-    ull tw[W ? kHomesPer : 1];                     // tag weights (weighted launches)
-    if (OKM_COUNT_LATE_RESET) {
-        lw0 = lt[2 * t];
-        lw1 = lt[2 * t + 1];
-        lt[2 * t] = lt[2 * t + 1] = 0;
-        rc[2 * t] = rc[2 * t + 1] = 0;
-        if (W) {
+    uint32_t nw0 = 0, nw1 = 0;  // tag counts (u16 pairs)
+    ull tw[W ? kHomesPer : 1];   // tag weights (weighted launches)
+    const uint32_t lw0 = lt[2 * t], lw1 = lt[2 * t + 1];  // rest keys below the tag
+    lt[2 * t] = lt[2 * t + 1] = 0;
+    rc[2 * t] = rc[2 * t + 1] = 0;
+    if (W) {
 #pragma unroll
-            for (int q = 0; q < kHomesPer; ++q) {
-                tw[q] = tc64[kHomesPer * t + q];
-                tc64[kHomesPer * t + q] = 0;
-            }
-        } else {
-            nw0 = tc16[2 * t];
-            nw1 = tc16[2 * t + 1];
-            tc16[2 * t] = tc16[2 * t + 1] = 0;
+        for (int q = 0; q < kHomesPer; ++q) {
+            tw[q] = tc64[kHomesPer * t + q];
+            tc64[kHomesPer * t + q] = 0;
         }
+    } else {
+        nw0 = tc16[2 * t];
+        nw1 = tc16[2 * t + 1];
+        tc16[2 * t] = tc16[2 * t + 1] = 0;
     }
     {
         const uint32_t w0 = hd[2 * t], w1 = hd[2 * t + 1];
@@ -657,7 +558,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 #pragma unroll
         for (int q = 0; q < kHomesPer; ++q) {
             tg[q] = tag[kHomesPer * t + q];
-            if (OKM_COUNT_LATE_RESET) tag[kHomesPer * t + q] = kEmptyKey;
+            tag[kHomesPer * t + q] = kEmptyKey;
             dq[q] += tg[q] != kEmptyKey;
             ho[q] = d;
             d += dq[q];
@@ -669,27 +570,22 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         hd[2 * t + 1] = ho[2] | (ho[3] << 16);
     }
     lds_sync();
-    PMARK(6);
     // 6a. tags: rank = home offset + rest distinct keys below the tag
     {
-        const uint32_t l0 = OKM_COUNT_LATE_RESET ? lw0 : lt[2 * t], l1 = OKM_COUNT_LATE_RESET ? lw1 : lt[2 * t + 1];
-        const uint32_t lq[kHomesPer] = {l0 & 0xFFFFu, l0 >> 16, l1 & 0xFFFFu, l1 >> 16};
+        const uint32_t lq[kHomesPer] = {lw0 & 0xFFFFu, lw0 >> 16, lw1 & 0xFFFFu, lw1 >> 16};
         uint32_t nq[kHomesPer];
         if (!W) {
-            const uint32_t n0 = OKM_COUNT_LATE_RESET ? nw0 : tc16[2 * t];
-            const uint32_t n1 = OKM_COUNT_LATE_RESET ? nw1 : tc16[2 * t + 1];
-            nq[0] = n0 & 0xFFFFu;
-            nq[1] = n0 >> 16;
-            nq[2] = n1 & 0xFFFFu;
-            nq[3] = n1 >> 16;
+            nq[0] = nw0 & 0xFFFFu;
+            nq[1] = nw0 >> 16;
+            nq[2] = nw1 & 0xFFFFu;
+            nq[3] = nw1 >> 16;
         }
 #pragma unroll
         for (int q = 0; q < kHomesPer; ++q) {
             if (!NW && tg[q] != kEmptyKey) {
                 const uint64_t o = out_off + ho[q] + lq[q];
                 out_keys[o] = tg[q];
-                const uint64_t cq = W ? (OKM_COUNT_LATE_RESET ? (uint64_t)tw[q] : (uint64_t)tc64[kHomesPer * t + q])
-                                      : (uint64_t)nq[q];
+                const uint64_t cq = W ? (uint64_t)tw[q] : (uint64_t)nq[q];
                 store_count<W>(out_counts, o, cq);
             }
         }
@@ -704,33 +600,16 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             uint32_t less = 0;
             for (uint32_t q = hs; q < he; ++q) less += (rf[q] && rk[q] < x) ? 1u : 0u;
             const uint32_t h = home_of(x, r);
-            const uint32_t tag_below = OKM_COUNT_LATE_RESET ? prange[k] >> 31 : (tag[h] < x ? 1u : 0u);
+            const uint32_t tag_below = prange[k] >> 31;
             const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + tag_below;
             out_keys[o] = x;
             store_count<W>(out_counts, o, (uint64_t)pc[k]);
         }
     }
-    PMARK(7);
     // late reset: everything but the home offsets (hd, cleared in the next
     // item's step 2) was cleared in step 5, and nothing read here is written
     // before the next item's first barrier: no trailing barriers, the next
     // item's loads overlap this step
-    if (OKM_COUNT_LATE_RESET) return __builtin_amdgcn_readfirstlane(D);
-    // reset this thread's homes for the next item once every reader is done
-    lds_sync();
-#pragma unroll
-    for (int q = 0; q < kHomesPer; ++q) {
-        tag[kHomesPer * t + q] = kEmptyKey;
-        if (W) tc64[kHomesPer * t + q] = 0;
-    }
-    if (!W) {
-        tc16[2 * t] = 0;
-        tc16[2 * t + 1] = 0;
-    }
-    rc[2 * t] = rc[2 * t + 1] = 0;
-    hd[2 * t] = hd[2 * t + 1] = 0;
-    lt[2 * t] = lt[2 * t + 1] = 0;
-    lds_sync();
     return __builtin_amdgcn_readfirstlane(D);
 }
 
@@ -800,20 +679,14 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
 // NW (weighted launches only): count each item's distinct keys into n_out and
 // write nothing -- the first pass of an exact-size two-pass count.
 template <bool W, bool NW = false>
-__global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : OKM_COUNT_WPE)))
+__global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : kCountWpe)))
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                    ull *__restrict__ ctl, uint32_t *__restrict__ defer, const ull *__restrict__ guard,
-                   const ull *__restrict__ d_nitems, uint32_t chunked) {
+                   const ull *__restrict__ d_nitems) {
     if (guard && (guard[0] | guard[1])) return;  // speculative launch whose items were not valid
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
-    // items dealt by stride (item = block + k * grid), or (chunked) as one
-    // contiguous range per block: neighbouring items, whose keys and output
-    // slots share lines at their boundaries, then run on one CU in turn
-    const uint32_t per = chunked ? (nitems + gridDim.x - 1) / gridDim.x : 1u;
-    const uint32_t ibeg = chunked ? blockIdx.x * per : blockIdx.x;
-    const uint32_t iend = chunked ? min(nitems, ibeg + per) : nitems;
-    const uint32_t istep = chunked ? 1u : gridDim.x;
+    // items dealt by stride (item = block + k * grid)
     __shared__ __attribute__((aligned(16))) ull lds[Lds<W>::kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     // multi-segment items: their descriptors are staged in the rest buffer,
@@ -824,15 +697,10 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
     static_assert(kSegCache * 20 + 4 <= Lds<W>::kRest * 8, "segment cache fits the rest buffer");
     const uint32_t t = threadIdx.x;
     tag_reset<W>(lds);
-    if (OKM_COUNT_PROF && t == 0) g_prof_last = clock64();
     // Block-uniform values that steer code containing barriers come from
     // blockIdx / scalar loads (see DESIGN.md on the structuriser).
-    DevItem nxt{};
-    if (OKM_COUNT_DESC_PF && ibeg < iend) nxt = items[ibeg];
-    for (uint32_t item = ibeg; item < iend; item += istep) {
-        PMARK(0);
-        const DevItem it = OKM_COUNT_DESC_PF ? nxt : items[item];
-        if (OKM_COUNT_DESC_PF && item + istep < iend) nxt = items[item + istep];
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const DevItem it = items[item];
         const uint64_t total = it.pad == kItemEmpty ? 0 : item_total(it, segs);
         if (total == 0) {  // an empty fan-out slot (block-uniform)
             if (t == 0) n_out[item] = 0;
@@ -848,7 +716,6 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
                 load_item_segs<W>(it, segs, kk, ww, seg_k, seg_c, seg_off);
             else
                 load_item<W>(it, segs, kk, ww);
-            PMARK(1);
             const uint32_t nrows = (uint32_t)((total + kCB - 1) / kCB);  // rows of kk in use (block-uniform)
             written = tag_item<W, NW>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);
         }
@@ -858,7 +725,6 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
             else
                 n_out[item] = written;
         }
-        PMARK(9);
     }
 }
 
@@ -875,63 +741,30 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
                                                     bool nowrite) {
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
-    constexpr int kHB = sizeof(KT) > 8 ? OKM_FULL_HB_W : kHomeBits;  // full-mode home bits
+    constexpr int kHB = sizeof(KT) > 8 ? kFullHomeBitsW : kHomeBits;  // full-mode home bits
     // full_item shifts a key by rem_bits - kHB with rem_bits > kDenseBits: the
     // shift stays non-negative only while kHB <= kDenseBits + 1
-    static_assert(kHB <= kDenseBits + 1, "full-mode home bits exceed kDenseBits + 1 (OKM_FULL_HB_W vs OKM_COUNT_CB)");
+    static_assert(kHB <= kDenseBits + 1, "full-mode home bits exceed kDenseBits + 1");
     constexpr int kFull = full_lds_bytes<W, KT, kHB>();
     constexpr int kDense = kHomes * ((int)sizeof(KT) + (W ? 8 : 4));
     constexpr int kBytes = kFull > kDense ? kFull : kDense;
     __shared__ __attribute__((aligned(16))) ull lds[kBytes / 8];
     __shared__ uint32_t wsum[kCB / 64 + 1];
     const uint32_t ndefer = defer ? *reinterpret_cast<volatile const unsigned int *>(ctl + 1) : nitems;
-    if (OKM_COUNT_PROF && threadIdx.x == 0) g_prof_last = clock64();
-    // Unweighted: the next item's keys are loaded while this one is counted
-    // (the kernel is LDS-bound to 2 workgroups per CU, so the registers are
-    // free); weighted items load in place.
-    constexpr bool kPre = !W && OKM_COUNT_PREFETCH;
     struct Next {
         uint32_t item;
         DevItem it;
         uint64_t total;
     };
-    auto fetch_meta = [&](uint32_t jj, Next &nx) {
-        nx.item = defer ? defer[jj] : jj;
-        nx.it = items[nx.item];
-        nx.total = nx.it.pad == kItemEmpty ? 0 : item_total(nx.it, segs);
-    };
-    auto is_full = [](const Next &nx) {
-        return nx.total != 0 && nx.it.rem_bits > (uint32_t)kDenseBits && nx.total <= (uint64_t)kCapI;
-    };
-    KT kn[kPer];
-    ull wn[kPer];
-    Next nx{};
-    uint32_t j = blockIdx.x;
-    if (kPre && j < ndefer) {
-        fetch_meta(j, nx);
-        if (is_full(nx)) load_item<W, KT>(nx.it, segs, kn, wn);
-    }
-    for (; j < ndefer; j += gridDim.x) {
+    for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
         Next cur;
+        cur.item = defer ? defer[j] : j;
+        cur.it = items[cur.item];
+        cur.total = cur.it.pad == kItemEmpty ? 0 : item_total(cur.it, segs);
         KT kk[kPer];
         ull ww[kPer];
-        if (kPre) {
-            cur = nx;
-#pragma unroll
-            for (int u = 0; u < kPer; ++u) {
-                kk[u] = kn[u];
-                ww[u] = 1;
-            }
-            const uint32_t jn = j + gridDim.x;
-            if (jn < ndefer) {
-                fetch_meta(jn, nx);
-                if (is_full(nx)) load_item<W, KT>(nx.it, segs, kn, wn);
-            }
-        } else {
-            fetch_meta(j, cur);
-            if (is_full(cur)) load_item<W, KT>(cur.it, segs, kk, ww);
-        }
-        PMARK(10);
+        if (cur.total != 0 && cur.it.rem_bits > (uint32_t)kDenseBits && cur.total <= (uint64_t)kCapI)
+            load_item<W, KT>(cur.it, segs, kk, ww);
         const uint32_t item = cur.item;
         const DevItem it = cur.it;
         const uint64_t total = cur.total;
@@ -953,13 +786,6 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
     }
 }
 
-// Phase cycle totals of an OKM_COUNT_PROF build (zeroes them).
-void count_prof_read(unsigned long long *out16) {
-    (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_count_prof), 16 * sizeof(unsigned long long));
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_count_prof), z, sizeof(z));
-}
-
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
@@ -969,14 +795,7 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
     // wide (full-mode) count: 8191 workgroups against 4095, k=63 at 1 Gbases
     // count_items 8.61-8.62 vs 8.75-8.78 ms over 3 interleaved runs (16383: 8.60-8.65);
     // the weighted tag kernel (C3's merges) showed no difference at 1023 / 16383
-    static const uint32_t wide_cap = [] {  // OKM_COUNT_WIDE_GRID: A/B runs
-        const char *e = getenv("OKM_COUNT_WIDE_GRID");
-        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 8191u;
-    }();
-    static const uint32_t weighted_cap = [] {  // OKM_COUNT_W_GRID: A/B runs
-        const char *e = getenv("OKM_COUNT_W_GRID");
-        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4095u;
-    }();
+    constexpr uint32_t wide_cap = 8191, weighted_cap = 4095;
     if (wide) {  // every item through the full / dense modes
         const uint32_t grid = nitems < wide_cap ? nitems : wide_cap;  // odd: fan-out slots spread over blocks
         if (weighted)
@@ -987,35 +806,27 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                                out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
         return;
     }
-    // OKM_COUNT_GRID: workgroups of the unweighted tag kernel (odd, so fan-out
-    // slots spread over blocks).  16383 (~11 C2 items each, 16 generations of
-    // the 1024 resident workgroups) against 4095: count_items 1.550 vs 1.590-1.600
-    // ms; 2047 1.653, 8191 1.568, 32767 1.563, 65535 1.589, one per item 1.802
-    // (profiles/r04_ab_count_grid.txt).  OKM_COUNT_CHUNKED=1: contiguous item
-    // ranges per workgroup instead of a stride (slower: 1.63 ms at 4095).
-    static const uint32_t grid_env = [] {
-        const char *e = getenv("OKM_COUNT_GRID");
-        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 16383u;
-    }();
-    static const uint32_t chunked = [] {
-        const char *e = getenv("OKM_COUNT_CHUNKED");
-        return e && *e == '1' ? 1u : 0u;
-    }();
-    const uint32_t grid = nitems < grid_env ? nitems : grid_env;
+    // workgroups of the unweighted tag kernel (odd, so fan-out slots spread
+    // over blocks).  16383 (~11 C2 items each, 16 generations of the 1024
+    // resident workgroups) against 4095: count_items 1.550 vs 1.590-1.600 ms;
+    // 2047 1.653, 8191 1.568, 32767 1.563, 65535 1.589, one per item 1.802
+    // (profiles/r04_ab_count_grid.txt)
+    constexpr uint32_t grid_cap = 16383;
+    const uint32_t grid = nitems < grid_cap ? nitems : grid_cap;
     const uint32_t wgrid = nitems < weighted_cap ? nitems : weighted_cap;  // weighted: one workgroup per CU resident
     const uint32_t sgrid = nitems < 1023u ? nitems : 1023u;  // exits at once when nothing was deferred
     if (weighted) {
         if (nowrite)
             hipLaunchKernelGGL((k_count_items<true, true>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
         else
             hipLaunchKernelGGL((k_count_items<true, false>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
+                               out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, defer, guard, d_nitems, chunked);
+                           out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
     }

@@ -10,24 +10,12 @@ namespace okm {
 
 typedef unsigned long long ull;
 
-#ifndef OKM_LDS_BARRIER
-#define OKM_LDS_BARRIER 0
-#endif
-// The streaming kernels' barriers.  OKM_LDS_BARRIER=1: a barrier that orders
-// LDS only (__syncthreads() also waits for every global load and store the
-// wave has in flight); every such barrier protects LDS (staging, histograms,
-// scans) and the global traffic is per-thread.  Measured on C2, 6 interleaved
-// pairs: the kernels within 1-2 % either way and the three-stream step 3 %
-// slower (5.69 vs 5.52 ms), so plain __syncthreads() stays the default.
-__device__ __forceinline__ void lds_sync() {
-#if OKM_LDS_BARRIER
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#else
-    __syncthreads();
-#endif
-}
+// The streaming kernels' barriers: plain __syncthreads().  (A barrier that
+// orders LDS only -- a workgroup fence on the local address space + s_barrier,
+// so global loads and stores stay in flight across it -- measured the kernels
+// within 1-2 % either way and the three-stream step 3 % slower, 5.69 vs 5.52
+// ms on C2: profiles/AB_LOG.md.)
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
 
 // A load through a pointer the kernel read from a descriptor (DevSeg /
 // DevItem keys and counts): the compiler cannot prove such a pointer global

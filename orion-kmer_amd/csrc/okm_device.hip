@@ -19,12 +19,6 @@ constexpr uint64_t kScanTile = (uint64_t)kScanBlock * kScanPer;
 // list and the larger ones from the back.
 constexpr uint64_t kFanSmallJob = 16384;
 
-#ifndef OKM_COMPACT_WAVE  // k_compact_items: one wave per item (0: one 256-thread block per item)
-#define OKM_COMPACT_WAVE 1
-#endif
-#ifndef OKM_MERGE_SIBLINGS  // k_make_items: count aligned groups of 2 / 4 sparse sibling children as one item
-#define OKM_MERGE_SIBLINGS 0  // measured: count_items 1.658 -> 1.711 ms on C2 (fuller items are slower)
-#endif
 
 __global__ __launch_bounds__(kScanBlock) void k_scan_block(const ull *__restrict__ in,
                                                            ull *__restrict__ out, uint64_t n,
@@ -102,61 +96,6 @@ __global__ __launch_bounds__(256) void k_make_items(const ull *__restrict__ offs
     const ull o = offs[i], len = (ends ? ends[i] : offs[i + 1]) - o;
     const ull so = doff ? doff[i] : o;  // staged output slot: dense, or the level's own range
     const uint32_t F = 1u << fan.bits;  // item slots per child (in key order)
-#if OKM_MERGE_SIBLINGS
-    // Sibling merge (no fan-out rounds only): an aligned group of 2 or 4
-    // sibling children whose instances fit one item together is counted as
-    // ONE item -- their union is the key range one bit (two bits) above them,
-    // so the item's homes are that range's top bits and the output stays in
-    // key order.  Power-of-two splits leave children between 1/2 and 1x the
-    // planner's target; merging the sparse ones fills items closer to the
-    // count kernel's capacity (fewer items, same instances).  The head child's
-    // item takes the group's segments (segs of consecutive children are
-    // consecutive when fan.bits = 0); the other members' slots are empty items.
-    if (fan.bits == 0 && len <= item_max) {
-        const uint32_t pb = parents[lo].out_base;
-        const uint32_t nch = (lo + 1 < nparents ? parents[lo + 1].out_base : nout) - pb;
-        const uint32_t j = i - pb;
-        uint32_t g = 1;
-        ull gsum = len;
-#pragma unroll
-        for (uint32_t m = 2; m >= 1; --m) {
-            const uint32_t gg = 1u << m;
-            if (g != 1 || nch % gg != 0) continue;
-            const uint32_t h = pb + (j & ~(gg - 1u));
-            ull s = 0;
-            for (uint32_t q = 0; q < gg; ++q) s += (ends ? ends[h + q] : offs[h + q + 1]) - offs[h + q];
-            if (s <= item_max && rem + m <= 64) {
-                g = gg;
-                gsum = s;
-            }
-        }
-        if (g > 1) {
-            const uint32_t head = pb + (j & ~(g - 1u));
-            DevSeg s;
-            s.keys = lk + o * kw;
-            s.counts = lc ? lc + o : nullptr;
-            s.len = len;
-            s.key_base = 0;
-            s.out_base = 0;
-            s.shift = kSingleBin;
-            s.nlocal = 1;
-            s.pad = 0;
-            segs[i] = s;
-            DevItem it;
-            it.seg_begin = head;
-            it.seg_count = g;
-            it.out_off = doff ? doff[head] : offs[head];
-            it.rem_bits = rem + (g == 4 ? 2u : 1u);
-            it.pad = i == head ? 0u : kItemEmpty;
-            it.total = i == head ? gsum : 0;
-            it.keys0 = s.keys;
-            it.counts0 = s.counts;
-            items[i] = it;
-            if (i == head) atomicMax(&flags[2], gsum);
-            return;
-        }
-    }
-#endif
     uint32_t b = 0;                     // this child's own fan-out
     if (len > item_max && rem > capbits) {
         if (fan.bits && len <= fan.split_max) {
@@ -230,9 +169,6 @@ void launch_child_offsets(void *stream, const ull *offs, const ull *ends, uint32
 // latency-bound (a few rows each), so two variants run: 512-thread
 // workgroups for jobs of <= 16 Ki keys (32 KiB of ranks: 4 workgroups per CU)
 // and 1024-thread ones with 128 KiB of ranks for the larger jobs.
-#ifndef OKM_FAN_REG  // unweighted jobs of <= 16 Ki keys: keys held in registers (read once)
-#define OKM_FAN_REG 1
-#endif
 constexpr int kFanBins = 16;  // <= 4 bits per job
 constexpr int kFanSmallBlock = 512, kFanSmallMax = 16384;
 constexpr int kFanBigBlock = 1024, kFanBigMax = 65536;
@@ -443,7 +379,7 @@ static void fan_launch(hipStream_t s, uint32_t max_jobs, const DevFanJob *jobs, 
                        const uint64_t *sc, KT *dk, uint64_t *dc, DevItem *items, DevSeg *segs, uint64_t item_max,
                        uint32_t capbits, ull *oflags) {
     const dim3 gs(max_jobs < 4096u ? max_jobs : 4096u), gb(max_jobs < 2048u ? max_jobs : 2048u);
-    if (!W && OKM_FAN_REG) {
+    if (!W) {  // unweighted jobs of <= 16 Ki keys: keys held in registers (read once)
         hipLaunchKernelGGL((k_fan_split_reg<KT>), gb, dim3(kFanRegBlock), 0, s, jobs, flags, sk, dk, items, segs,
                            item_max, capbits, oflags);
     } else {
@@ -663,7 +599,6 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
                                                        const ull *__restrict__ d_nitems) {
     if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
-#if OKM_COMPACT_WAVE
     // One wave per item (an item holds ~600 entries at C2: a 256-thread block
     // per item left most lanes idle behind three dependent descriptor loads);
     // the next item's descriptor is loaded during this item's copy, and every
@@ -711,15 +646,6 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
         src = ns;
         dst = nd;
     }
-#else
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const uint64_t n = n_out[item], src = items[item].out_off, dst = dense_off[item];
-        for (uint64_t j = threadIdx.x; j < n; j += 256) {
-            dk[dst + j] = sk[src + j];
-            dc[dst + j] = NARROW ? (uint64_t)reinterpret_cast<const uint32_t *>(sc)[src + j] : sc[src + j];
-        }
-    }
-#endif
 }
 
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
@@ -728,15 +654,8 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
                           const unsigned long long *err, const unsigned long long *d_nitems) {
     if (!nitems) return;
-#if OKM_COMPACT_WAVE
-    static const uint32_t cap = [] {  // OKM_COMPACT_GRID: A/B runs
-        const char *e = getenv("OKM_COMPACT_GRID");
-        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4096u;
-    }();
+    constexpr uint32_t cap = 4096;  // grids of 2048 / 8192 measured the same (profiles/AB_LOG.md round 4)
     const dim3 g(nitems / 4u + 1u < cap ? nitems / 4u + 1u : cap), b(256);  // one wave per item
-#else
-    const dim3 g(nitems < 8191u ? nitems : 8191u), b(256);  // odd: fan-out slots spread over blocks
-#endif
     hipStream_t s = (hipStream_t)stream;
     const K128 *sk2 = reinterpret_cast<const K128 *>(src_keys);
     K128 *dk2 = reinterpret_cast<K128 *>(dst_keys);

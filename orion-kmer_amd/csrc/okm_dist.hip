@@ -56,6 +56,7 @@
 
 #include "okm_dev_common.h"
 #include "okm_hip_try.h"
+#include "orion_kmer_testing.h"
 
 namespace okm {
 
@@ -378,10 +379,7 @@ class Transport {
 class RcclTransport final : public Transport {
   public:
     explicit RcclTransport(ncclComm_t nc) : nc_(nc) {}
-    bool owned_send_buffers() const override {
-        const char *e = getenv("OKM_RCCL_SEND_IN_PLACE");  // 1: send the table slices in place (A/B)
-        return !(e && *e == '1');
-    }
+    bool owned_send_buffers() const override { return true; }
     ~RcclTransport() override {
         if (nc_) (void)rccl().CommDestroy(nc_);
     }
@@ -430,9 +428,9 @@ struct LoopHub {
     std::vector<std::vector<P2POp>> sends;    // each rank's sends of the current group
     explicit LoopHub(int n) : P(n), post(n, nullptr), sends(n) {}
 
-    static double timeout_s() {
-        const char *e = getenv("OKM_LOOPBACK_TIMEOUT_S");
-        return e && atof(e) > 0 ? atof(e) : 300.0;
+    static double timeout_s() {  // OKM_TEST_LOOPBACK_TIMEOUT_MS (tests), else 300 s
+        const int64_t ms = test_knob(OKM_TEST_LOOPBACK_TIMEOUT_MS);
+        return ms > 0 ? (double)ms * 1e-3 : 300.0;
     }
     // false: aborted (now or while waiting) or timed out (the hub is then aborted)
     bool barrier() {
@@ -549,16 +547,15 @@ class LoopTransport final : public Transport {
     int me_;
 };
 
-// Bytes per point-to-point message piece (OKM_RCCL_PIECE, default and
-// maximum 512 MiB).  RCCL 2.27.7 (ROCm 7.2) delivers only the FIRST HALF of a
+// Bytes per point-to-point message piece (512 MiB; OKM_TEST_PIECE_BYTES
+// smaller in tests).  RCCL 2.27.7 (ROCm 7.2) delivers only the FIRST HALF of a
 // self send/recv above 1 GiB -- every byte from size/2 on is left unwritten,
 // for u8 and u64 messages alike (1.5 GiB, 2 GiB, 4 GiB, 7.9 GB all lose their
 // second half; 1 GiB arrives intact: tools/rccl_big_p2p.hip,
 // profiles/r03_rccl_self_p2p_sizes.txt) -- so pieces stay well below 1 GiB.
 static uint64_t piece_bytes() {
     constexpr uint64_t kMax = uint64_t(1) << 29;
-    const char *e = getenv("OKM_RCCL_PIECE");
-    const long long v = e ? atoll(e) : 0;
+    const int64_t v = test_knob(OKM_TEST_PIECE_BYTES);
     return v >= 8 ? std::min<uint64_t>((uint64_t)v & ~uint64_t(7), kMax) : kMax;
 }
 
@@ -643,13 +640,10 @@ okm_status broke(okm_comm *m, okm_status st) {
     return st;
 }
 
-// Test hook: OKM_DIST_FAIL_RANK=r makes rank r fail while sizing its receive
+// Test hook: OKM_TEST_FAIL_RANK = r makes rank r fail while sizing its receive
 // buffers (after the size exchange, before any send): every rank must return
 // an error and the communicator must stay usable.
-int debug_fail_rank() {
-    const char *e = getenv("OKM_DIST_FAIL_RANK");
-    return e ? atoi(e) : -1;
-}
+int debug_fail_rank() { return (int)test_knob(OKM_TEST_FAIL_RANK); }
 
 // One local table taking part in a merge.
 struct Table {
@@ -663,7 +657,7 @@ struct Table {
 // summed, then over ranks; the owner split balances the sum, so equal keys of
 // different tables meet on one rank.  Returns with every rank agreeing on
 // success: the word nb of the all-reduce carries "this rank failed".
-// Keys as 5-byte deltas on the wire: OKM_WIRE_DELTAS=1 / 0 forces either;
+// Keys as 5-byte deltas on the wire: OKM_TEST_WIRE_DELTAS = 1 / 0 forces either;
 // by default (2) with 2 to 4 ranks, where one to three xGMI links per GPU
 // bound the exchange and 9 -> 6 B per pair pays for the receiver's decode
 // passes (with 8 ranks and seven links per GPU the decode costs about what
@@ -672,8 +666,8 @@ struct Table {
 // total / P) leaves a mean gap of at most 2^38 over the 2^(2k-1) canonical
 // keys (an exponential gap passes 2^40 with probability e^-4: +0.3 B a pair).
 int want_deltas(uint32_t P) {
-    const char *e = getenv("OKM_WIRE_DELTAS");
-    if (e && *e) return *e != '0' ? 1 : 0;
+    const int64_t e = test_knob(OKM_TEST_WIRE_DELTAS);
+    if (e >= 0) return e != 0 ? 1 : 0;
     return P > 1 && P <= 4 ? 2 : 0;
 }
 bool dense_enough(uint64_t pairs_per_rank, uint32_t k) {
@@ -741,7 +735,7 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     if (st != OKM_OK) return st;
     if (h_sum[nb]) return fail(OKM_E_COMM, "okm_merge_owned: a peer rank failed before the exchange");
     if ((h_sum[nb + 1] != 0 && h_sum[nb + 1] != P) || (h_sum[nb + 2] != 0 && h_sum[nb + 2] != P))
-        return fail(OKM_E_COMM, "okm_merge_owned: ranks disagree on the key wire format (OKM_WIRE_DELTAS)");
+        return fail(OKM_E_COMM, "okm_merge_owned: ranks disagree on the key wire format (OKM_TEST_WIRE_DELTAS)");
     uint64_t pairs = 0;
     for (uint32_t b = 0; b < nb; ++b) pairs += h_sum[b];
     // every rank sees the same sums: the same decision everywhere
@@ -862,7 +856,7 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
         if (st == OKM_OK && nks) st = m->kesc.ensure(2 * nks * sizeof(uint64_t));
         if (st == OKM_OK) st = m->stmp.ensure(scan_tmp_elems(max_rs + 1) * sizeof(ull));
     }
-    if (st == OKM_OK && debug_fail_rank() == (int)me) st = fail(OKM_E_NOMEM, "okm_merge_owned: OKM_DIST_FAIL_RANK test hook");
+    if (st == OKM_OK && debug_fail_rank() == (int)me) st = fail(OKM_E_NOMEM, "okm_merge_owned: OKM_TEST_FAIL_RANK test hook");
     if (st == OKM_OK && !set && nesc) {  // escapes grouped by destination
         HIP_TRY(hipMemcpyAsync(m->esc_cur.p, eoff.data(), P * sizeof(ull), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_pack_counts<true>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +32,7 @@
 #include "okm_hip_try.h"
 #include "okm_internal.h"
 #include "okm_key.h"
+#include "orion_kmer_testing.h"
 
 namespace okm {
 
@@ -44,55 +46,60 @@ okm_status fail(okm_status s, const std::string &msg) {
 }
 
 // ---------------------------------------------------------------------------
-// Device memory pool (best-fit free list; GB-sized buffers are reused across
-// okm_count calls instead of hipMalloc/hipFree in the hot loop).
+// Device memory: one virtual-memory arena per context (okm_arena.h), under
+// ONE budget for every context of the process on a device.
 // ---------------------------------------------------------------------------
 struct DevPool;
-static bool pool_trace() {
-    static const bool on = getenv("OKM_POOL_TRACE") != nullptr;
-    return on;
-}
 static std::mutex g_pools_mu;
-static std::vector<DevPool *> g_pools;  // every live context's pool (cross-pool trim on OOM)
+static std::vector<DevPool *> g_pools;  // every live context's pool (cross-pool trim, the budget)
+static constexpr size_t kArenaChunk = size_t(1) << 30;  // 1 GiB: 64 MiB chunks cost the streaming kernels TLB reach
 
-// Share of HBM the pools aim to stay under (OKM_HBM_CAP, default 0.9).
-static double hbm_cap_frac() {
-    static const double frac = [] {
-        const char *e = getenv("OKM_HBM_CAP");
-        const double f = e ? atof(e) : 0.9;
-        return f > 0.0 && f <= 1.0 ? f : 0.9;
-    }();
-    return frac;
+// The device memory the process's contexts may map together: OKM_HBM_CAP, a
+// fraction of HBM (<= 1, default 0.9) or a byte count (> 1; "16e9" or with a
+// K/M/G/T suffix, powers of 1024), or the OKM_TEST_HBM_BUDGET_BYTES test hook.
+// A hard limit: past it the arena first unmaps idle chunks (its own, then the
+// other contexts'), and an allocation that still does not fit fails with
+// OKM_E_NOMEM -- which the counting paths plan around (key-range groups,
+// folding, tables moved to host memory: DESIGN.md §5).
+static double parse_budget(const char *e, double total) {
+    if (!e || !*e) return 0.9 * total;
+    char *end = nullptr;
+    double v = strtod(e, &end);
+    if (!(v > 0)) return 0.9 * total;
+    if (end && *end) {
+        const char u = (char)(*end | 0x20);
+        v *= u == 'k' ? 1024.0 : u == 'm' ? 1048576.0 : u == 'g' ? 1073741824.0 : u == 't' ? 1099511627776.0 : 1.0;
+    }
+    return v <= 1.0 ? v * total : std::min(v, total);
 }
-
-// OKM_POOL=classic: the cache of whole hipMalloc blocks instead of the arena
-// (A/B runs); OKM_ARENA_CHUNK_MB: the arena's physical chunk (default 1 GiB:
-// interleaved C2 runs 5.155 ms per step against 5.36 with 64 MiB chunks and
-// 5.373 with whole hipMalloc blocks, profiles/r04_ab_pool.txt).
-static bool arena_wanted() {
-    static const bool on = [] {
-        const char *e = getenv("OKM_POOL");
-        return !(e && strcmp(e, "classic") == 0);
-    }();
-    return on;
+static double device_total_bytes(int device) {
+    static std::atomic<size_t> totals[64];
+    const int d = device & 63;
+    size_t t = totals[d].load(std::memory_order_relaxed);
+    if (!t) {
+        if (hipDeviceTotalMem(&t, device) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0.0;
+        }
+        totals[d] = t;
+    }
+    return (double)t;
 }
-static size_t arena_chunk_bytes() {
-    static const size_t b = [] {
-        const char *e = getenv("OKM_ARENA_CHUNK_MB");
-        const long mb = e ? atol(e) : 1024;
-        return (size_t)(mb > 0 ? mb : 1024) << 20;
-    }();
-    return b;
+static double hbm_budget(int device) {
+    const double total = device_total_bytes(device);
+    const int64_t t = test_knob(OKM_TEST_HBM_BUDGET_BYTES);
+    if (t > 0) return std::min((double)t, total);
+    static const std::string env = getenv("OKM_HBM_CAP") ? getenv("OKM_HBM_CAP") : "";
+    return parse_budget(env.c_str(), total);
 }
 
 struct DevPool {
-    std::multimap<size_t, void *> free_;
-    std::map<void *, size_t> size_;
-    size_t held = 0;
     int device = 0;
-    int mode = -1;  // -1: undecided (first get), 0: whole-block cache, 1: arena
+    bool ready = false;
     VmmArena arena;
-    std::mutex mu;  // the owning context's thread, or another pool trimming this one on OOM
+    std::atomic<size_t> mapped_bytes{0};  // arena.mapped, readable without mu (the budget sums every pool)
+    size_t peak_in_use = 0;               // high-water mark of live ranges (okm_engine_info.device_peak_bytes)
+    std::mutex mu;  // the owning context's thread, or another pool trimming this one
 
     void attach(int dev) {
         device = dev;
@@ -103,133 +110,32 @@ struct DevPool {
         std::lock_guard<std::mutex> g(g_pools_mu);
         g_pools.erase(std::remove(g_pools.begin(), g_pools.end(), this), g_pools.end());
     }
-    bool arena_mode() {
-        std::lock_guard<std::mutex> g(mu);
-        return decide();
-    }
-    bool decide() {  // mu held
-        if (mode < 0) mode = arena_wanted() && arena.init(device, arena_chunk_bytes()) ? 1 : 0;
-        return mode == 1;
+    bool init_locked() {  // mu held
+        if (!ready) ready = arena.init(device, kArenaChunk);
+        return ready;
     }
     bool owns(const void *p) const {
         const char *q = static_cast<const char *>(p);
         return arena.base && q >= arena.base && q < arena.base + arena.reserved;
     }
-    okm_status get(size_t bytes, void **out) {
-        {
-            std::lock_guard<std::mutex> g(mu);
-            if (decide()) return arena_get(bytes, out);
-        }
-        bytes = (bytes + 255) & ~size_t(255);
-        if (bytes == 0) bytes = 256;
-        if (bytes > (64u << 20)) {  // big buffers: 1/16 size classes, so run-to-run size jitter reuses blocks
-            size_t g = 1;
-            while ((g << 5) <= bytes) g <<= 1;
-            bytes = (bytes + g - 1) & ~(g - 1);
-        }
-        {
-            std::lock_guard<std::mutex> g(mu);
-            auto it = free_.lower_bound(bytes);
-            // GB-sized requests take a block at most 1/4 larger (a 2x block would strand HBM)
-            const size_t slack = bytes > (size_t(1) << 30) ? bytes / 4 : bytes;
-            if (it != free_.end() && it->first <= bytes + slack) {
-                *out = it->second;
-                if (pool_trace()) fprintf(stderr, "[pool] reuse %zu for %zu held %zu\n", it->first, bytes, held);
-                free_.erase(it);
-                return OKM_OK;
-            }
-        }
-        void *p = nullptr;
-        // Soft cap on the device's memory in use (OKM_HBM_CAP, default 0.9 of
-        // HBM): past it, cached blocks are reused or released first, as when
-        // HBM is full; only then does the allocation go past the cap.
-        auto try_alloc = [&]() -> hipError_t {
-            if (over_cap(bytes)) return hipErrorOutOfMemory;
-            return hipMalloc(&p, bytes);
-        };
-        hipError_t e = try_alloc();
-        if (e != hipSuccess) {
-            // HBM is full: any larger cached block beats freeing and re-mapping
-            // (hipFree + hipMalloc of tens of GB costs hundreds of ms per step)
-            (void)hipGetLastError();
-            {
-                std::lock_guard<std::mutex> g(mu);
-                auto it = free_.lower_bound(bytes);
-                if (it != free_.end()) {
-                    *out = it->second;
-                    free_.erase(it);
-                    return OKM_OK;
-                }
-            }
-            // release cached blocks, largest first, until the block fits (the
-            // rest stay cached for the sizes that come back every step); then
-            // every other pool's on the device
-            (void)hipGetLastError();
-            size_t freed = 0;
-            while (e != hipSuccess) {
-                {
-                    std::lock_guard<std::mutex> g(mu);
-                    if (free_.empty()) break;
-                    auto big = std::prev(free_.end());
-                    (void)hipFree(big->second);
-                    held -= size_[big->second];
-                    freed += big->first;
-                    size_.erase(big->second);
-                    free_.erase(big);
-                }
-                if (freed + (size_t(256) << 20) < bytes) continue;  // not enough back yet
-                (void)hipGetLastError();
-                e = try_alloc();
-            }
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                e = try_alloc();
-            }
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                trim_others();
-                e = try_alloc();
-            }
-            if (e != hipSuccess) {  // nothing cached is left to give back: the cap is soft
-                (void)hipGetLastError();
-                e = hipMalloc(&p, bytes);
-            }
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                if (pool_trace()) {  // what holds the device: every block, in use or cached
-                    std::lock_guard<std::mutex> g(mu);
-                    for (auto &kv : size_) {
-                        bool cached_blk = false;
-                        for (auto &f : free_) cached_blk |= f.second == kv.first;
-                        fprintf(stderr, "[pool] block %p %.2f GB %s\n", kv.first, kv.second / 1e9,
-                                cached_blk ? "cached" : "in use");
-                    }
-                }
-                size_t fr = 0, tot = 0;
-                (void)hipMemGetInfo(&fr, &tot);
-                (void)hipGetLastError();
-                return fail(OKM_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e) +
-                                             " (context holds " + std::to_string(held) + " B in " +
-                                             std::to_string(size_.size()) + " blocks, " + std::to_string(cached()) +
-                                             " B cached; device free " + std::to_string(fr) + " of " +
-                                             std::to_string(tot) + " B)");
-            }
-        }
-        std::lock_guard<std::mutex> g(mu);
-        size_[p] = bytes;
-        held += bytes;
-        *out = p;
-        if (getenv("OKM_PROFILE_HOST") || pool_trace())
-            fprintf(stderr, "[okm pool] hipMalloc %zu bytes (held %zu, free blocks %zu) %p\n", bytes, held, free_.size(),
-                    p);
-        return OKM_OK;
+    // Bytes every pool on this device has mapped.
+    static size_t device_mapped(int device) {
+        std::lock_guard<std::mutex> g(g_pools_mu);
+        size_t b = 0;
+        for (DevPool *o : g_pools)
+            if (o->device == device) b += o->mapped_bytes.load(std::memory_order_relaxed);
+        return b;
     }
-    // Arena allocation (mu held): a best-fit address range, then physical
-    // chunks for the parts of it that are not mapped yet.  Past the soft cap,
-    // idle chunks of this arena (then of the other pools on the device) are
-    // unmapped first — after a device sync, since a freed range's last kernel
-    // may still be in flight.
-    okm_status arena_get(size_t bytes, void **out) {
+    // Would `bytes` more mapped memory take the device's pools past the budget?
+    bool over_budget(size_t bytes) const { return (double)device_mapped(device) + (double)bytes > hbm_budget(device); }
+
+    // A best-fit address range, then physical chunks for the parts of it that
+    // are not mapped yet.  Past the budget, idle chunks of this arena (then of
+    // the other pools on the device) are unmapped first -- after a device
+    // sync, since a freed range's last kernel may still be in flight.
+    okm_status get(size_t bytes, void **out) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!init_locked()) return fail(OKM_E_DEVICE, "device arena: no virtual memory management on this device");
         bytes = VmmArena::round_up(std::max<size_t>(bytes, 256), 256);
         const size_t off = arena.take(bytes);
         if (off == ~size_t(0))
@@ -246,23 +152,24 @@ struct DevPool {
         };
         if (missing) {
             const size_t need = missing * arena.chunk;
-            if (over_cap(need) && arena.idle()) {
+            if (over_budget(need) && arena.idle()) {
                 (void)hipDeviceSynchronize();
                 arena.unmap_idle(need);
+                mapped_bytes = arena.mapped;
             }
-            if (over_cap(need)) {  // other contexts' idle chunks (their locks, not ours)
+            if (over_budget(need)) {  // other contexts' idle chunks (their locks, not ours)
                 mu.unlock();
                 trim_others();
                 mu.lock();
             }
-            const auto t0 = std::chrono::steady_clock::now();
-            hipError_t e = hipSuccess;
+            hipError_t e = over_budget(need) ? hipErrorOutOfMemory : hipSuccess;
             for (size_t i = c0; i <= c1 && e == hipSuccess; ++i)
                 if (!arena.chunks[i].mapped) e = arena.map_chunk(i);
-            if (e != hipSuccess) {  // HBM full: give back everything idle and try once more
+            if (e != hipSuccess && !over_budget(need)) {  // HBM full (other allocations): everything idle back, once more
                 (void)hipGetLastError();
                 (void)hipDeviceSynchronize();
                 arena.unmap_idle(~size_t(0));
+                mapped_bytes = arena.mapped;
                 mu.unlock();
                 trim_others();
                 mu.lock();
@@ -270,12 +177,7 @@ struct DevPool {
                 for (size_t i = c0; i <= c1 && e == hipSuccess; ++i)
                     if (!arena.chunks[i].mapped) e = arena.map_chunk(i);
             }
-            held = arena.mapped;
-            if (getenv("OKM_PROFILE_HOST") || pool_trace())
-                fprintf(stderr, "[okm arena] mapped %zu chunks for %zu B in %.3f ms (mapped %.2f GB, in use %.2f GB)\n",
-                        missing, bytes,
-                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
-                        arena.mapped / 1e9, arena.in_use / 1e9);
+            mapped_bytes = arena.mapped;
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 undo();
@@ -283,44 +185,30 @@ struct DevPool {
                 (void)hipMemGetInfo(&fr, &tot);
                 (void)hipGetLastError();
                 return fail(OKM_E_NOMEM, "device arena: mapping " + std::to_string(bytes) + " B: " +
-                                             hipGetErrorString(e) + " (context maps " + std::to_string(arena.mapped) +
-                                             " B, " + std::to_string(arena.in_use) + " B in use; device free " +
+                                             (over_budget(need) ? std::string("over the device budget of ") +
+                                                                      std::to_string((uint64_t)hbm_budget(device)) + " B"
+                                                                : std::string(hipGetErrorString(e))) +
+                                             " (context maps " + std::to_string(arena.mapped) + " B, " +
+                                             std::to_string(arena.in_use) + " B in use; device free " +
                                              std::to_string(fr) + " of " + std::to_string(tot) + " B)");
             }
         }
+        peak_in_use = std::max(peak_in_use, arena.in_use);
         *out = arena.base + off;
         return OKM_OK;
-    }
-    // Would `bytes` more take the device past the soft cap?
-    bool over_cap(size_t bytes) const {
-        const double frac = hbm_cap_frac();
-        if (frac >= 1.0) return false;
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) {
-            (void)hipGetLastError();
-            return false;
-        }
-        return (double)(tot - fr) + (double)bytes > frac * (double)tot;
     }
     void put(void *p) {
         if (!p) return;
         std::lock_guard<std::mutex> g(mu);
-        if (owns(p)) {
-            const size_t off = static_cast<char *>(p) - arena.base;
-            auto it = arena.live.find(off);
-            if (it == arena.live.end()) return;  // a pointer inside a block (e.g. a table's counts)
-            for (size_t i = arena.first_chunk(off); i <= arena.last_chunk(off, it->second); ++i) arena.chunks[i].users--;
-            arena.give_back(off);
-            return;
-        }
-        auto it = size_.find(p);
-        if (it == size_.end()) return;
-        if (pool_trace()) fprintf(stderr, "[pool] put %zu %p\n", it->second, p);
-        free_.emplace(it->second, p);
+        if (!owns(p)) return;
+        const size_t off = static_cast<char *>(p) - arena.base;
+        auto it = arena.live.find(off);
+        if (it == arena.live.end()) return;  // a pointer inside a block (e.g. a table's counts)
+        for (size_t i = arena.first_chunk(off); i <= arena.last_chunk(off, it->second); ++i) arena.chunks[i].users--;
+        arena.give_back(off);
     }
-    // Arena ranges only: keep the first `bytes` of the allocation at p (its
-    // tail returns to the arena, nothing moves); false when p is not an arena
-    // allocation.
+    // Keep the first `bytes` of the allocation at p (its tail returns to the
+    // arena, nothing moves); false when p is not an allocation of this pool.
     bool shrink(void *p, size_t bytes) {
         std::lock_guard<std::mutex> g(mu);
         if (!owns(p)) return false;
@@ -331,59 +219,34 @@ struct DevPool {
     }
     size_t size_of(const void *p) {
         std::lock_guard<std::mutex> g(mu);
-        if (owns(p)) {
-            auto it = arena.live.find(static_cast<const char *>(p) - arena.base);
-            return it == arena.live.end() ? 0 : it->second;
-        }
-        auto it = size_.find(const_cast<void *>(p));
-        return it == size_.end() ? 0 : it->second;
+        if (!owns(p)) return 0;
+        auto it = arena.live.find(static_cast<const char *>(p) - arena.base);
+        return it == arena.live.end() ? 0 : it->second;
     }
-    // OKM_POOL_DUMP=1 (tuning): every block, its size and whether it is cached
-    void dump(const char *tag) {
+    size_t held() {
         std::lock_guard<std::mutex> g(mu);
-        if (mode == 1) {
-            fprintf(stderr, "[okm arena %s] mapped %.2f GB, in use %.2f GB in %zu ranges, %zu free ranges, idle %.2f GB\n",
-                    tag, arena.mapped / 1e9, arena.in_use / 1e9, arena.live.size(), arena.free_off.size(),
-                    arena.idle() / 1e9);
-            return;
-        }
-        size_t c = 0;
-        for (auto &f : free_) c += f.first;
-        fprintf(stderr, "[okm pool %s] %zu blocks, held %.2f GB, cached %.2f GB:", tag, size_.size(), held / 1e9, c / 1e9);
-        for (auto &kv : size_) {
-            bool cached_blk = false;
-            for (auto &f : free_) cached_blk |= f.second == kv.first;
-            fprintf(stderr, " %.3f%s", kv.second / 1e9, cached_blk ? "c" : "");
-        }
-        fprintf(stderr, "\n");
+        return arena.mapped;
     }
-    // Bytes held but not in use (reusable without new device memory).
+    size_t peak() {
+        std::lock_guard<std::mutex> g(mu);
+        return peak_in_use;
+    }
+    void reset_peak() {
+        std::lock_guard<std::mutex> g(mu);
+        peak_in_use = arena.in_use;
+    }
+    // Bytes mapped but not in use (reusable without new device memory).
     size_t cached() {
         std::lock_guard<std::mutex> g(mu);
-        if (mode == 1) return arena.mapped - std::min(arena.mapped, arena.in_use);
-        size_t b = 0;
-        for (auto &kv : free_) b += kv.first;
-        return b;
+        return arena.mapped - std::min(arena.mapped, arena.in_use);
     }
-    // hipFree synchronises the device, so a block freed here is idle even if
-    // its owner put it back while its kernels were still queued (the arena
-    // synchronises before unmapping for the same reason)
     void trim() {
         std::lock_guard<std::mutex> g(mu);
-        if (mode == 1) {
-            if (arena.idle()) {
-                (void)hipDeviceSynchronize();
-                arena.unmap_idle(~size_t(0));
-                held = arena.mapped;
-            }
-            return;
+        if (arena.idle()) {
+            (void)hipDeviceSynchronize();
+            arena.unmap_idle(~size_t(0));
+            mapped_bytes = arena.mapped;
         }
-        for (auto &kv : free_) {
-            (void)hipFree(kv.second);
-            held -= size_[kv.second];
-            size_.erase(kv.second);
-        }
-        free_.clear();
     }
     void trim_others() {
         std::lock_guard<std::mutex> g(g_pools_mu);
@@ -393,10 +256,8 @@ struct DevPool {
     void release_all() {
         std::lock_guard<std::mutex> g(mu);
         arena.release();
-        for (auto &kv : size_) (void)hipFree(kv.first);
-        size_.clear();
-        free_.clear();
-        held = 0;
+        mapped_bytes = 0;
+        ready = false;
     }
 };
 
@@ -542,6 +403,7 @@ struct Run {
     bool sorted = false;         // strictly ascending unique keys (okm_add_sorted_pairs_device)
     bool borrowed = false;       // caller-owned memory: never returned to the pool
     bool folded = false;         // a counted table kept as a weighted L1 run (fold(), bins by binary search)
+    bool host = false;           // keys / counts in page-locked HOST memory (a folded table moved off a full device)
     uint64_t len(uint32_t b) const { return (end.empty() ? off[b + 1] : end[b]) - off[b]; }
 };
 
@@ -575,7 +437,7 @@ struct okm_ctx {
     size_t Hg_cap = 0;
     unsigned long long *flag = nullptr;  // overflow word
     unsigned long long *l1cap = nullptr; // sampled L1: cap_end | start | overflow
-    unsigned long long *curpad = nullptr;  // sampled L1 claim cursors, OKM_L1_CUR_STRIDE apart
+    unsigned long long *curpad = nullptr;  // sampled L1 claim cursors, kL1CurStride apart
     uint8_t *staging = nullptr;          // device copy of a host batch
     size_t staging_cap = 0;
     uint8_t *pinned = nullptr;           // pinned host staging
@@ -609,6 +471,9 @@ struct okm_ctx {
     bool share_result = false;
     uint64_t *res_keys = nullptr, *res_counts = nullptr;
     uint64_t n_res = 0;
+    bool res_host = false;     // the result lies in page-locked HOST memory (too big to stay beside its inputs)
+    uint64_t host_bytes = 0;   // host memory held by host runs and a host result
+    uint32_t spills = 0;       // tables moved to host memory
     okm_engine_info info{};
 };
 
@@ -680,17 +545,30 @@ static okm_status ensure_staging(okm_ctx *c, size_t bytes) {
     return OKM_OK;
 }
 
+static void host_table_free(okm_ctx *c, uint64_t *keys, uint64_t *counts, uint64_t n) {
+    host_pinned_free(keys);
+    host_pinned_free(counts);
+    const uint64_t b = n * 8 * c->kw + (counts ? n * 8 : 0);
+    c->host_bytes -= std::min(c->host_bytes, b);
+}
+
 static void invalidate_result(okm_ctx *c) {
-    if (c->res_keys) c->pool.put(c->res_keys);
-    if (c->res_counts) c->pool.put(c->res_counts);
+    if (c->res_host) {
+        host_table_free(c, c->res_keys, c->res_counts, c->n_res);
+    } else {
+        if (c->res_keys) c->pool.put(c->res_keys);
+        if (c->res_counts) c->pool.put(c->res_counts);
+    }
+    c->res_host = false;
     c->res_keys = c->res_counts = nullptr;
     c->n_res = 0;
     c->counted = false;
     c->res_is_input = false;
 }
 
-// Device memory this context may still use: free + its pool's cached blocks,
-// and no more than the room under the pools' soft cap (OKM_HBM_CAP).
+// Device memory this context may still use: the budget (OKM_HBM_CAP) less
+// what every pool on the device maps, plus this pool's cached (idle) part --
+// and no more than the device's free memory plus that cached part.
 static double device_room(okm_ctx *c) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
@@ -698,8 +576,8 @@ static double device_room(okm_ctx *c) {
         free_b = 0;
     }
     const double cached = (double)c->pool.cached();
-    double room = (double)free_b + cached;
-    if (total_b) room = std::min(room, hbm_cap_frac() * (double)total_b - (double)(total_b - free_b) + cached);
+    const double room = std::min((double)free_b + cached,
+                                 hbm_budget(c->device) - (double)DevPool::device_mapped(c->device) + cached);
     return std::max(room, 0.0);
 }
 
@@ -757,14 +635,8 @@ static okm_status hist_to_offsets(okm_ctx *c, size_t nb, std::vector<uint64_t> &
     return OKM_OK;
 }
 
-// Tile sampling stride of the sampled L1 placement (0/1: always exact).
-static uint32_t l1_sample_stride() {
-    static const uint32_t s = [] {
-        const char *e = getenv("OKM_L1_SAMPLE");
-        return e ? (uint32_t)atoi(e) : 16u;
-    }();
-    return s;
-}
+// Tile sampling stride of the sampled L1 placement.
+static constexpr uint32_t kL1SampleStride = 16;
 
 // Sampled L1 placement: histogram every S-th tile, size each bin from that
 // sample (launch_l1_capacity), scatter with per-tile claims.  One host sync,
@@ -780,8 +652,8 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     const uint64_t last = (uint64_t)(gs.nblocks - 1) * S * tile;  // the only sampled tile that can be short
     const uint64_t sbytes = (uint64_t)(gs.nblocks - 1) * tile + std::min(tile, n - last);
     const double scale = (double)n / (double)sbytes;
-    const char *dbg = getenv("OKM_L1_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
-    const double mul = dbg ? atof(dbg) : 1.0;
+    const int64_t dbg = test_knob(OKM_TEST_L1_CAP_PERMILLE);  // tests: shrink capacities to force the exact redo
+    const double mul = dbg >= 0 ? (double)dbg / 1000.0 : 1.0;
     // sum_b scale s_b <= w n (windows <= bytes; w = the windows-per-byte ratio
     // seen so far on this context, 1 before the first batch: the run is sized
     // for the keys it gets, not for the bytes); sum_b sqrt(s_b) <= sqrt(nb * w * sbytes).
@@ -812,7 +684,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     unsigned long long *cap = c->hres, *ends = c->hres + 2 * nb + 2;  // 3 nb + 2 <= kHresCount words
     HIP_TRY(hipMemcpyAsync(cap, c->l1cap, (2 * nb + 2) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
-    HIP_TRY(hipMemcpy2DAsync(ends, sizeof(unsigned long long), cur, OKM_L1_CUR_STRIDE * sizeof(unsigned long long),
+    HIP_TRY(hipMemcpy2DAsync(ends, sizeof(unsigned long long), cur, kL1CurStride * sizeof(unsigned long long),
                              sizeof(unsigned long long), nb, hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     if (cap[2 * nb + 1]) {  // some bin outgrew its sampled capacity: redo exactly
@@ -853,7 +725,30 @@ static void set_l1_geometry(okm_ctx *c) {
 
 // L1 bin bounds of a sorted run by binary search (a sorted table is already
 // partitioned by key range: nothing moves).
+// L1 bin b of a key: its top l1 bits (the same cut as k_bin_bounds).
+static uint64_t key_bin_host(const okm_ctx *c, const uint64_t *keys, uint64_t i) {
+    if (c->wide) {
+        const uint64_t lo = keys[2 * i], hi = keys[2 * i + 1];
+        const uint32_t sh = c->shift1;
+        return sh >= 128 ? 0 : sh >= 64 ? hi >> (sh - 64) : sh == 0 ? lo : (hi << (64 - sh)) | (lo >> sh);
+    }
+    return c->shift1 >= 64 ? 0 : keys[i] >> c->shift1;
+}
+
 static okm_status sorted_run_bins(okm_ctx *c, Run &run) {
+    if (run.host) {  // a table in host memory: the bin starts by binary search on the host
+        run.off.assign(c->nbins + 1, run.n);
+        for (uint32_t b = 0; b <= c->nbins; ++b) {
+            uint64_t lo = 0, hi = run.n;  // first i with bin(i) >= b
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                if (key_bin_host(c, run.keys, mid) < b) lo = mid + 1; else hi = mid;
+            }
+            run.off[b] = lo;
+        }
+        run.off[c->nbins] = run.n;
+        return OKM_OK;
+    }
     OKM_TRY(ensure_hg(c, c->nbins + 1));
     launch_bin_bounds(c->stream, run.keys, run.n, c->shift1, c->nbins, c->Hg, c->wide);
     HIP_TRY(hipGetLastError());
@@ -866,14 +761,16 @@ static okm_status sorted_run_bins(okm_ctx *c, Run &run) {
 // The counted result becomes a folded run: a sorted weighted table owned by
 // the context, at its exact size (the count sized it by its instances).
 static okm_status result_to_folded_run(okm_ctx *c, Run *out) {
-    OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.25));
+    if (!c->res_host) OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.25));
     Run run;
     run.keys = c->res_keys;
     run.counts = c->res_counts;
     run.n = c->n_res;
     run.sorted = true;
     run.folded = true;
+    run.host = c->res_host;
     c->res_keys = c->res_counts = nullptr;
+    c->res_host = false;
     c->n_res = 0;
     c->counted = false;
     if (run.n) OKM_TRY(sorted_run_bins(c, run));
@@ -903,12 +800,21 @@ static okm_status before_add(okm_ctx *c) {
     return OKM_OK;
 }
 
-static void release_runs(okm_ctx *c, std::vector<Run> &runs) {
-    for (auto &r : runs) {
-        if (r.borrowed) continue;
+// A run's memory back to the pool (device) or the host (host runs); borrowed
+// runs belong to the caller.
+static void free_run(okm_ctx *c, Run &r) {
+    if (r.borrowed) return;
+    if (r.host) {
+        host_table_free(c, r.keys, r.counts, r.n);
+    } else {
         c->pool.put(r.keys);
         c->pool.put(r.counts);
     }
+    r.keys = r.counts = nullptr;
+}
+
+static void release_runs(okm_ctx *c, std::vector<Run> &runs) {
+    for (auto &r : runs) free_run(c, r);
     runs.clear();
 }
 
@@ -939,15 +845,6 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
     return OKM_OK;
 }
 
-// OKM_L1_FOLD=0: a folding context keeps the batch-by-batch geometry (A/B).
-static bool fold_geometry_wanted() {
-    static const bool on = [] {
-        const char *e = getenv("OKM_L1_FOLD");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-
 // Fold (memory bounded by distinct keys, not by input): the batches added
 // since the last fold are counted into a sorted (key, count) table that
 // replaces their L1 runs; every kFoldMergeRuns tables are merged into one
@@ -955,7 +852,57 @@ static bool fold_geometry_wanted() {
 // last batches' table.  The reference's DashMap grows with distinct k-mers
 // only (count.rs:48); without folding every batch's instances would stay
 // resident until okm_count.
+// Device bytes a run holds (borrowed and host runs: none).
+static uint64_t run_device_bytes(okm_ctx *c, const Run &r) {
+    if (r.borrowed || r.host) return 0;
+    return c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
+}
+
+// Move folded tables to page-locked host memory, oldest first, until the
+// device has `need` bytes of room (or no table is left on it).  The
+// reference's DashMap grows in host RAM until the machine runs out
+// (count.rs:48); here a table that no longer fits beside the next count's
+// working set waits in host memory, and okm_count merges every table key
+// range by key range (count_spilled), the host ones streamed back in slices.
+static okm_status spill_tables(okm_ctx *c, double need) {
+    for (auto &r : c->runs) {
+        if (device_room(c) >= need) break;
+        if (!r.folded || r.host || r.borrowed || r.n == 0) continue;
+        const uint64_t kb = r.n * 8 * c->kw, cb = r.counts ? r.n * 8 : 0;
+        uint64_t *hk = static_cast<uint64_t *>(host_pinned_alloc(kb));
+        uint64_t *hc = cb ? static_cast<uint64_t *>(host_pinned_alloc(cb)) : nullptr;
+        if (!hk || (cb && !hc)) {
+            host_pinned_free(hk);
+            host_pinned_free(hc);
+            return fail(OKM_E_NOMEM, "moving a " + std::to_string(kb + cb) +
+                                         " B table off the device: page-locked host allocation failed");
+        }
+        HIP_TRY(hipMemcpyAsync(hk, r.keys, kb, hipMemcpyDeviceToHost, c->stream));
+        if (cb) HIP_TRY(hipMemcpyAsync(hc, r.counts, cb, hipMemcpyDeviceToHost, c->stream));
+        OKM_TRY(sync(c));
+        c->pool.put(r.keys);
+        c->pool.put(r.counts);  // (inside the keys' block when shrink_table joined them: ignored)
+        r.keys = hk;
+        r.counts = hc;
+        r.host = true;
+        c->host_bytes += kb + cb;
+        c->spills += 1;
+        c->hprof.mark("spill");
+    }
+    return OKM_OK;
+}
+
+// Device bytes of the uncounted batch runs (their count needs ~4.5x that:
+// level array, staged runs, the exact table).
+static double uncounted_bytes(okm_ctx *c) {
+    double b = 0;
+    for (auto &r : c->runs)
+        if (!r.sorted) b += (double)run_device_bytes(c, r);
+    return b;
+}
+
 static okm_status fold(okm_ctx *c) {
+    OKM_TRY(spill_tables(c, 4.5 * uncounted_bytes(c)));
     OKM_TRY(count_unsorted_to_table(c));
     c->folds += 1;
     // A context that folds takes 10 L1 bits from here on (and after okm_reset):
@@ -964,7 +911,7 @@ static okm_status fold(okm_ctx *c) {
     // (C3 on one GPU: 414 vs 461 ms; a batch-by-batch C2 count stays at 9 bits,
     // its extraction writes longer runs: 5.23 vs 5.44 ms).  Only sorted runs
     // (tables) are left here, and their bins come from a binary search.
-    if (!c->l1_fold && !c->wide && fold_geometry_wanted()) {
+    if (!c->l1_fold && !c->wide) {
         bool all_sorted = true;
         for (auto &r : c->runs) all_sorted &= r.sorted;
         if (all_sorted) {
@@ -974,22 +921,34 @@ static okm_status fold(okm_ctx *c) {
                 if (r.n) OKM_TRY(sorted_run_bins(c, r));
         }
     }
-    static const uint32_t merge_runs = [] {
-        const char *e = getenv("OKM_FOLD_MERGE_RUNS");
-        return e ? std::max(2, atoi(e)) : 4;
-    }();
+    // four tables merge into one (3: 438-448 ms per C3 job, 6: 446-451, 8: 499,
+    // 4: 409-412; profiles/AB_LOG.md round 4)
+    // Tables in host memory wait for okm_count; the device ones merge when
+    // the merge's exact table fits beside them, else they go to host memory too.
+    constexpr uint32_t merge_runs = 4;
     uint32_t tables = 0;
     bool only_folded = true;
+    double dev_pairs = 0;
     for (auto &r : c->runs) {
-        tables += r.folded;
+        tables += r.folded && !r.host;
         only_folded &= r.folded;
+        if (!r.host) dev_pairs += (double)r.n;
     }
     if (tables >= merge_runs && only_folded) {
-        OKM_TRY(do_count(c));
-        release_runs(c, c->runs);
-        Run t;
-        OKM_TRY(result_to_folded_run(c, &t));
-        if (t.n) c->runs.push_back(std::move(t));
+        if (device_room(c) < 1.5 * (8.0 * c->kw + 8.0) * dev_pairs) {
+            OKM_TRY(spill_tables(c, INFINITY));
+        } else {
+            std::vector<Run> host_runs, dev_runs;
+            for (auto &r : c->runs) (r.host ? host_runs : dev_runs).push_back(std::move(r));
+            c->runs = std::move(dev_runs);
+            okm_status st = do_count(c);
+            if (st == OKM_OK) release_runs(c, c->runs);
+            Run t;
+            if (st == OKM_OK) st = result_to_folded_run(c, &t);
+            for (auto &r : host_runs) c->runs.push_back(std::move(r));
+            OKM_TRY(st);
+            if (t.n) c->runs.push_back(std::move(t));
+        }
     }
     c->hprof.mark("fold");
     if (c->hprof.on) {
@@ -999,7 +958,7 @@ static okm_status fold(okm_ctx *c) {
             tn += r.n;
         }
         fprintf(stderr, "[okm fold] #%u: %zu runs of %.3f G keys holding %.1f GB; pool held %.1f GB, cached %.1f GB\n",
-                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held / 1e9, c->pool.cached() / 1e9);
+                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held() / 1e9, c->pool.cached() / 1e9);
     }
     return OKM_OK;
 }
@@ -1016,20 +975,8 @@ static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
         uncounted = true;
     }
     const double w = c->l1_ratio > 0 ? std::min(1.0, c->l1_ratio * 1.03) : 1.0;
-    // ... and never more than OKM_FOLD_MAX_KEYS instances in one fold (0 / unset:
-    // no cap; the byte threshold bounds it; C3 on one GPU: 5-batch folds of
-    // 2.5 G instances 816 ms per job, 4-batch folds 1006 ms)
-    static const uint64_t kFoldMaxKeys = [] {
-        const char *e = getenv("OKM_FOLD_MAX_KEYS");
-        return e && atoll(e) > 0 ? (uint64_t)atoll(e) : ~0ull;
-    }();
-    uint64_t keys = 0;
-    for (auto &r : c->runs)
-        if (!r.borrowed && !r.folded && !r.off.empty())
-            for (uint32_t b = 0; b + 1 < r.off.size(); ++b) keys += r.len(b);
     if (!uncounted) return OKM_OK;
-    if (held + (uint64_t)(w * (double)n) * 8 * c->kw <= c->fold_bytes && keys + (uint64_t)(w * (double)n) <= kFoldMaxKeys)
-        return OKM_OK;
+    if (held + (uint64_t)(w * (double)n) * 8 * c->kw <= c->fold_bytes) return OKM_OK;
     return fold(c);
 }
 
@@ -1042,17 +989,13 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     const uint64_t tile = extract_tile();
     uint64_t tiles = (n + tile - 1) / tile;
     // extraction workgroups: 8192 (C2: ~4 tiles each) against 2048: extract_scatter
-    // 1.438 vs 1.484 ms over 4 interleaved runs, 4096 1.447 (profiles/r04_ab_extract_blocks.txt);
-    // OKM_EXTRACT_BLOCKS overrides
-    static const uint64_t max_blocks = [] {
-        const char *e = getenv("OKM_EXTRACT_BLOCKS");
-        return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 8192ull;
-    }();
+    // 1.438 vs 1.484 ms over 4 interleaved runs, 4096 1.447 (profiles/r04_ab_extract_blocks.txt)
+    constexpr uint64_t max_blocks = 8192;
     uint32_t nblocks = (uint32_t)std::min<uint64_t>(tiles, max_blocks);
     uint64_t chunk = ((tiles + nblocks - 1) / nblocks) * tile;
     nblocks = (uint32_t)((n + chunk - 1) / chunk);
     ExtractGeom g{n, c->k, c->shift1, c->nbins, nblocks, chunk, 1};
-    const uint32_t S = l1_sample_stride();
+    const uint32_t S = kL1SampleStride;
     if (S > 1 && tiles >= 64ull * S && c->nbins > 1) {
         bool placed = false;
         OKM_TRY(l1_sampled(c, d_seq, n, g, S, &placed));
@@ -1093,10 +1036,7 @@ struct Part {
     uint32_t consumed;
 };
 
-#ifndef OKM_PART_CHUNK  // keys per partition chunk (a multiple of the scatter tiles)
-#define OKM_PART_CHUNK 65536
-#endif
-static const uint64_t kChunkKeys = OKM_PART_CHUNK;
+static constexpr uint64_t kChunkKeys = 65536;  // keys per partition chunk (a multiple of the scatter tiles)
 
 // Output of one partition pass: a level array whose bins are the children, in
 // key order, of the parts that took part (offsets stay on the device).
@@ -1118,14 +1058,8 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
                                        const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
                                        std::vector<void *> &level_bufs, Level &L, unsigned long long *ovf);
 
-// Tile sampling stride of the sampled partition placement (0/1: exact).
-static uint32_t part_sample_stride() {
-    static const uint32_t s = [] {
-        const char *e = getenv("OKM_PART_SAMPLE");
-        return e ? (uint32_t)atoi(e) : 16u;
-    }();
-    return s;
-}
+// Tile sampling stride of the sampled partition placement.
+static constexpr uint32_t kPartSampleStride = 16;
 
 // ovf (sampled mode): size the children from a histogram of 1/S of every
 // chunk (launch_part_capacity) instead of an exact pass, so no host sync
@@ -1212,7 +1146,7 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
                                        const std::vector<DevChunk> &chunks, const std::vector<uint32_t> &todo,
                                        const std::vector<uint32_t> &bits, bool weighted, uint32_t max_local,
                                        std::vector<void *> &level_bufs, Level &L, unsigned long long *ovf) {
-    const uint32_t S = part_sample_stride(), nout = L.nout;
+    const uint32_t S = kPartSampleStride, nout = L.nout;
     L.d_ovf = ovf;
     const uint64_t piece = kChunkKeys / S;
     // sample = the first 1/S of every chunk; per parent: keys / sampled keys
@@ -1239,8 +1173,8 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
         const double nl = (double)(1u << bits[t]);
         limit += 1.01 * scale * ((double)sl + 6.0 * std::sqrt(nl * (double)sl) + 9.0 * nl) + 80.0 * nl;
     }
-    const char *dbg = getenv("OKM_PART_CAP_DEBUG");  // tests: shrink capacities to force the exact redo
-    const double mul = dbg ? atof(dbg) : 1.0;
+    const int64_t dbg = test_knob(OKM_TEST_PART_CAP_PERMILLE);  // tests: shrink capacities to force the exact redo
+    const double mul = dbg >= 0 ? (double)dbg / 1000.0 : 1.0;
     // the four host tables travel in one copy
     TablePack pack;
     const size_t o_segs = pack.add(psegs), o_chunks = pack.add(chunks), o_sample = pack.add(sample),
@@ -1833,19 +1767,15 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     // exact table beside them; a context's own folded tables take it too when
     // that fits (C3 on one GPU, two merges of ~5 G pairs: 497 vs 559 ms per
     // job against the exact two-pass count, at the same peak memory)
-    // OKM_MERGE_KERNEL=1: the merge kernel, =2: the two-pass count (tests and
-    // A/B timing); OKM_NO_MERGE_KERNEL: the staged count path always
-    const char *mk = getenv("OKM_MERGE_KERNEL");
-    const int mkv = mk ? atoi(mk) : 0;
-    const bool staged_only = getenv("OKM_NO_MERGE_KERNEL") != nullptr;
+    // OKM_TEST_SORTED_PATH: 1 the merge kernel, 2 the two-pass count (tests)
+    const int64_t mkv = test_knob(OKM_TEST_SORTED_PATH);
     const double need = 2.0 * (8.0 * c->kw + 8.0) * (double)in_total;
-    const bool tight = !staged_only && need > 0.9 * device_room(c);
+    const bool tight = need > 0.9 * device_room(c);
     // weighted runs at the limit: the count kernels in two passes
     // (tools/merge8_cost.py, 8 runs: see DESIGN.md §8)
-    if (!staged_only && weighted && (mkv == 2 || (tight && mkv != 1)))
+    if (weighted && (mkv == 2 || (tight && mkv != 1)))
         return count_sorted_two_pass(c, d_items, d_segs, nitems, in_total, bufs);
-    const bool merge = !staged_only && (mkv == 1 || tight) && R <= merge_max_runs() &&
-                       item_max <= merge_item_capacity();
+    const bool merge = (mkv == 1 || tight) && R <= merge_max_runs() && item_max <= merge_item_capacity();
     if (merge) return merge_sorted_items(c, d_items, d_segs, nitems, in_total, weighted, bufs);
     return count_and_compact(c, d_items, d_segs, nitems, in_total, in_total, weighted, bufs);
 }
@@ -1878,7 +1808,18 @@ static okm_status do_count(okm_ctx *c) {
     if (outer) c->took_runs = false;
     c->may_take_runs = true;
     if (outer) c->share_result = true;
-    const okm_status st = do_count_runs(c);
+    okm_status st = do_count_runs(c);
+    if (st == OKM_E_NOMEM && !c->input_lost && outer) {
+        // out of device memory: every table to host memory, then the key-range
+        // grouped count of count_spilled (the reference's map just grows)
+        bool tables = false;
+        for (auto &r : c->runs) tables |= r.folded && !r.host && !r.borrowed;
+        if (tables) {
+            c->hprof.mark("count_nomem");
+            st = spill_tables(c, INFINITY);
+            if (st == OKM_OK) st = do_count_runs(c);
+        }
+    }
     if (outer) c->may_take_runs = c->share_result = false;
     OKM_TRY(st);
     bool borrowed = false;
@@ -1890,12 +1831,33 @@ static okm_status do_count(okm_ctx *c) {
     return OKM_OK;
 }
 
+static okm_status count_spilled(okm_ctx *c);
+
+// Every run sorted: split by binary search into key-range items (count_sorted),
+// or -- a key range too dense for one item -- partition the runs first.
+static okm_status count_all_sorted(okm_ctx *c) {
+    bool fallback = false;
+    OKM_TRY(count_sorted(c, &fallback));
+    if (!fallback) return OKM_OK;
+    for (auto &r : c->runs) {
+        Run owned;
+        OKM_TRY(partition_pairs(c, r.keys, r.counts, r.n, owned));
+        free_run(c, r);
+        r = std::move(owned);
+    }
+    return count_general(c);
+}
+
 static okm_status do_count_runs(okm_ctx *c) {
     invalidate_result(c);
+    bool any_host = false;
+    for (auto &r : c->runs) any_host |= r.host;
+    if (any_host && !(c->runs.size() == 1 && c->runs[0].folded)) return count_spilled(c);
     if (c->runs.size() == 1 && c->runs[0].folded) {  // nothing added since the fold: its table is the result
         Run &r = c->runs[0];
         c->res_keys = r.keys;
         c->res_counts = r.counts;
+        c->res_host = r.host;
         c->n_res = r.n;
         c->info.distinct = r.n;
         c->runs.clear();
@@ -1931,10 +1893,7 @@ static okm_status do_count_runs(okm_ctx *c) {
         }
         c->timer.end(c->stream, "sorted_copy", 2.0 * (8.0 * c->kw + 8.0) * (double)n);
         OKM_TRY(sync(c));  // a borrowed run may be freed once okm_count returns
-        if (!r.borrowed) {
-            c->pool.put(r.keys);
-            c->pool.put(r.counts);
-        }
+        free_run(c, r);
         c->runs.clear();
         c->n_res = n;
         c->info.distinct = n;
@@ -1944,22 +1903,139 @@ static okm_status do_count_runs(okm_ctx *c) {
         c->res_is_input = true;  // its run is gone: the copy is kept on the next add
         return OKM_OK;
     }
-    if (all_sorted) {
-        bool fallback = false;
-        OKM_TRY(count_sorted(c, &fallback));
-        if (!fallback) return OKM_OK;
-        // a key range too dense for one merge item: partition the sorted runs
-        for (auto &r : c->runs) {
-            Run owned;
-            OKM_TRY(partition_pairs(c, r.keys, r.counts, r.n, owned));
-            if (!r.borrowed) {
-                c->pool.put(r.keys);
-                c->pool.put(r.counts);
-            }
-            r = std::move(owned);
-        }
-    }
+    if (all_sorted) return count_all_sorted(c);
     return count_general(c);
+}
+
+// okm_count with tables in host memory (spill_tables): the batches are
+// counted into one more table first; then the key space is counted in
+// groups of L1 bins sized to the device's room -- each group's slices of the
+// device tables in place and of the host tables copied in, merged by the
+// sorted-run count -- and the groups' tables, in key order, are the result:
+// on the device when it fits there, else in page-locked host memory
+// (okm_fetch_counts / the TSV writer stream it; okm_result_device uploads it
+// or fails with OKM_E_NOMEM).
+static okm_status count_spilled(okm_ctx *c) {
+    bool any_unsorted = false;
+    for (auto &r : c->runs) any_unsorted |= !r.sorted;
+    if (any_unsorted) {
+        OKM_TRY(spill_tables(c, 4.5 * uncounted_bytes(c)));
+        OKM_TRY(count_unsorted_to_table(c));
+    }
+    const uint32_t nb = c->nbins;
+    const uint64_t kw = c->kw;
+    bool weighted = false;
+    std::vector<uint64_t> binlen(nb, 0);
+    for (auto &r : c->runs) {
+        weighted |= r.counts != nullptr;
+        for (uint32_t b = 0; b < nb; ++b) binlen[b] += r.len(b);
+    }
+    // per input pair of a group: its upload (host slices), the sorted count's
+    // staged slots and exact table (count_sorted_plan: ~2 x 16 B), slack
+    const double per_pair = 4.0 * (8.0 * kw + 8.0);
+    const uint64_t gmax = std::max<uint64_t>(1, (uint64_t)(0.6 * device_room(c) / per_pair));
+    std::vector<uint64_t> hk, hc;  // the groups' tables, in key order
+    std::vector<Run> all = std::move(c->runs);
+    c->runs.clear();
+    okm_status st = OKM_OK;
+    uint32_t groups = 0;
+    for (uint32_t b0 = 0; b0 < nb && st == OKM_OK;) {
+        uint32_t b1 = b0;
+        uint64_t pairs = 0;
+        while (b1 < nb && (b1 == b0 || pairs + binlen[b1] <= gmax)) pairs += binlen[b1++];
+        uint64_t host_pairs = 0;
+        for (auto &r : all)
+            if (r.host) host_pairs += r.off[b1] - r.off[b0];
+        uint64_t *uk = nullptr, *uc = nullptr;
+        if (host_pairs) {
+            st = pool_get(c->pool, host_pairs * kw, &uk);
+            if (st == OKM_OK && weighted) st = pool_get(c->pool, host_pairs, &uc);
+        }
+        std::vector<Run> grp;
+        uint64_t at = 0;
+        for (auto &r : all) {
+            if (st != OKM_OK) break;
+            const uint64_t a = r.off[b0], e = r.off[b1];
+            if (a == e) continue;
+            Run t;
+            t.sorted = t.borrowed = true;
+            t.n = e - a;
+            if (r.host) {
+                t.keys = uk + at * kw;
+                t.counts = r.counts ? uc + at : nullptr;
+                if (hipMemcpyAsync(t.keys, r.keys + a * kw, t.n * 8 * kw, hipMemcpyHostToDevice, c->stream) !=
+                        hipSuccess ||
+                    (r.counts &&
+                     hipMemcpyAsync(t.counts, r.counts + a, t.n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess))
+                    st = fail(OKM_E_DEVICE, "count_spilled: host-to-device copy");
+                at += t.n;
+            } else {
+                t.keys = r.keys + a * kw;
+                t.counts = r.counts ? r.counts + a : nullptr;
+            }
+            t.off.assign(nb + 1, 0);
+            for (uint32_t b = 0; b <= nb; ++b) t.off[b] = std::min(std::max(r.off[b], a), e) - a;
+            grp.push_back(std::move(t));
+        }
+        if (st == OKM_OK && !grp.empty()) {
+            c->runs = std::move(grp);
+            c->counted = false;
+            st = count_all_sorted(c);
+            c->runs.clear();
+            if (st == OKM_OK && c->n_res) {  // the group's table off the device, appended in key order
+                const size_t o = hk.size() / kw;
+                hk.resize((o + c->n_res) * kw);
+                hc.resize(o + c->n_res);
+                if (hipMemcpyAsync(hk.data() + o * kw, c->res_keys, c->n_res * 8 * kw, hipMemcpyDeviceToHost,
+                                   c->stream) != hipSuccess ||
+                    hipMemcpyAsync(hc.data() + o, c->res_counts, c->n_res * 8, hipMemcpyDeviceToHost, c->stream) !=
+                        hipSuccess)
+                    st = fail(OKM_E_DEVICE, "count_spilled: device-to-host copy");
+                if (st == OKM_OK) st = sync(c);
+            }
+            invalidate_result(c);
+        }
+        c->pool.put(uk);
+        c->pool.put(uc);
+        ++groups;
+        b0 = b1;
+    }
+    c->runs = std::move(all);
+    OKM_TRY(st);
+    release_runs(c, c->runs);
+    // the result: on the device when it fits beside what is left, else on the host
+    const uint64_t nd = hc.size();
+    if ((double)nd * (8.0 * kw + 8.0) <= 0.8 * device_room(c)) {
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * kw, &c->res_keys));
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        if (nd) {
+            HIP_TRY(hipMemcpyAsync(c->res_keys, hk.data(), nd * 8 * kw, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->res_counts, hc.data(), nd * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        OKM_TRY(sync(c));
+    } else {
+        uint64_t *pk = static_cast<uint64_t *>(host_pinned_alloc(std::max<uint64_t>(nd, 1) * 8 * kw));
+        uint64_t *pc = static_cast<uint64_t *>(host_pinned_alloc(std::max<uint64_t>(nd, 1) * 8));
+        if (!pk || !pc) {
+            host_pinned_free(pk);
+            host_pinned_free(pc);
+            return fail(OKM_E_NOMEM, "count_spilled: page-locked host memory for a " + std::to_string(nd) +
+                                         "-entry table");
+        }
+        std::memcpy(pk, hk.data(), nd * 8 * kw);
+        std::memcpy(pc, hc.data(), nd * 8);
+        c->res_keys = pk;
+        c->res_counts = pc;
+        c->res_host = true;
+        c->host_bytes += nd * 8 * kw + nd * 8;
+    }
+    c->n_res = nd;
+    c->info.distinct = nd;
+    c->info.groups = groups;
+    c->counted = true;
+    c->res_is_input = true;  // every run is gone: the table is kept on the next add
+    c->hprof.mark("count_spilled");
+    return OKM_OK;
 }
 
 // Every run an L1-partitioned batch (or partitioned pairs): key-range passes
@@ -1979,8 +2055,8 @@ static okm_status count_general(okm_ctx *c) {
     bool weighted = false;
     for (auto &r : c->runs) weighted |= (r.counts != nullptr);
     uint32_t maxb = log2_floor(part_max_bins(weighted, c->wide));  // bits one pass can split
-    if (const char *e = getenv("OKM_PART_MAXB"))                // tests: force small passes (fan-out, host rounds)
-        maxb = std::max(1, std::min((int)maxb, atoi(e)));
+    if (const int64_t e = test_knob(OKM_TEST_PART_MAX_BITS); e > 0)  // tests: small passes (fan-out, host rounds)
+        maxb = std::max<uint32_t>(1, std::min<uint32_t>(maxb, (uint32_t)e));
     c->hprof.mark("pre_count");
 
     // initial parts: the L1 bins, each a list of per-run segments
@@ -2053,10 +2129,6 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
             // not uniform inside a part).
             FanOut fan;
             {
-                static const int fan_env = [] {
-                    const char *e = getenv("OKM_FAN_BITS");
-                    return e ? atoi(e) : -1;
-                }();
                 uint32_t fb = 0;
                 for (uint32_t i = 0; i < parts.size(); ++i) {
                     const uint64_t child = 2 * (parts[i].len >> bits[i]);
@@ -2065,7 +2137,6 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                     while (f < 4 && (child >> f) > target) ++f;
                     fb = std::max(fb, f);
                 }
-                if (fan_env >= 0) fb = std::min<uint32_t>(fb, (uint32_t)fan_env);
                 fan.bits = fb;
                 fan.target = target;
                 fan.split_max = fan_split_max();
@@ -2073,7 +2144,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
             c->hprof.mark("split.plan");
             uint64_t keys_in = 0;
             for (const Part &p : parts) keys_in += p.len;
-            const bool try_sampled = part_tile_mode() && part_sample_stride() > 1 && keys_in >= (1ull << 22);
+            const bool try_sampled = keys_in >= (1ull << 22);
             // The level's bins become the items and are counted at once
             // (speculatively: the count kernels check make_items' flags), so
             // the first host sync of the round comes after the compaction.
@@ -2222,8 +2293,8 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
 // one table sized by the instance bound (when it fits beside the runs), or
 // each group gets an exact table and the tables are joined at the end.
 // Needed from ~4 G instances on one GPU (e.g. BASELINE configs[3], k=63 over
-// 5.4 Gbases: 85 GB of L1 runs + 127 GB of result); OKM_GROUP_KEYS /
-// OKM_GROUP_MODE (A: bound table, B: exact tables) force it in tests.
+// 5.4 Gbases: 85 GB of L1 runs + 127 GB of result); OKM_TEST_GROUP_KEYS /
+// OKM_TEST_GROUP_EXACT (0: bound table, 1: exact tables) force it in tests.
 static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::vector<Part> &parts, bool weighted,
                                 const CountPlan &cp) {
     uint64_t total = 0;
@@ -2241,11 +2312,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     const double avail = 0.75 * room;
     uint64_t group_keys = total;
     int mode = 0;  // 0: one group (no grouping)
-    const char *ge = getenv("OKM_GROUP_KEYS");
-    const char *gm = getenv("OKM_GROUP_MODE");
-    if (ge && atoll(ge) > 0) {
-        group_keys = (uint64_t)atoll(ge);
-        mode = (gm && gm[0] == 'B') ? 2 : 1;
+    const int64_t ge = test_knob(OKM_TEST_GROUP_KEYS);
+    if (ge > 0) {
+        group_keys = (uint64_t)ge;
+        mode = test_knob(OKM_TEST_GROUP_EXACT) == 1 ? 2 : 1;
     } else if ((double)total * one_key > avail) {
         // beside a bound-sized table: the 3/4 margin over both (room_a), or —
         // the last resort below, when per-group tables could not be joined —
@@ -2347,7 +2417,6 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     } else {
         nd = 0;
         for (auto &t : tabs) nd += t.n;
-        if (!c->pool.arena_mode()) c->pool.trim();  // the groups' working buffers make room for the joined table
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         uint64_t o = 0;
@@ -2383,6 +2452,29 @@ static bool device_ok(int device, std::string *why) {
     return true;
 }
 
+}  // namespace okm
+
+// l1_batch, once more after making room when the device is out of memory:
+// what is pending is folded into a table and the tables go to host memory.
+static okm_status l1_batch_or_spill(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
+    okm_status st = l1_batch(c, d_seq, n);
+    if (st != OKM_E_NOMEM || c->input_lost) return st;
+    bool pending = false;
+    for (auto &r : c->runs) pending |= !r.sorted;
+    if (pending) OKM_TRY(fold(c));
+    OKM_TRY(spill_tables(c, INFINITY));
+    return l1_batch(c, d_seq, n);
+}
+
+namespace okm {
+okm_status result_view(okm_ctx *c, const uint64_t **keys, const uint64_t **counts, uint64_t *n, bool *on_host) {
+    OKM_TRY(okm_count(c, nullptr));
+    *keys = c->res_keys;
+    *counts = c->res_counts;
+    *n = c->n_res;
+    *on_host = c->res_host;
+    return OKM_OK;
+}
 }  // namespace okm
 
 // ===========================================================================
@@ -2435,29 +2527,6 @@ const char *okm_device_arch(int device) {
     return buf;
 }
 
-// OKM_CU_SLICES=n (experiment): contexts created in turn get streams on
-// disjoint CU subsets (CU i belongs to slice i % n, so every slice spans every
-// XCD), so batches in flight on different contexts run side by side instead
-// of taking the whole chip kernel by kernel.
-static hipError_t create_ctx_stream(int device, hipStream_t *st) {
-    static std::atomic<uint32_t> next{0};
-    const char *e = getenv("OKM_CU_SLICES");
-    const int n = e ? atoi(e) : 0;
-    if (n > 1) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount >= n) {
-            const uint32_t me = next.fetch_add(1) % (uint32_t)n;
-            const int ncu = prop.multiProcessorCount;
-            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-            for (int cu = 0; cu < ncu; ++cu)
-                if ((uint32_t)(cu % n) == me) mask[cu / 32] |= 1u << (cu % 32);
-            return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
-        }
-        (void)hipGetLastError();
-    }
-    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-}
-
 okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint64_t distinct_hint) {
     if (!out) return fail(OKM_E_ARG, "okm_create: out is NULL");
     *out = nullptr;
@@ -2481,19 +2550,17 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
     c->l1_fold = !c->wide && distinct_hint >= (1ull << 30);  // a table this big is built by folding
     set_l1_geometry(c);
     {
-        // fold threshold: OKM_FOLD_BYTES (tests), else 10 % of the device's memory
-        // (the count of the folded runs needs ~4.5x their bytes of working set;
-        // C3 on one GPU: 8 % 596 ms, 10 % 569 ms; 12 % needs key-range groups
-        // and re-maps pool blocks: 2.5 s)
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) (void)hipGetLastError();
+        // fold threshold: OKM_FOLD_BYTES, else a ninth of the device budget (10 %
+        // of HBM at the default 0.9; the count of the folded runs needs ~4.5x their
+        // bytes of working set; C3 on one GPU: 8 % 596 ms, 10 % 569 ms; 12 % needs
+        // key-range groups: 2.5 s)
         const char *fe = getenv("OKM_FOLD_BYTES");
-        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(0.10 * (double)total_b);
+        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(hbm_budget(device) / 9.0);
     }
-    if (create_ctx_stream(device, &c->stream) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->l1cap, (2 * (size_t)extract_max_bins(c->wide) + 2) * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->curpad, (size_t)extract_max_bins(c->wide) * OKM_L1_CUR_STRIDE * sizeof(unsigned long long)) !=
+        hipMalloc(&c->curpad, (size_t)extract_max_bins(c->wide) * kL1CurStride * sizeof(unsigned long long)) !=
             hipSuccess ||
         hipHostMalloc(&c->hpin, kHpinBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->hres, kHresWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
@@ -2511,6 +2578,8 @@ void okm_destroy(okm_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->timer.destroy();
+    invalidate_result(c);  // host tables are freed here; device memory goes with the arena
+    release_runs(c, c->runs);
     c->pool.detach();
     c->pool.release_all();
     if (c->HC) (void)hipFree(c->HC);
@@ -2527,9 +2596,6 @@ void okm_destroy(okm_ctx *c) {
     delete c;
 }
 
-// Tuning hook (not part of the C ABI header): phase cycle totals of an
-// OKM_COUNT_PROF=1 build of the counting kernel; zeroes them.
-extern "C" void okm_debug_count_prof(unsigned long long *out16) { okm::count_prof_read(out16); }
 
 okm_status okm_trim(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
@@ -2543,20 +2609,12 @@ okm_status okm_reset(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(sync(c));
-    static const bool dump = [] {
-        const char *e = getenv("OKM_POOL_DUMP");
-        return e && *e && *e != '0';
-    }();
-    if (dump) c->pool.dump("reset");
     invalidate_result(c);
-    for (auto &r : c->runs) {
-        if (r.borrowed) continue;
-        c->pool.put(r.keys);
-        c->pool.put(r.counts);
-    }
-    c->runs.clear();
+    release_runs(c, c->runs);
     c->info = okm_engine_info{};
+    c->spills = 0;
     c->folds = 0;
+    c->pool.reset_peak();
     c->input_lost = false;
     c->hprof.mark("reset");
     return OKM_OK;
@@ -2593,7 +2651,7 @@ okm_status okm_add_batch(okm_ctx *c, const uint8_t *seq, const uint64_t *offsets
     OKM_TRY(ensure_staging(c, o));
     HIP_TRY(hipMemcpyAsync(c->staging, dst, o, hipMemcpyHostToDevice, c->stream));
     OKM_TRY(before_add(c));
-    return l1_batch(c, c->staging, o);
+    return l1_batch_or_spill(c, c->staging, o);
 }
 
 okm_status okm_add_batch_device(okm_ctx *c, const uint8_t *d_seq, uint64_t n_bytes) {
@@ -2605,9 +2663,9 @@ okm_status okm_add_batch_device(okm_ctx *c, const uint8_t *d_seq, uint64_t n_byt
     if ((reinterpret_cast<uintptr_t>(d_seq) & 15u) != 0) {
         OKM_TRY(ensure_staging(c, n_bytes));
         HIP_TRY(hipMemcpyAsync(c->staging, d_seq, n_bytes, hipMemcpyDeviceToDevice, c->stream));
-        return l1_batch(c, c->staging, n_bytes);
+        return l1_batch_or_spill(c, c->staging, n_bytes);
     }
-    return l1_batch(c, d_seq, n_bytes);
+    return l1_batch_or_spill(c, d_seq, n_bytes);
 }
 
 okm_status okm_add_pairs_device(okm_ctx *c, const uint64_t *d_keys, const uint64_t *d_counts, uint64_t n) {
@@ -2664,35 +2722,137 @@ okm_status okm_count(okm_ctx *c, uint64_t *n_distinct) {
     return OKM_OK;
 }
 
+// A result in host memory (count_spilled) moved to the device, when it fits.
+static okm_status result_to_device(okm_ctx *c) {
+    if (!c->res_host) return OKM_OK;
+    const uint64_t n = c->n_res;
+    uint64_t *dk = nullptr, *dc = nullptr;
+    okm_status st = pool_get(c->pool, std::max<uint64_t>(n, 1) * c->kw, &dk);
+    if (st == OKM_OK) st = pool_get(c->pool, std::max<uint64_t>(n, 1), &dc);
+    if (st != OKM_OK) {
+        c->pool.put(dk);
+        return fail(OKM_E_NOMEM, "the counted table (" + std::to_string(n) +
+                                     " entries) lies in host memory and does not fit on the device: read it with "
+                                     "okm_fetch_counts / okm_finish_counts");
+    }
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(dk, c->res_keys, n * 8 * c->kw, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(dc, c->res_counts, n * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    OKM_TRY(sync(c));
+    host_table_free(c, c->res_keys, c->res_counts, n);
+    c->res_keys = dk;
+    c->res_counts = dc;
+    c->res_host = false;
+    return OKM_OK;
+}
+
 okm_status okm_result_device(okm_ctx *c, const uint64_t **d_keys, const uint64_t **d_counts, uint64_t *n) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     OKM_TRY(okm_count(c, nullptr));
+    OKM_TRY(result_to_device(c));
     if (d_keys) *d_keys = c->res_keys;
     if (d_counts) *d_counts = c->res_counts;
     if (n) *n = c->n_res;
     return OKM_OK;
 }
 
+// count.rs:106-116 over a device range of the result: the entries with count
+// >= min_count (min_count <= 1: all) copied to keys / counts (device or host
+// memory) at most `cap` of them; *m = how many there are (cap == 0 and no
+// outputs: only counted).
+static okm_status fetch_range(okm_ctx *c, const uint64_t *dk, const uint64_t *dc, uint64_t n, uint64_t min_count,
+                              uint64_t *keys, uint64_t *counts, uint64_t cap, uint64_t *m, bool dst_on_device) {
+    *m = 0;
+    if (!n) return OKM_OK;
+    const uint64_t *src_k = dk, *src_c = dc;
+    uint64_t cnt = n;
+    uint64_t *tk = nullptr, *tc = nullptr;
+    if (min_count > 1) {
+        const uint32_t nb = filter_blocks(n);
+        unsigned long long *bc, *bo, *tmp;
+        OKM_TRY(pool_get(c->pool, nb + 1, &bc));
+        OKM_TRY(pool_get(c->pool, nb + 1, &bo));
+        OKM_TRY(pool_get(c->pool, scan_tmp_elems(nb + 1), &tmp));
+        HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
+        launch_filter_count(c->stream, dc, n, min_count, bc, nb);
+        launch_exclusive_scan(c->stream, bc, bo, nb + 1, tmp);
+        unsigned long long tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, bo + nb, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
+        OKM_TRY(sync(c));
+        cnt = tot;
+        if ((keys || counts) && cnt > cap) {
+            c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+            return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
+        }
+        if (cnt && (keys || counts)) {
+            OKM_TRY(pool_get(c->pool, cnt * c->kw, &tk));
+            OKM_TRY(pool_get(c->pool, cnt, &tc));
+            launch_filter_scatter(c->stream, dk, dc, n, min_count, bo, tk, tc, c->wide);
+            HIP_TRY(hipGetLastError());
+        }
+        c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+        src_k = tk;
+        src_c = tc;
+    } else if ((keys || counts) && cnt > cap) {
+        return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
+    }
+    if (cnt && (keys || counts)) {
+        const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        if (keys) HIP_TRY(hipMemcpyAsync(keys, src_k, cnt * 8 * c->kw, kind, c->stream));
+        if (counts) HIP_TRY(hipMemcpyAsync(counts, src_c, cnt * 8, kind, c->stream));
+        OKM_TRY(sync(c));
+    }
+    if (tk) c->pool.put(tk);
+    if (tc) c->pool.put(tc);
+    *m = cnt;
+    return OKM_OK;
+}
+
+// fetch_range over the whole result; a host-resident result goes through the
+// device filter in slices of `kSlice` entries.
+static okm_status fetch_result(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint64_t *counts, uint64_t cap,
+                               uint64_t *n, bool dst_on_device) {
+    *n = 0;
+    if (c->n_res == 0) return OKM_OK;
+    if (!c->res_host)
+        return fetch_range(c, c->res_keys, c->res_counts, c->n_res, min_count, keys, counts, cap, n, dst_on_device);
+    constexpr uint64_t kSlice = uint64_t(1) << 26;
+    const uint64_t sl = std::min<uint64_t>(kSlice, c->n_res);
+    uint64_t *dk = nullptr, *dc = nullptr;
+    OKM_TRY(pool_get(c->pool, sl * c->kw, &dk));
+    okm_status st = pool_get(c->pool, sl, &dc);
+    uint64_t done = 0;
+    for (uint64_t o = 0; o < c->n_res && st == OKM_OK; o += sl) {
+        const uint64_t len = std::min(sl, c->n_res - o);
+        if (hipMemcpyAsync(dk, c->res_keys + o * c->kw, len * 8 * c->kw, hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess ||
+            hipMemcpyAsync(dc, c->res_counts + o, len * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+            st = fail(OKM_E_DEVICE, "okm_fetch_counts: host-to-device copy");
+            break;
+        }
+        uint64_t got = 0;
+        const bool out = keys || counts;
+        st = fetch_range(c, dk, dc, len, min_count, out && keys ? keys + done * c->kw : nullptr,
+                         out && counts ? counts + done : nullptr, out ? cap - done : 0, &got, dst_on_device);
+        done += got;
+    }
+    c->pool.put(dk);
+    c->pool.put(dc);
+    OKM_TRY(st);
+    *n = done;
+    return OKM_OK;
+}
+
 okm_status okm_result_size(okm_ctx *c, uint64_t min_count, uint64_t *n) {
     if (!c || !n) return fail(OKM_E_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(okm_count(c, nullptr));
     if (min_count <= 1 || c->n_res == 0) {
         *n = c->n_res;
         return OKM_OK;
     }
-    const uint32_t nb = filter_blocks(c->n_res);
-    unsigned long long *bc;
-    OKM_TRY(pool_get(c->pool, nb + 1, &bc));
-    HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
-    launch_filter_count(c->stream, c->res_counts, c->n_res, min_count, bc, nb);
-    std::vector<unsigned long long> h(nb);
-    HIP_TRY(hipMemcpyAsync(h.data(), bc, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    OKM_TRY(sync(c));
-    c->pool.put(bc);
-    uint64_t t = 0;
-    for (auto v : h) t += v;
-    *n = t;
-    return OKM_OK;
+    return fetch_result(c, min_count, nullptr, nullptr, 0, n, false);
 }
 
 okm_status okm_fetch_counts(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint64_t *counts, uint64_t cap,
@@ -2701,49 +2861,7 @@ okm_status okm_fetch_counts(okm_ctx *c, uint64_t min_count, uint64_t *keys, uint
     HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(okm_count(c, nullptr));
     *n = 0;
-    if (c->n_res == 0) return OKM_OK;
-    const uint64_t *src_k = c->res_keys, *src_c = c->res_counts;
-    uint64_t m = c->n_res;
-    uint64_t *tk = nullptr, *tc = nullptr;
-    if (min_count > 1) {
-        const uint32_t nb = filter_blocks(c->n_res);
-        unsigned long long *bc, *bo, *tmp;
-        OKM_TRY(pool_get(c->pool, nb + 1, &bc));
-        OKM_TRY(pool_get(c->pool, nb + 1, &bo));
-        OKM_TRY(pool_get(c->pool, scan_tmp_elems(nb + 1), &tmp));
-        HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
-        launch_filter_count(c->stream, c->res_counts, c->n_res, min_count, bc, nb);
-        launch_exclusive_scan(c->stream, bc, bo, nb + 1, tmp);
-        unsigned long long tot = 0;
-        HIP_TRY(hipMemcpyAsync(&tot, bo + nb, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
-        OKM_TRY(sync(c));
-        m = tot;
-        if (m > cap) {
-            c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
-            return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
-        }
-        if (m) {
-            OKM_TRY(pool_get(c->pool, m * c->kw, &tk));
-            OKM_TRY(pool_get(c->pool, m, &tc));
-            launch_filter_scatter(c->stream, c->res_keys, c->res_counts, c->n_res, min_count, bo, tk, tc, c->wide);
-            HIP_TRY(hipGetLastError());
-        }
-        c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
-        src_k = tk;
-        src_c = tc;
-    } else if (m > cap) {
-        return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
-    }
-    if (m) {
-        const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-        if (keys) HIP_TRY(hipMemcpyAsync(keys, src_k, m * 8 * c->kw, kind, c->stream));
-        if (counts) HIP_TRY(hipMemcpyAsync(counts, src_c, m * 8, kind, c->stream));
-    }
-    OKM_TRY(sync(c));
-    if (tk) c->pool.put(tk);
-    if (tc) c->pool.put(tc);
-    *n = m;
-    return OKM_OK;
+    return fetch_result(c, min_count, keys, counts, cap, n, dst_on_device != 0);
 }
 
 okm_status okm_finish_counts(okm_ctx *c, uint64_t min_count, uint64_t **keys, uint64_t **counts, uint64_t *n) {
@@ -2884,7 +3002,10 @@ okm_status okm_engine_info_get(okm_ctx *c, okm_engine_info *info) {
     if (!c || !info) return fail(OKM_E_ARG, "null argument");
     *info = c->info;
     info->folds = c->folds;
-    info->device_bytes = c->pool.held + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    info->device_bytes = c->pool.held() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    info->device_peak_bytes = c->pool.peak() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    info->host_bytes = c->host_bytes;
+    info->spills = c->spills;
     return OKM_OK;
 }
 

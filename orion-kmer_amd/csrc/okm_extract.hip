@@ -40,56 +40,30 @@ __device__ __forceinline__ uint32_t bin_k(uint64_t key, uint32_t shift) {
     return bin_of(key, shift);
 }
 
-#ifndef OKM_EXTRACT_BLOCK
-#define OKM_EXTRACT_BLOCK 1024
-#endif
-#ifndef OKM_EXTRACT_SEG
-#define OKM_EXTRACT_SEG 16
-#endif
-#ifndef OKM_EXTRACT_WPE  // scatter: waves per SIMD the register budget must allow
-#define OKM_EXTRACT_WPE 4
-#endif
-#ifndef OKM_EXTRACT_EXPT  // timing experiments only (tools/extract_only.py): 1 no HBM writes, 2 no staging
-#define OKM_EXTRACT_EXPT 0
-#endif
-#ifndef OKM_EXTRACT_PF_LATE  // scatter: issue that load after the tile's claim, not before it
-#define OKM_EXTRACT_PF_LATE 0
-#endif
-#ifndef OKM_EXTRACT_PREFETCH  // scatter: load the next tile's bytes during this tile
-#define OKM_EXTRACT_PREFETCH 1
-#endif
-constexpr int kExtractBlock = 256;
-constexpr int kScatBlock = OKM_EXTRACT_BLOCK;  // k <= 32 scatter
-constexpr int kSegS = OKM_EXTRACT_SEG;         // scatter: window starts per thread
-constexpr int kTile = kScatBlock * kSegS;      // scatter tile: 16384 windows
-static_assert(kScatBlock >= 256, "one L1 bin per scatter thread");
+constexpr int kExtractBlock = 256;  // histogram kernels
+constexpr int kScatBlock = 1024;    // k <= 32 scatter: one workgroup per CU (128 KiB of staged keys)
+constexpr int kScatWpe = 4;         // ... waves per SIMD its register budget must allow
+constexpr int kSegS = 16;           // scatter: window starts per thread
+constexpr int kTile = kScatBlock * kSegS;  // scatter tile: 16384 windows
 static_assert(kSegS % 16 == 0, "scan_windows loads whole 16-B words");
-#ifndef OKM_EXTRACT_HSEG  // hist: window starts per thread (kHTile must be a multiple of the scatter tile)
-#define OKM_EXTRACT_HSEG 64
-#endif
-constexpr int kSegH = OKM_EXTRACT_HSEG;         // hist: window starts per thread
+constexpr int kSegH = 64;                      // hist: window starts per thread
 constexpr int kHTile = kExtractBlock * kSegH;  // hist tile: 16384 windows
 static_assert(kHTile % kTile == 0, "scatter tile must divide the hist tile");
-#ifndef OKM_L1_BITS  // first-level key-range bins of the k <= 32 extraction (2^bits <= kScatBlock)
-#define OKM_L1_BITS 9  // 8: extraction 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms (C2), C3 724 vs 696 ms
-#endif
-#ifndef OKM_L1_BITS_FOLD  // ... for a context that folds (okm_engine.hip fold(): C3 414 vs 461 ms, C2 5.44 vs 5.23)
-#define OKM_L1_BITS_FOLD 10
-#endif
-constexpr int kMaxL1Bins = 1 << (OKM_L1_BITS_FOLD > OKM_L1_BITS ? OKM_L1_BITS_FOLD : OKM_L1_BITS);  // k <= 32 kernels
-static_assert(2 * 21 - (OKM_L1_BITS_FOLD > OKM_L1_BITS ? OKM_L1_BITS_FOLD : OKM_L1_BITS) >= 32,
-              "bin_k: the L1 shift of k >= 21 lies in the key's high word");
-#ifndef OKM_L1_BITS_W  // first-level bins of the k in 33..64 extraction (2^bits <= OKM_WIDE_SCAT_BLOCK)
-#define OKM_L1_BITS_W 9  // 8: k=63 1 Gbases 39.3 vs 34.8 ms (children past one fan-out job), C4 248 vs 237 ms
-#endif
-constexpr int kMaxL1BinsW = 1 << OKM_L1_BITS_W;  // k in 33..64 kernels
+// First-level key-range bins (2^bits <= the scatter block): 9 bits (8: extraction
+// 1.51 vs 1.56 ms but partition 1.92 vs 1.74 ms on C2, C3 724 vs 696 ms); 10 for a
+// context that folds (okm_engine.hip fold(): C3 414 vs 461 ms, C2 5.44 vs 5.23);
+// k in 33..64: 9 (8: k=63 1 Gbases 39.3 vs 34.8 ms, C4 248 vs 237 ms)
+constexpr int kL1Bits = 9, kL1BitsFold = 10, kL1BitsW = 9;
+constexpr int kMaxL1Bins = 1 << kL1BitsFold;  // k <= 32 kernels
+static_assert(2 * 21 - kL1BitsFold >= 32, "bin_k: the L1 shift of k >= 21 lies in the key's high word");
+constexpr int kMaxL1BinsW = 1 << kL1BitsW;  // k in 33..64 kernels
 static_assert(kMaxL1Bins <= kScatBlock, "one bin per scatter thread");
 
 constexpr uint32_t gcd_u32(uint32_t a, uint32_t b) { return b ? gcd_u32(b, a % b) : a; }
 constexpr uint32_t lcm_u32(uint32_t a, uint32_t b) { return a / gcd_u32(a, b) * b; }
 uint32_t extract_max_bins(bool wide) { return (uint32_t)(wide ? kMaxL1BinsW : kMaxL1Bins); }
 uint32_t extract_l1_bits(bool wide, bool folding) {
-    return wide ? (uint32_t)OKM_L1_BITS_W : (uint32_t)(folding ? OKM_L1_BITS_FOLD : OKM_L1_BITS);
+    return wide ? (uint32_t)kL1BitsW : (uint32_t)(folding ? kL1BitsFold : kL1Bits);
 }
 
 template <int K>
@@ -137,7 +111,7 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
         const uint32_t h = hist[t];
         ull g = ~0ull;
         if (h) {
-            const ull p = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)h);
+            const ull p = atomicAdd(&cursor[t * kL1CurStride], (ull)h);
             if (p + h <= cap_end[t])
                 g = p;
             else
@@ -147,42 +121,16 @@ __device__ __forceinline__ void claim_tile(uint32_t t, uint32_t nb, const uint32
     }
 }
 
-#ifndef OKM_EXTRACT_SHARE  // scatter: each thread codes only its own 16 bytes; the 32-byte halo comes from LDS
-#define OKM_EXTRACT_SHARE 0  // measured: no change (1.483 vs 1.474 ms), 2 VGPRs spill
-#endif
-#ifndef OKM_EXTRACT_STORE_NOWAIT
-#define OKM_EXTRACT_STORE_NOWAIT 0  // measured: 1.495 vs 1.476 ms (no gain)
-#endif
-constexpr unsigned kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0), expcnt / lgkmcnt not waited (gfx9 encoding)
-constexpr bool kShareCodes = OKM_EXTRACT_SHARE && kSegS == 16 && OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE;
-
-// The 16 bytes at w0 as (MSB-first codes, LSB-first complemented codes,
-// invalid-base bits, 0); bytes at or past n are invalid (the clamped load read
-// other bytes there).
-__device__ __forceinline__ uint4 own_codes(const WinWords<kSegS, 0> &b, uint64_t n, uint64_t w0) {
-    Codes<1> c;
-    make_codes<1, false>(b.w, c);
-    const uint64_t avail = w0 < n ? n - w0 : 0;
-    if (avail < 16) mark_tail<1>(c, avail);
-    return make_uint4(c.p[0], c.q[0], (uint32_t)c.bad[0] & 0xFFFFu, 0u);
-}
-
 template <int K>
-__global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_EXTRACT_WPE))) void k_extract_scatter(const uint8_t *__restrict__ seq, ExtractGeom g,
-                                                                   const uint32_t *__restrict__ HC,
-                                                                   ull *__restrict__ cursor,
-                                                                   uint64_t *__restrict__ out,
-                                                                   const ull *__restrict__ cap_end,
-                                                                   ull *__restrict__ ovf) {
+__global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(kScatWpe))) void k_extract_scatter(
+    const uint8_t *__restrict__ seq, ExtractGeom g, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
+    uint64_t *__restrict__ out, const ull *__restrict__ cap_end, ull *__restrict__ ovf) {
     __shared__ ull stage[kTile + 64];        // + one dummy slot per lane for invalid windows
     __shared__ ull gcur[kMaxL1Bins];         // this block's next output index per bin
     __shared__ uint32_t hist[kMaxL1Bins + 1];
     __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
     __shared__ uint32_t lcur[kMaxL1Bins];
     __shared__ ull wsum[kScatBlock / 64];
-    // shared codes: thread t's 16 bytes as (fwd codes, rc codes, invalid bits);
-    // [kScatBlock, +2): the 32 bytes after the tile (the last two threads' halo)
-    __shared__ uint4 xcode[kShareCodes ? kScatBlock + 2 : 1];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     // HC: exact per-block counts (one claim per bin for the whole chunk);
@@ -195,31 +143,14 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
     const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
-    WinWords<kSegS> ww;  // this tile's bytes, loaded one tile ahead (branch-free: load_windows_clamped)
-    WinWords<kSegS, 0> own, extra;  // kShareCodes: this thread's 16 bytes; the halo after the tile (last two threads)
-    // the extra 16 B: threads kScatBlock-2.. load the 32 bytes after the tile; the others
-    // reload their own (a cached line: the load stays unconditional and branch-free)
-    auto extra_at = [&](uint64_t tt0) -> uint64_t {
-        return t >= (uint32_t)kScatBlock - 2 ? tt0 + kTile + (uint64_t)kSegS * (t - (kScatBlock - 2))
-                                              : tt0 + (uint64_t)t * kSegS;
-    };
-    if (kShareCodes) {
-        load_windows_clamped<kSegS, 0>(seq, g.n, beg + (uint64_t)t * kSegS, own);
-        load_windows_clamped<kSegS, 0>(seq, g.n, extra_at(beg), extra);
-    } else if (OKM_EXTRACT_PREFETCH) {
-        load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
-    }
+    // this tile's bytes, loaded one tile ahead by branch-free clamped loads
+    // (load_windows_clamped: bytes past the batch are marked invalid later)
+    WinWords<kSegS> ww;
+    load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
-    // (the first tile's bytes: no loop-carried load is then pending at the loop head,
-    // so the head does not wait for the previous tile's stores; see the copy-out)
-    if (OKM_EXTRACT_STORE_NOWAIT) __builtin_amdgcn_s_waitcnt(kWaitVm0);
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
         for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
-        if (kShareCodes) {  // every thread codes its own 16 bytes once; neighbours read them from LDS
-            xcode[t] = own_codes(own, g.n, w0);
-            if (t >= (uint32_t)kScatBlock - 2) xcode[t + 2] = own_codes(extra, g.n, extra_at(t0));
-        }
         lds_sync();
         const bool live = w0 < end;
         uint32_t tile_n;
@@ -235,36 +166,10 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                 rk[j >> 1] |= (atomicAdd(&hist[b], 1u) & 0xFFFFu) << (16 * (j & 1));
                 vm |= valid ? 1u << j : 0u;
             };
-            if (kShareCodes) {
-                if (live) {
-                    constexpr int NP = WinWords<kSegS>::kLoad / 16;  // 3: own 16 bytes + a 32-byte halo
-                    Codes<NP> c;
-                    uint64_t bad = 0;
-#pragma unroll
-                    for (int i = 0; i < NP; ++i) {
-                        const uint4 x = xcode[t + i];
-                        c.p[i] = x.x;
-                        c.q[i] = x.y;
-                        bad |= (uint64_t)x.z << (16 * i);
-                    }
-                    c.bad[0] = bad;
-                    c.bad[1] = 0;
-                    const uint32_t k = K ? (uint32_t)K : g.k;
-                    const uint32_t inv = invalid_windows<kSegS, NP>(c, k);
-#pragma unroll
-                    for (int j = 0; j < kSegS; ++j) emit(j, window_key_nv(c, j, k), ((inv >> j) & 1u) == 0);
-                }
-                // next tile's bytes, in flight meanwhile
-                load_windows_clamped<kSegS, 0>(seq, g.n, w0 + kTile, own);
-                load_windows_clamped<kSegS, 0>(seq, g.n, extra_at(t0 + kTile), extra);
-            } else {
-                if (!OKM_EXTRACT_PREFETCH && live) load_windows_clamped<kSegS>(seq, g.n, w0, ww);
-                if (live) scan_words<kSegS, K>(ww, g.k, emit, g.n - w0);
-                // next tile, in flight meanwhile; unconditional (a clamped load past the
-                // end is harmless), so the loaded registers need no merge copies
-                if (OKM_EXTRACT_PREFETCH && !OKM_EXTRACT_PF_LATE)
-                    load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
-            }
+            if (live) scan_words<kSegS, K>(ww, g.k, emit, g.n - w0);
+            // next tile, in flight meanwhile; unconditional (a clamped load past the
+            // end is harmless), so the loaded registers need no merge copies
+            load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
             lds_sync();
             tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
             // sampled capacities: issue this tile's claim now, consume it after the staging
@@ -272,14 +177,14 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
             ull cp;
             if (!HC && t < nb) {
                 ch = hist[t];
-                cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);  // + 0 when empty: no branch
+                cp = atomicAdd(&cursor[t * kL1CurStride], (ull)ch);  // + 0 when empty: no branch
             }
             lds_sync();
 #pragma unroll
             for (int j = 0; j < kSegS; ++j) {
                 const uint32_t rank = (rk[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
                 const uint32_t dst = (vm >> j) & 1u ? lofs[bin_k<K>(kk[j], shift)] + rank : (uint32_t)kTile + (t & 63u);
-                if (OKM_EXTRACT_EXPT != 2 || kk[j] == 0x123456789ull) stage[dst] = kk[j];
+                stage[dst] = kk[j];
             }
             if (!HC && t < nb) {
                 const bool fits = ch && cp + ch <= capb;
@@ -287,20 +192,13 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(OKM_
                 gcur[t] = fits ? cp : ~0ull;
             }
         }
-        // late prefetch: after the claim's returning atomic was consumed (vmcnt
-        // retires in order, so waiting for the claim waits for any load before it)
-        if (OKM_EXTRACT_PREFETCH && OKM_EXTRACT_PF_LATE) load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
-        // the next tile's bytes are waited for HERE, before this tile's stores: vmcnt
-        // retires in issue order, so a wait at the next tile's first use would also
-        // wait for every store of the copy-out below to complete
-        if (OKM_EXTRACT_STORE_NOWAIT) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         lds_sync();
         // each bin's keys are contiguous in `stage` and go to a contiguous run
-        for (uint32_t j = t; j < (OKM_EXTRACT_EXPT == 2 ? 0u : tile_n); j += kScatBlock) {
+        for (uint32_t j = t; j < tile_n; j += kScatBlock) {
             const ull key = stage[j];
             const uint32_t b = bin_k<K>(key, shift);
             const ull gb = gcur[b];
-            if (gb != ~0ull && (OKM_EXTRACT_EXPT != 1 || key == 0x123456789ull)) out[gb + (j - lofs[b])] = key;
+            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
         lds_sync();
         if (HC && t < nb) gcur[t] += hist[t];
@@ -311,7 +209,7 @@ __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__
                                                          uint64_t *__restrict__ keys, const ull *__restrict__ cap) {
     const uint32_t b = blockIdx.x * 16 + (threadIdx.x >> 4), j = threadIdx.x & 15;
     if (b >= nbins) return;
-    const ull e = end[cap ? b * OKM_L1_CUR_STRIDE : b];
+    const ull e = end[cap ? b * kL1CurStride : b];
     if (cap && e > cap[b]) return;  // an overflowed bin (the batch is redone)
     if (e + j < ((e + 15) & ~15ull)) keys[e + j] = kEmptyKey;
 }
@@ -320,13 +218,9 @@ __global__ __launch_bounds__(256) void k_fill_line_tails(const ull *__restrict__
 // k in 33..64: two-u64 keys (K128, MSB-first over 2k bits), runtime k
 // ---------------------------------------------------------------------------
 
-constexpr int kSegW = 16;                       // scatter windows per thread
-constexpr int kTileW = kExtractBlock * kSegW;   // 4096 windows: 64 KiB stage
-#ifndef OKM_WIDE_SCAT_BLOCK  // single-sweep wide scatter: threads per workgroup (tile = 16 windows each)
-#define OKM_WIDE_SCAT_BLOCK 512
-#endif
-constexpr int kScatBlockW = OKM_WIDE_SCAT_BLOCK;
-constexpr int kTileW1 = kScatBlockW * kSegW;     // 256 threads: 64 KiB stage; 512: 128 KiB (one per CU)
+constexpr int kSegW = 16;                    // scatter windows per thread
+constexpr int kScatBlockW = 512;             // wide scatter: threads per workgroup
+constexpr int kTileW1 = kScatBlockW * kSegW;  // 8192 windows: 128 KiB of staged K128 keys (one workgroup per CU)
 static_assert(kScatBlockW >= kMaxL1BinsW, "one L1 bin per wide scatter thread");
 // chunks are multiples of every tile (the hist walks kHTile steps, the scatters kTile / kTileW1 steps)
 uint32_t extract_tile() { return lcm_u32(lcm_u32((uint32_t)kHTile, (uint32_t)kTile), (uint32_t)kTileW1); }
@@ -378,73 +272,13 @@ __global__ __launch_bounds__(kExtractBlock) void k_extract_hist_wide(const uint8
     }
 }
 
-__global__ __launch_bounds__(kExtractBlock) void k_extract_scatter_wide(const uint8_t *__restrict__ seq,
-                                                                        ExtractGeom g,
-                                                                        const uint32_t *__restrict__ HC,
-                                                                        ull *__restrict__ cursor,
-                                                                        K128 *__restrict__ out,
-                                                                        const ull *__restrict__ cap_end,
-                                                                        ull *__restrict__ ovf) {
-    __shared__ K128 stage[kTileW];
-    __shared__ ull gcur[kMaxL1BinsW];
-    __shared__ uint32_t hist[kMaxL1BinsW + 1];
-    __shared__ uint32_t lofs[kMaxL1BinsW];
-    __shared__ uint32_t lcur[kMaxL1BinsW];
-    __shared__ ull wsum[kExtractBlock / 64];
-    const uint32_t t = threadIdx.x;
-    const uint32_t nb = g.nbins;
-    // HC: exact per-block counts (one claim per bin for the whole chunk);
-    // HC == nullptr: sampled capacities, one claim per (tile, bin), checked
-    // against cap_end (a run that would cross it is dropped and *ovf set)
-    if (t < nb && HC) {
-        const uint32_t h = HC[(uint64_t)blockIdx.x * nb + t];
-        gcur[t] = h ? atomicAdd(&cursor[t], (ull)h) : 0ull;
-    }
-    const uint64_t beg = (uint64_t)blockIdx.x * g.chunk;
-    const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
-    const uint32_t shift = g.shift;
-    for (uint64_t t0 = beg; t0 < end; t0 += kTileW) {
-        for (uint32_t b = t; b <= nb; b += blockDim.x) hist[b] = 0;  // + the dummy bin (nb may equal the block)
-        lds_sync();
-        const uint64_t w0 = t0 + (uint64_t)t * kSegW;
-        const bool live = w0 < end;
-        if (live)
-            scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
-                atomicAdd(&hist[valid ? bin_of_wide(key, shift) : nb], 1u);
-            });
-        lds_sync();
-        const uint32_t tile_n = tile_offsets<kExtractBlock>(t, nb, hist, lofs, lcur, wsum);
-        if (!HC) claim_tile(t, nb, hist, cursor, cap_end, ovf, gcur);
-        lds_sync();
-        if (live)
-            scan_windows_wide<kSegW>(seq, g.n, w0, g.k, [&](int, const K128 &key, bool valid) {
-                if (valid) stage[atomicAdd(&lcur[bin_of_wide(key, shift)], 1u)] = key;
-            });
-        lds_sync();
-        for (uint32_t j = t; j < tile_n; j += kExtractBlock) {
-            const K128 key = stage[j];
-            const uint32_t b = bin_of_wide(key, shift);
-            const ull gb = gcur[b];
-            if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
-        }
-        lds_sync();
-        if (HC && t < nb) gcur[t] += hist[t];
-    }
-}
-
-// Single sweep (OKM_WIDE_SWEEP1, default; OKM_WIDE_SCAT_BLOCK = 512 threads, so an
-// 8192-window tile: 128 KiB of staged keys, 512-B runs per bin; 256 threads
-// measured 7.09 vs 6.29 ms at 1 Gbases, k=63): the 16 keys of a thread and their
-// within-bin ranks (returned by the histogram atomic) stay in registers, as
-// in k_extract_scatter, so each window is extracted once and the second LDS
-// atomic pass of the two-sweep kernel above is gone; the next tile's bytes
-// are loaded while this tile is staged and written.
-#ifndef OKM_WIDE_SWEEP1
-#define OKM_WIDE_SWEEP1 1
-#endif
-#ifndef OKM_WIDE_SHARE  // single sweep: each thread codes its own 16 bytes once (halo codes from LDS)
-#define OKM_WIDE_SHARE 1
-#endif
+// Single sweep (512-thread workgroups, so an 8192-window tile: 128 KiB of
+// staged keys, 512-B runs per bin; 256 threads measured 7.09 vs 6.29 ms at 1
+// Gbases, k=63): the 16 keys of a thread and their within-bin ranks (returned
+// by the histogram atomic) stay in registers, as in k_extract_scatter, so each
+// window is extracted once; each thread codes only its own 16 bytes (the
+// 64-byte halo's codes come from its next four neighbours' LDS slots); the
+// next tile's bytes are loaded while this tile is staged and written.
 // The 16 bytes at w0 as (MSB-first codes, LSB-first complemented codes,
 // invalid-base bits, 0); bytes at or past n are invalid.
 __device__ __forceinline__ uint4 slot_codes(const uint32_t (&w)[4], uint64_t n, uint64_t w0) {
@@ -467,11 +301,11 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     __shared__ uint32_t lofs[kMaxL1BinsW];
     __shared__ uint32_t lcur[kMaxL1BinsW];
     __shared__ ull wsum[kScatBlockW / 64];
-    // OKM_WIDE_SHARE: each thread codes only its own 16 bytes; the 64-byte halo's
-    // codes come from its next four neighbours' slots ([kScatBlockW, +4): the 64
-    // bytes after the tile, coded by the last four threads)
+    // each thread codes only its own 16 bytes; the 64-byte halo's codes come
+    // from its next four neighbours' slots ([kScatBlockW, +4): the 64 bytes
+    // after the tile, coded by the last four threads)
     constexpr int kXS = 4;  // halo slots: 64 bytes
-    __shared__ uint4 xcode[OKM_WIDE_SHARE ? kScatBlockW + kXS : 1];
+    __shared__ uint4 xcode[kScatBlockW + kXS];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
     if (t < nb && HC) {
@@ -482,27 +316,20 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
     const uint64_t end = beg + g.chunk < g.n ? beg + g.chunk : g.n;
     const uint32_t shift = g.shift;
     constexpr int NP = WinWords<kSegW, 64>::kLoad / 16;
-    static_assert(!OKM_WIDE_SHARE || (kSegW == 16 && NP == 1 + kXS), "one 16-byte slot per thread");
-    WinWords<kSegW, 64> ww;  // this tile's bytes, loaded one tile ahead (branch-free, as k_extract_scatter)
-    WinWords<kSegW, 0> own, extra;  // OKM_WIDE_SHARE: this thread's 16 bytes; a halo slot after the tile
+    static_assert(kSegW == 16 && NP == 1 + kXS, "one 16-byte slot per thread");
+    WinWords<kSegW, 0> own, extra;  // this thread's 16 bytes; a halo slot after the tile (one tile ahead)
     auto extra_at = [&](uint64_t tt0) -> uint64_t {  // the last kXS threads: the bytes after the tile
         return t >= (uint32_t)(kScatBlockW - kXS) ? tt0 + kTileW1 + (uint64_t)kSegW * (t - (kScatBlockW - kXS))
                                                    : tt0 + (uint64_t)t * kSegW;
     };
-    if (OKM_WIDE_SHARE) {
-        load_windows_clamped<kSegW, 0>(seq, g.n, beg + (uint64_t)t * kSegW, own);
-        load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(beg), extra);
-    } else {
-        load_windows_clamped<kSegW, 64>(seq, g.n, beg + (uint64_t)t * kSegW, ww);
-    }
+    load_windows_clamped<kSegW, 0>(seq, g.n, beg + (uint64_t)t * kSegW, own);
+    load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(beg), extra);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
     for (uint64_t t0 = beg; t0 < end; t0 += kTileW1) {
         for (uint32_t b = t; b <= nb; b += blockDim.x) hist[b] = 0;  // + the dummy bin (nb may equal the block)
         const uint64_t w0 = t0 + (uint64_t)t * kSegW;
-        if (OKM_WIDE_SHARE) {
-            xcode[t] = slot_codes(own.w, g.n, w0);
-            if (t >= (uint32_t)(kScatBlockW - kXS)) xcode[t + kXS] = slot_codes(extra.w, g.n, extra_at(t0));
-        }
+        xcode[t] = slot_codes(own.w, g.n, w0);
+        if (t >= (uint32_t)(kScatBlockW - kXS)) xcode[t + kXS] = slot_codes(extra.w, g.n, extra_at(t0));
         lds_sync();
         const bool live = w0 < end;
         uint32_t tile_n;
@@ -514,19 +341,14 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
             for (int j = 0; j < kSegW / 2; ++j) rk[j] = 0;
             if (live) {
                 Codes<NP> c;
-                if (OKM_WIDE_SHARE) {
 #pragma unroll
-                    for (int i = 0; i < (NP * 16 + 63) / 64 + 1; ++i) c.bad[i] = 0;
+                for (int i = 0; i < (NP * 16 + 63) / 64 + 1; ++i) c.bad[i] = 0;
 #pragma unroll
-                    for (int i = 0; i < NP; ++i) {
-                        const uint4 x = xcode[t + i];
-                        c.p[i] = x.x;
-                        c.q[i] = x.y;
-                        c.bad[i >> 2] |= (uint64_t)x.z << (16 * (i & 3));
-                    }
-                } else {
-                    make_codes<NP, false>(ww.w, c);
-                    if (g.n - w0 < (uint64_t)WinWords<kSegW, 64>::kLoad) mark_tail<NP>(c, g.n - w0);
+                for (int i = 0; i < NP; ++i) {
+                    const uint4 x = xcode[t + i];
+                    c.p[i] = x.x;
+                    c.q[i] = x.y;
+                    c.bad[i >> 2] |= (uint64_t)x.z << (16 * (i & 3));
                 }
 #pragma unroll
                 for (int j = 0; j < kSegW; ++j) {
@@ -538,19 +360,16 @@ __global__ __launch_bounds__(kScatBlockW) void k_extract_scatter_wide1(const uin
                     vm |= valid ? 1u << j : 0u;
                 }
             }
-            if (OKM_WIDE_SHARE) {  // next tile, in flight (harmless past the end)
-                load_windows_clamped<kSegW, 0>(seq, g.n, w0 + kTileW1, own);
-                load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(t0 + kTileW1), extra);
-            } else {
-                load_windows_clamped<kSegW, 64>(seq, g.n, w0 + kTileW1, ww);
-            }
+            // next tile, in flight (harmless past the end)
+            load_windows_clamped<kSegW, 0>(seq, g.n, w0 + kTileW1, own);
+            load_windows_clamped<kSegW, 0>(seq, g.n, extra_at(t0 + kTileW1), extra);
             lds_sync();
             tile_n = tile_offsets<kScatBlockW>(t, nb, hist, lofs, lcur, wsum);
             uint32_t ch = 0;
             ull cp;
             if (!HC && t < nb) {
                 ch = hist[t];
-                cp = atomicAdd(&cursor[t * OKM_L1_CUR_STRIDE], (ull)ch);  // + 0 when empty: no branch
+                cp = atomicAdd(&cursor[t * kL1CurStride], (ull)ch);  // + 0 when empty: no branch
             }
             lds_sync();
 #pragma unroll
@@ -582,7 +401,7 @@ __global__ __launch_bounds__(256) void k_fill_line_tails_wide(const ull *__restr
                                                               K128 *__restrict__ keys, const ull *__restrict__ cap) {
     const uint32_t b = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
     if (b >= nbins) return;
-    const ull e = end[cap ? b * OKM_L1_CUR_STRIDE : b];
+    const ull e = end[cap ? b * kL1CurStride : b];
     if (cap && e > cap[b]) return;
     if (e + j < ((e + 7) & ~7ull)) keys[e + j] = KeyOps<K128>::empty();
 }
@@ -614,12 +433,8 @@ void launch_extract_scatter(void *stream, const uint8_t *seq, const ExtractGeom 
                             const unsigned long long *cap_end, unsigned long long *ovf) {
     hipStream_t s = (hipStream_t)stream;
     if (g.k > 32) {
-        if (OKM_WIDE_SWEEP1 || kMaxL1BinsW > kExtractBlock)  // the two-sweep kernel holds <= 256 bins
-            hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kScatBlockW), 0, s, seq, g, HC,
-                               cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
-        else
-            hipLaunchKernelGGL(k_extract_scatter_wide, dim3(g.nblocks), dim3(kExtractBlock), 0, s, seq, g, HC,
-                               cursor, reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
+        hipLaunchKernelGGL(k_extract_scatter_wide1, dim3(g.nblocks), dim3(kScatBlockW), 0, s, seq, g, HC, cursor,
+                           reinterpret_cast<K128 *>(out_keys), cap_end, ovf);
         return;
     }
     switch (g.k) {
@@ -669,7 +484,7 @@ __global__ __launch_bounds__(256) void k_l1_capacity(const ull *__restrict__ Hs,
             const ull st = o < limit ? o : limit;
             o += cap[b];
             const ull en = o < limit ? o : limit;
-            cursor[b * OKM_L1_CUR_STRIDE] = st;
+            cursor[b * kL1CurStride] = st;
             l1cap[b] = en;
             l1cap[nb + b] = st;
         }

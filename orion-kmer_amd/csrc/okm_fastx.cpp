@@ -294,7 +294,7 @@ okm_status okm_reader_next(okm_reader *r, uint64_t max_bytes, const uint8_t **se
     auto T1 = std::chrono::steady_clock::now();
     r->p.emit(spans, r->seq, r->off);
     auto T2 = std::chrono::steady_clock::now();
-    if (getenv("OKM_PROF_READER"))
+    if (prof_host())
         fprintf(stderr, "reader: spans %.3f ms emit %.3f ms (%zu records)\n",
                 std::chrono::duration<double, std::milli>(T1 - T0).count(),
                 std::chrono::duration<double, std::milli>(T2 - T1).count(), spans.size());

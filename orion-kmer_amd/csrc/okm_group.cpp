@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "okm_internal.h"
+#include "orion_kmer_testing.h"
 #include "okm_io.h"
 
 namespace {
@@ -303,16 +304,18 @@ okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t m
         const uint64_t *k, *c;
         uint64_t n;
         int device;  // the owning GPU: the copy runs on its device, not device 0's
+        bool host;   // a table count_spilled left in host memory
     };
     std::vector<Chunk> chunks;
     uint64_t per = uint64_t(1) << 24;  // entries per chunk (256 MB of keys + counts at k <= 32)
-    if (const char *e = getenv("OKM_TSV_CHUNK")) per = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
+    if (const int64_t e = okm::test_knob(OKM_TEST_TSV_CHUNK); e > 0) per = std::max<uint64_t>(1024, (uint64_t)e);
     for (auto &W : g->w) {
         const uint64_t *dk = nullptr, *dc = nullptr;
         uint64_t n = 0;
-        if ((s = okm_result_device(W.ctx, &dk, &dc, &n)) != OKM_OK) return s;
+        bool host = false;
+        if ((s = okm::result_view(W.ctx, &dk, &dc, &n, &host)) != OKM_OK) return s;
         for (uint64_t o = 0; o < n; o += per)
-            chunks.push_back({dk + o * kw, dc + o, std::min(per, n - o), okm::ctx_device(W.ctx)});
+            chunks.push_back({dk + o * kw, dc + o, std::min(per, n - o), okm::ctx_device(W.ctx), host});
     }
     uint64_t cap = 0;
     for (auto &c : chunks) cap = std::max(cap, c.n);
@@ -349,8 +352,14 @@ okm_status okm_group_write_counts_tsv(okm_group *g, const char *path, uint64_t m
                 cv.wait(lk, [&] { return stop || i < consumed + 2; });
                 if (stop) return;
             }
-            okm_status st = okm::memcpy_d2h_on(chunks[i].device, sl.k, chunks[i].k, chunks[i].n * kw * 8);
-            if (st == OKM_OK) st = okm::memcpy_d2h_on(chunks[i].device, sl.c, chunks[i].c, chunks[i].n * 8);
+            okm_status st = OKM_OK;
+            if (chunks[i].host) {
+                memcpy(sl.k, chunks[i].k, chunks[i].n * kw * 8);
+                memcpy(sl.c, chunks[i].c, chunks[i].n * 8);
+            } else {
+                st = okm::memcpy_d2h_on(chunks[i].device, sl.k, chunks[i].k, chunks[i].n * kw * 8);
+                if (st == OKM_OK) st = okm::memcpy_d2h_on(chunks[i].device, sl.c, chunks[i].c, chunks[i].n * 8);
+            }
             std::lock_guard<std::mutex> lk(mu);
             if (st != OKM_OK) {
                 copy_st = st;

@@ -44,6 +44,7 @@
 
 #include "okm_internal.h"
 #include "okm_io.h"
+#include "orion_kmer_testing.h"
 
 namespace okm {
 
@@ -478,21 +479,21 @@ size_t gzip_header_len(const uint8_t *in, size_t n) {
 
 }  // namespace
 
-// OKM_GZ_PAR_MIN_MB: smallest member inflated in parallel (default 16 MiB);
-// OKM_GZ_CHUNK_KB: compressed bytes per chunk (default 4 MiB; tests go lower).
-static size_t env_size(const char *name, size_t dflt, size_t unit) {
-    const char *e = getenv(name);
-    return e && *e ? (size_t)atoll(e) * unit : dflt;
+// Smallest member inflated in parallel (16 MiB) and compressed bytes per
+// chunk (4 MiB); tests go lower (OKM_TEST_GZ_PAR_MIN_BYTES / _CHUNK_BYTES).
+static size_t knob_or(int knob, size_t dflt) {
+    const int64_t v = test_knob(knob);
+    return v >= 0 ? (size_t)v : dflt;
 }
 
 okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_t *used, bool *applied) {
     *applied = false;
     *used = 0;
     const int nt = host_threads();
-    const char *off = getenv("OKM_GZ_PARALLEL");
-    const bool forced = off && *off == '2';  // tests: also on one thread
+    const char *off = getenv("OKM_GZ_PARALLEL");  // 0: serial inflate
+    const bool forced = test_knob(OKM_TEST_GZ_STRICT) == 1;  // tests: also on one thread
     if ((off && *off == '0') || (nt < 2 && !forced) ||
-        n < std::max<size_t>(env_size("OKM_GZ_PAR_MIN_MB", 16u << 20, 1u << 20), 1 << 12))
+        n < std::max<size_t>(knob_or(OKM_TEST_GZ_PAR_MIN_BYTES, 16u << 20), 1 << 12))
         return OKM_OK;
     const size_t h = gzip_header_len(in, n);
     if (!h) return OKM_OK;
@@ -500,7 +501,7 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
     const uint8_t *p = in + h;
     const size_t nbytes = n - h;
     // chunk cuts in compressed bytes: ~4 MiB each, at least two per thread
-    const size_t cb = std::max<size_t>(env_size("OKM_GZ_CHUNK_KB", 4u << 20, 1u << 10), 1 << 10);
+    const size_t cb = std::max<size_t>(knob_or(OKM_TEST_GZ_CHUNK_BYTES, 4u << 20), 1 << 10);
     const size_t want = std::max<size_t>(2 * (size_t)nt, nbytes / cb);
     const size_t nch = std::max<size_t>(1, std::min<size_t>(want, nbytes / std::min<size_t>(cb, 1 << 16) + 1));
     std::vector<size_t> cut(nch + 1);
@@ -508,8 +509,8 @@ okm_status gunzip_member_parallel(const uint8_t *in, size_t n, Bytes &out, size_
     cut[nch] = SIZE_MAX;
     // rounds of R chunks: the 16-bit pieces of one round at a time (host memory
     // stays ~R x 4 MiB x 12 B whatever the member's size)
-    const size_t R = std::max<size_t>(2, env_size("OKM_GZ_ROUND_CHUNKS", 2 * (size_t)nt, 1));
-    const bool prof = getenv("OKM_GZ_PROF") != nullptr;
+    const size_t R = std::max<size_t>(2, 2 * (size_t)nt);
+    const bool prof = prof_host();
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t_dec = 0, t_res = 0, t_crc = 0;
     size_t rounds = 0, used_pieces = 0, dropped = 0;

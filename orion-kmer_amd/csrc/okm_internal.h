@@ -24,9 +24,17 @@ void host_pinned_free(void *p);
 // Device-to-host copy issued on `device` (this thread's current device is set
 // to it first, so the copy does not queue behind device 0's null stream).
 okm_status memcpy_d2h_on(int device, void *dst, const void *src, size_t bytes);
+// Test hook value (orion_kmer_testing.h okm_test_knob), -1 when unset.
+int64_t test_knob(int knob);
+
 // Give back the idle device memory every context's pool on `device` caches
 // (a hipMalloc outside the pools, e.g. a communicator buffer, retries after it).
 void trim_device_pools(int device);
+
+// The counted table where it lies: device memory, or (*on_host) page-locked
+// host memory when count_spilled left it there (okm_group_write_counts_tsv
+// streams either without moving it).
+okm_status result_view(okm_ctx *c, const uint64_t **keys, const uint64_t **counts, uint64_t *n, bool *on_host);
 
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);
@@ -72,11 +80,9 @@ struct DevItem {
     const uint64_t *counts0; //   dependent segment load in the count kernels)
 };
 
-// Sampled L1 placement: bin b's claim cursor lives at cursor[b * OKM_L1_CUR_STRIDE]
-// (a stride > 1 puts every cursor on its own 128-B line).
-#ifndef OKM_L1_CUR_STRIDE
-#define OKM_L1_CUR_STRIDE 1
-#endif
+// Sampled L1 placement: bin b's claim cursor lives at cursor[b * kL1CurStride]
+// (a stride > 1, every cursor on its own 128-B line, measured no faster).
+constexpr uint32_t kL1CurStride = 1;
 
 struct ExtractGeom {
     uint64_t n;        // bytes in the batch
@@ -113,7 +119,6 @@ void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunk
                          uint32_t nchunks, uint32_t max_local, const uint32_t *HC,
                          unsigned long long *cursor, uint64_t *out_keys, uint64_t *out_counts, bool wide,
                          const unsigned long long *cap_end = nullptr, unsigned long long *ovf = nullptr);
-bool part_tile_mode();
 // Sampled partition capacities: H[b] (sampled count of output bin b) becomes
 // the bin's capacity (in place); parents sorted by out_base.
 struct DevCapParent {
@@ -145,7 +150,6 @@ void launch_exclusive_scan(void *stream, const unsigned long long *in, unsigned 
 // deferred-item count (both zeroed before the launch).  An item holds at most count_item_capacity() instances unless
 // its rem_bits <= count_dense_bits() (direct-address counting, any size).
 uint32_t count_item_capacity();
-void count_prof_read(unsigned long long *out16);  // OKM_COUNT_PROF builds only
 uint32_t count_dense_bits();
 // ctl[1] counts deferred items (list `defer`, nitems entries) for the second
 // kernel of the launch.

@@ -36,6 +36,7 @@
 
 #include "okm_io.h"
 #include "okm_internal.h"
+#include "orion_kmer_testing.h"
 
 namespace okm {
 
@@ -164,7 +165,7 @@ static Deflate *deflate_lib() {
     static bool tried = false;
     if (!tried) {
         tried = true;
-        if (!getenv("OKM_NO_LIBDEFLATE")) D.h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (test_knob(OKM_TEST_NO_LIBDEFLATE) != 1) D.h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (D.h && !(bind(D.h, "libdeflate_alloc_decompressor", D.alloc_decompressor) &&
                      bind(D.h, "libdeflate_free_decompressor", D.free_decompressor) &&
                      bind(D.h, "libdeflate_gzip_decompress_ex", D.gzip_decompress_ex) &&
@@ -209,7 +210,7 @@ static bool bgzf_members(const uint8_t *in, size_t n, std::vector<size_t> &mb, s
 }
 
 // A member inflated on the host threads (okm_inflate.cpp): true when that
-// path took it (pos advanced past it, or st set under OKM_GZ_PARALLEL=2, which
+// path took it (pos advanced past it, or st set under OKM_TEST_GZ_STRICT, which
 // makes a rejected member an error instead of a serial retry: tests).
 static bool member_parallel(const uint8_t *in, size_t n, size_t &pos, Bytes &out, okm_status &st) {
     const size_t base = out.size();
@@ -223,8 +224,7 @@ static bool member_parallel(const uint8_t *in, size_t n, size_t &pos, Bytes &out
         return true;
     }
     out.resize(base);
-    const char *e = getenv("OKM_GZ_PARALLEL");
-    if (e && *e == '2') {
+    if (test_knob(OKM_TEST_GZ_STRICT) == 1) {
         st = s;
         return true;
     }
@@ -449,6 +449,14 @@ int host_threads() {
         n = std::max(1, std::min(v > 0 ? v : 1, 16));
     }
     return n;
+}
+
+bool prof_host() {
+    static const bool on = [] {
+        const char *e = getenv("OKM_PROFILE_HOST");
+        return e && *e && *e != '0';
+    }();
+    return on;
 }
 
 okm_status read_whole_file(const std::string &path, Bytes &data) {

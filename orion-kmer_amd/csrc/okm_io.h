@@ -33,6 +33,8 @@ using Bytes = std::vector<uint8_t, DefaultInitAlloc<uint8_t>>;
 // Host worker threads for the feed (parse, normalise, (de)compress, format):
 // OKM_HOST_THREADS, else OMP_NUM_THREADS, else the hardware's, capped at 16.
 int host_threads();
+// OKM_PROFILE_HOST=1: host-phase wall times on stderr.
+bool prof_host();
 
 // Run f(i) for i in [0, n) on up to host_threads() threads (dynamic).
 template <typename F> void parallel_for(size_t n, F &&f) {

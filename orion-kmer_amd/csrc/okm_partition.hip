@@ -1,54 +1,31 @@
 // okm_partition.hip — key-range partition passes over key arrays.
 //
 // Splits every segment of a pass into 2^b sub-ranges of its keys (the next b
-// key bits below the segment's common prefix) with exact placement:
-//   part_hist    per chunk (64 Ki keys) and local bin: key count -> HC, and
-//                the count rounded up to a 128-B line -> Hg (bin totals);
-//   (device)     exclusive scan of Hg -> every output bin starts on a line;
-//   part_scatter each chunk claims a line-aligned slice per bin, appends keys
-//                to per-bin one-line LDS buffers and writes each full buffer
-//                as ONE aligned 128-B line; the chunk's last partial line of a
-//                bin is padded with the empty key (skipped by every consumer).
-// HBM therefore only sees whole-line writes (8-byte scattered stores cost
-// ~3.5x the bytes: partially written lines leave the 4 MiB XCD L2 early).
-// Instantiated for u64 keys (k <= 32, 16 keys per line) and K128 keys
-// (k <= 64, 8 keys per line).
+// key bits below the segment's common prefix):
+//   part_hist    per chunk (64 Ki keys) and local bin: key count -> HC (exact
+//                placement), or only the bin totals Hg of a sample (sampled);
+//   (device)     exclusive scan of the totals / capacities -> bin starts;
+//   part_scatter every LDS tile of a chunk is counting-sorted by local bin and
+//                each bin's run leaves as one contiguous stretch of its slice
+//                (claimed per chunk, or per tile against a sampled capacity),
+//                so HBM sees long runs instead of 8-byte scattered stores
+//                (which cost ~3.5x the bytes: partially written lines leave
+//                the 4 MiB XCD L2 early).
+// Instantiated for u64 keys (k <= 32) and K128 keys (k <= 64).
 #include "okm_dev_common.h"
 
 namespace okm {
 
-#ifndef OKM_PART_BLOCK
-#define OKM_PART_BLOCK 1024
-#endif
-constexpr int kPartBlock = OKM_PART_BLOCK;  // threads per workgroup (scatter: LDS-limited to 1 block/CU)
-#ifndef OKM_PART_LOADU
-#define OKM_PART_LOADU 8
-#endif
-constexpr int kLoadU = OKM_PART_LOADU;  // keys per thread in flight per scatter batch
-constexpr int kHistU = 4;      // 16-B loads per thread in flight (histogram)
-
-#ifndef OKM_PART_COPY_BINS  // tile copy-out by bin (one wave per bin's run) when runs average >= 48 keys
-#define OKM_PART_COPY_BINS 0
-#endif
-#ifndef OKM_PART_TILE
-#define OKM_PART_TILE 1  // 1: LDS tile counting sort (exact runs, no padding); 0: per-bin line buffers
-#endif
-
-template <typename KT> struct Line {
-    static constexpr int kKeys = 128 / (int)sizeof(KT);  // keys per 128-B line
-};
+constexpr int kPartBlock = 1024;  // threads per workgroup (scatter: LDS-limited to 1 block/CU)
+constexpr int kHistU = 4;         // 16-B loads per thread in flight (histogram)
 
 // Output bins one pass can split a part into.  u64 unweighted passes take up
 // to 2048 (two bins per scatter thread, 15 Ki-key tiles), so a fold's L1 bin
 // of ~8 M instances splits straight into ~4 Ki-key children -- one item each,
-// with no fan-out pass (k_fan_split) after the partition (OKM_PART_2048=0:
-// 1024, one bin per thread).
-#ifndef OKM_PART_2048
-#define OKM_PART_2048 1
-#endif
+// with no fan-out pass (k_fan_split) after the partition.
 uint32_t part_max_bins(bool weighted, bool wide) {
     // the tile scan gives each thread one bin (two in the 2048-bin variant)
-    return weighted ? 512u : (!wide && OKM_PART_2048 ? 2u * kPartBlock : (uint32_t)kPartBlock);
+    return weighted ? 512u : (!wide ? 2u * kPartBlock : (uint32_t)kPartBlock);
 }
 
 template <typename KT>
@@ -57,13 +34,6 @@ __device__ __forceinline__ uint32_t local_bin(const KT &key, const DevSeg &s) {
     // segment's range (the difference is < nlocal)
     const uint64_t b = (s.shift >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(key, s.shift)) - s.key_base;
     return b < s.nlocal ? (uint32_t)b : s.nlocal - 1;  // clamp: never true for canonical keys
-}
-
-template <typename KT>
-__device__ __forceinline__ ull pad_line(ull n) {
-    if (OKM_PART_TILE) return n;  // tile scatter: exact placement, no line padding
-    constexpr int L = Line<KT>::kKeys;
-    return (n + L - 1) & ~(ull)(L - 1);
 }
 
 template <typename KT>
@@ -118,140 +88,32 @@ __global__ __launch_bounds__(kPartBlock) void k_part_hist(const DevSeg *__restri
         for (uint32_t b = threadIdx.x; b < s.nlocal; b += kPartBlock) {
             const uint32_t h = lh[b];
             if (HC) HC[(uint64_t)c * max_local + b] = h;
-            if (h) atomicAdd(&Hg[s.out_base + b], pad_line<KT>(h));
+            if (h) atomicAdd(&Hg[s.out_base + b], (ull)h);
         }
         lds_sync();
     }
 }
 
-// Writes one full line (keys [+ counts]) from LDS buffers to global.
-template <typename KT, bool W>
-__device__ __forceinline__ void flush_line(const KT *bk, const ull *bc, KT *ok, uint64_t *oc) {
-    constexpr int L = Line<KT>::kKeys;
-    const uint4 *src = reinterpret_cast<const uint4 *>(bk);
-    uint4 *dst = reinterpret_cast<uint4 *>(ok);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dst[q] = src[q];
-    if (W) {
-        const uint4 *cs = reinterpret_cast<const uint4 *>(bc);
-        uint4 *cd = reinterpret_cast<uint4 *>(oc);
-#pragma unroll
-        for (int q = 0; q < L / 2; ++q) cd[q] = cs[q];
-    }
-}
-
-template <typename KT, bool W>
-__global__ __launch_bounds__(kPartBlock) void k_part_scatter(
-    const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
-    uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
-    uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts) {
-    constexpr int L = Line<KT>::kKeys;
-    extern __shared__ __attribute__((aligned(16))) ull lds[];
-    KT *buf = reinterpret_cast<KT *>(lds);                               // [max_local][L] keys (128 B each)
-    ull *cbuf = lds + (size_t)max_local * 16;                            // [max_local][L] counts (W)
-    ull *gcur = W ? cbuf + (size_t)max_local * L : cbuf;                 // [max_local]
-    uint32_t *fill = reinterpret_cast<uint32_t *>(gcur + max_local);     // [max_local]
-    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
-    const uint32_t t = threadIdx.x;
-
-    for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const DevChunk ch = chunks[c];
-        const DevSeg s = segs[ch.seg];
-        const uint32_t nl = s.nlocal;
-        for (uint32_t b = t; b < nl; b += kPartBlock) {
-            const uint32_t h = HC[(uint64_t)c * max_local + b];
-            gcur[b] = h ? atomicAdd(&cursor[s.out_base + b], pad_line<KT>(h)) : 0ull;
-            fill[b] = 0;
-        }
-        __syncthreads();
-        const KT *keys = reinterpret_cast<const KT *>(s.keys) + ch.begin;
-        const uint64_t *cnts = s.counts ? s.counts + ch.begin : nullptr;
-        for (uint64_t base = 0; base < ch.len; base += (uint64_t)kPartBlock * kLoadU) {
-            KT kk[kLoadU];
-            ull ww[kLoadU];
-            uint32_t pend = 0;
-#pragma unroll
-            for (int u = 0; u < kLoadU; ++u) {
-                const uint64_t idx = base + (uint64_t)u * kPartBlock + t;
-                kk[u] = idx < ch.len ? gload(keys + idx) : KeyOps<KT>::empty();
-                ww[u] = (W && idx < ch.len) ? (cnts ? gload(cnts + idx) : 1ull) : 1ull;
-                if (!KeyOps<KT>::is_empty(kk[u])) pend |= 1u << u;
-            }
-            // append rounds: a key whose bin buffer is full waits for the flush
-            while (__syncthreads_or(pend != 0)) {
-#pragma unroll
-                for (int u = 0; u < kLoadU; ++u) {
-                    if (pend & (1u << u)) {
-                        const uint32_t b = local_bin(kk[u], s);
-                        const uint32_t pos = atomicAdd(&fill[b], 1u);
-                        if (pos < (uint32_t)L) {
-                            // slot order inside a line is free: swizzle it by the bin so
-                            // that lanes filling the same position of different bins hit
-                            // different LDS banks (bins are 128 B apart)
-                            const uint32_t sl = b * L + (pos ^ (b & (L - 1)));
-                            buf[sl] = kk[u];
-                            if (W) cbuf[sl] = ww[u];
-                            pend &= ~(1u << u);
-                        }
-                    }
-                }
-                __syncthreads();
-                for (uint32_t b = t; b < nl; b += kPartBlock) {
-                    if (fill[b] >= (uint32_t)L) {
-                        const ull g = gcur[b];
-                        flush_line<KT, W>(buf + b * L, cbuf + b * L, out_keys + g, W ? out_counts + g : nullptr);
-                        gcur[b] = g + L;
-                        fill[b] = 0;  // keys that overshot retry next round
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        // last partial line per bin, padded
-        for (uint32_t b = t; b < nl; b += kPartBlock) {
-            const uint32_t f = fill[b];
-            if (f) {
-                for (uint32_t q = f; q < (uint32_t)L; ++q) {
-                    const uint32_t sl = b * L + (q ^ (b & (L - 1)));
-                    buf[sl] = KeyOps<KT>::empty();
-                    if (W) cbuf[sl] = 0;
-                }
-                const ull g = gcur[b];
-                flush_line<KT, W>(buf + b * L, cbuf + b * L, out_keys + g, W ? out_counts + g : nullptr);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// Tile variant: every 64-Ki-key chunk is processed in LDS tiles that are
-// counting-sorted by local bin, and each bin's run leaves as one contiguous
-// stretch of the chunk's exact slice (no padding, no append rounds).
-#ifndef OKM_PART_TILE_XL  // u64 unweighted passes of <= 512 bins: tiles of this many keys (0: off)
-#define OKM_PART_TILE_XL 0
-#endif
-template <typename KT, bool W, bool BIG = false, bool XL = false> struct Tile {
+// Every 64-Ki-key chunk is processed in LDS tiles that are counting-sorted by
+// local bin, and each bin's run leaves as one contiguous stretch of the
+// chunk's slice (exact placement: no padding, no append rounds).
+template <typename KT, bool W, bool BIG = false> struct Tile {
     // <= 128 KiB of staged keys (+ counts), + 16 KiB of per-bin state; BIG
-    // (2048 bins: 32 KiB of per-bin state): 120 KiB of staged keys
-#ifndef OKM_PART_TILE_KEYS
-#define OKM_PART_TILE_KEYS 16384
-#endif
-    static constexpr int kKeys = XL ? (OKM_PART_TILE_XL ? OKM_PART_TILE_XL : OKM_PART_TILE_KEYS)
-                                : BIG ? 15 * kPartBlock
-                                     : ((W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : OKM_PART_TILE_KEYS));
+    // (2048 bins: 32 KiB of per-bin state): 120 KiB of staged keys.  (18 Ki-key
+    // tiles for <= 512 bins: 1.742 vs 1.738 ms, not kept; profiles/AB_LOG.md)
+    static constexpr int kKeys = BIG ? 15 * kPartBlock
+                                     : ((W && sizeof(KT) > 8) ? 4096 : ((W || sizeof(KT) > 8) ? 8192 : 16384));
     static constexpr int kPer = kKeys / kPartBlock;
 };
 
-// OKM_PART_BLOCK=512 builds: two workgroups per CU (half-size tiles), so one
-// workgroup's loads overlap the other's LDS phases and stores; <= 128 VGPRs
-template <typename KT, bool W, bool BIG = false, bool XL = false>
-__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(kPartBlock == 512 ? 4 : 1)))
+template <typename KT, bool W, bool BIG = false>
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(1)))
 void k_part_scatter_tile(
     const DevSeg *__restrict__ segs, const DevChunk *__restrict__ chunks, uint32_t nchunks,
     uint32_t max_local, const uint32_t *__restrict__ HC, ull *__restrict__ cursor,
     uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts, const ull *__restrict__ cap_end,
     ull *__restrict__ ovf) {
-    constexpr int T = Tile<KT, W, BIG, XL>::kKeys, P = Tile<KT, W, BIG, XL>::kPer;
+    constexpr int T = Tile<KT, W, BIG>::kKeys, P = Tile<KT, W, BIG>::kPer;
     constexpr uint32_t BPT = BIG ? 2 : 1;  // bins per thread in the scan / claim phase
     extern __shared__ __attribute__((aligned(16))) ull lds[];
     KT *stage = reinterpret_cast<KT *>(lds);                              // [T]
@@ -347,18 +209,6 @@ void k_part_scatter_tile(
             }
             lds_sync();
             // each bin's run is contiguous in `stage` and in the output slice
-            if (OKM_PART_COPY_BINS && (uint32_t)tile_n >= 48u * nl) {  // long runs: one wave per bin, no lookups
-                const uint32_t lane = t & 63u;
-                for (uint32_t b = t >> 6; b < nl; b += kPartBlock / 64) {
-                    const ull g = gcur[b];
-                    if (g == ~0ull) continue;
-                    const uint32_t lo = lofs[b], n = hist[b];
-                    for (uint32_t q = lane; q < n; q += 64) {
-                        out_keys[g + q] = stage[lo + q];
-                        if (W) out_counts[g + q] = cstage[lo + q];
-                    }
-                }
-            } else
             for (uint32_t j = t; j < (uint32_t)tile_n; j += kPartBlock) {
                 const KT key = stage[j];
                 const uint32_t b = local_bin(key, s);
@@ -376,14 +226,9 @@ void k_part_scatter_tile(
     }
 }
 
-// OKM_PART_GRID: cap on the partition kernels' workgroups (A/B runs)
-static uint32_t part_grid(uint32_t nchunks) {
-    static const uint32_t cap = [] {
-        const char *e = getenv("OKM_PART_GRID");
-        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 4096u;
-    }();
-    return nchunks < cap ? nchunks : cap;
-}
+// Workgroups of the partition kernels (grids of 2048 / 8192 measured the same,
+// profiles/AB_LOG.md round 4)
+static uint32_t part_grid(uint32_t nchunks) { return nchunks < 4096u ? nchunks : 4096u; }
 
 void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                       uint32_t max_local, uint32_t *HC, unsigned long long *Hg, bool wide) {
@@ -396,8 +241,6 @@ void launch_part_hist(void *stream, const DevSeg *segs, const DevChunk *chunks, 
         hipLaunchKernelGGL(k_part_hist<ull>, g, b, lds, (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, Hg);
 }
 
-bool part_tile_mode() { return OKM_PART_TILE != 0; }
-
 template <typename KT, bool W>
 static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,
                            uint32_t max_local, const uint32_t *HC, unsigned long long *cursor, uint64_t *out_keys,
@@ -408,57 +251,27 @@ static void scatter_launch(void *stream, const DevSeg *segs, const DevChunk *chu
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || optin <= 0)
             optin = 64 * 1024;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter<KT, W>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, optin);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, optin);
         (void)hipGetLastError();  // an unsupported attribute must not poison later checks
         attr_done = true;
     }
-    if (OKM_PART_TILE) {
-        static bool attr_tile = false;
-        if (!attr_tile) {
-            int dev = 0, optin = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess ||
-                optin <= 0)
-                optin = 64 * 1024;
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, optin);
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, optin);
-            if (OKM_PART_TILE_XL)
-                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_part_scatter_tile<KT, W, false, true>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, optin);
-            (void)hipGetLastError();
-            attr_tile = true;
-        }
-        const size_t bin_state = (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
-        if (max_local > (uint32_t)kPartBlock) {  // 2048 bins: u64 unweighted passes only (part_max_bins)
-            constexpr int T = Tile<KT, W, true>::kKeys;
-            const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) + bin_state;
-            hipLaunchKernelGGL((k_part_scatter_tile<KT, W, true>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
-                               (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
-                               cap_end, ovf);
-            return;
-        }
-        if (OKM_PART_TILE_XL && !W && sizeof(KT) == 8 && max_local <= 512u) {  // longer runs where they fit
-            constexpr int T = Tile<KT, W, false, true>::kKeys;
-            const size_t lds = (size_t)T * sizeof(KT) + bin_state;
-            hipLaunchKernelGGL((k_part_scatter_tile<KT, W, false, true>), dim3(part_grid(nchunks)), dim3(kPartBlock),
-                               lds, (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys,
-                               out_counts, cap_end, ovf);
-            return;
-        }
-        constexpr int T = Tile<KT, W>::kKeys;
+    const size_t bin_state = (size_t)max_local * (sizeof(ull) + 2 * sizeof(uint32_t));
+    if (max_local > (uint32_t)kPartBlock) {  // 2048 bins: u64 unweighted passes only (part_max_bins)
+        constexpr int T = Tile<KT, W, true>::kKeys;
         const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) + bin_state;
-        hipLaunchKernelGGL((k_part_scatter_tile<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
+        hipLaunchKernelGGL((k_part_scatter_tile<KT, W, true>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
                            (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts,
                            cap_end, ovf);
         return;
     }
-    constexpr int L = Line<KT>::kKeys;
-    const size_t lds = (size_t)max_local * (128 + (W ? L * sizeof(ull) : 0) + sizeof(ull) + sizeof(uint32_t));
-    hipLaunchKernelGGL((k_part_scatter<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
-                       (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts);
+    constexpr int T = Tile<KT, W>::kKeys;
+    const size_t lds = (size_t)T * (sizeof(KT) + (W ? sizeof(ull) : 0)) + bin_state;
+    hipLaunchKernelGGL((k_part_scatter_tile<KT, W>), dim3(part_grid(nchunks)), dim3(kPartBlock), lds,
+                       (hipStream_t)stream, segs, chunks, nchunks, max_local, HC, cursor, out_keys, out_counts, cap_end,
+                       ovf);
 }
 
 void launch_part_scatter(void *stream, const DevSeg *segs, const DevChunk *chunks, uint32_t nchunks,

@@ -243,246 +243,6 @@ __global__ __launch_bounds__(kProbeBlock) void k_query_hits(const uint8_t *__res
 }
 
 // ---------------------------------------------------------------------------
-// query over a minimizer-bucketed copy of the set
-//
-// The hash set costs one random 128-B line per probed window, and at C2 scale
-// every one is an HBM miss (0.79 of the random-probe ceiling).
-// Here the set's keys are grouped by the MINIMIZER of each k-mer: the m-mer
-// (m = min(k, 15)) whose canonical value has the smallest hash among the
-// k - m + 1 m-mers of the k-mer.  The canonical m-mers of a k-mer and of its
-// reverse complement are the same set, so a window and the canonical key
-// agree on the minimizer whatever strand the read came from.  Consecutive
-// k-mers share their minimizer for ~(k - m + 2) / 2 windows on average.
-// Each bucket (a hash of the minimizer) is a small open-addressing table of
-// kMiniSlots keys (four 128-B lines): a window probes ONE slot of its bucket,
-// and the windows of a read that share the bucket probe the same four lines,
-// so a 150-bp read misses on ~15 buckets' lines instead of ~120 random slots.
-// A bucket given more than kMiniSlots / 2 keys is marked overflowed (every
-// slot kMiniOvf, a value no canonical key takes) and its windows probe the
-// hash set instead.  The hits are exactly the hash set's (query.rs:86-93:
-// membership of the canonical key); only where the key is looked up changes.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kMiniM = 15;        // m-mer length (m = min(k, 15))
-constexpr uint32_t kMiniSlots = 64;    // slots per bucket (512 B)
-constexpr uint32_t kMiniKeysPerBucket = 4;  // buckets = keys / 4; ~8 % of the keys sit in overflowed buckets
-// ~1: TTT...TG for k = 32 (its reverse complement CAA...A is smaller), and
-// more than 2k bits for k < 32 -- never a canonical key
-constexpr ull kMiniOvf = ~1ull;
-
-struct MiniTab {
-    const ull *tab;  // nb buckets of kMiniSlots keys (kEmpty: free, kMiniOvf: bucket overflowed)
-    SetTab set;      // the hash set (overflowed buckets)
-    uint32_t nb;     // buckets
-    uint32_t m;      // m-mer length
-};
-
-__host__ __device__ __forceinline__ uint32_t mini_hash(uint32_t canon_m) {  // murmur3 fmix32, seeded
-    uint32_t h = canon_m ^ 0x9E3779B9u;
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    h *= 0xC2B2AE35u;
-    h ^= h >> 16;
-    return h;
-}
-// The minimum of k - m + 1 hashes is skewed towards 0: mixed again before it
-// picks a bucket, or the low buckets would take every key.
-__host__ __device__ __forceinline__ uint32_t mini_bucket(uint32_t h, uint32_t nb) {
-    h ^= 0x7F4A7C15u;
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    h *= 0xC2B2AE35u;
-    h ^= h >> 16;
-    return (uint32_t)(((uint64_t)h * nb) >> 32);
-}
-__host__ __device__ __forceinline__ uint32_t canon_mmer(uint32_t fwd, uint32_t m) {
-    const uint32_t mask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
-    const uint32_t rc = ~rev2(fwd << (32 - 2 * m)) & mask;  // reverse complement of the m bases
-    return fwd < rc ? fwd : rc;
-}
-// A key's home slot inside its bucket.
-__device__ __forceinline__ uint32_t mini_slot(ull key) {
-    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 58);  // top 6 bits (kMiniSlots = 64)
-}
-// Bucket of a canonical k-mer key (2k bits, MSB-first).
-__host__ __device__ __forceinline__ uint32_t key_bucket(uint64_t key, uint32_t k, uint32_t m, uint32_t nb) {
-    const uint32_t mask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
-    uint32_t best = ~0u;
-    for (uint32_t i = 0; i + m <= k; ++i) {
-        const uint32_t f = (uint32_t)(key >> (2 * (k - m - i))) & mask;  // bases i .. i+m-1
-        const uint32_t h = mini_hash(canon_mmer(f, m));
-        best = h < best ? h : best;
-    }
-    return mini_bucket(best, nb);
-}
-
-// Build pass 1: keys per bucket.
-__global__ __launch_bounds__(kProbeBlock) void k_mini_count(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
-                                                            uint32_t m, uint32_t nb, uint32_t *__restrict__ cnt) {
-    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
-        const ull x = slots[i];
-        if (x != kEmpty) atomicAdd(&cnt[key_bucket(x, k, m, nb)], 1u);
-    }
-}
-// Build pass 2: every bucket's slots: kMiniOvf when it has too many keys, else empty.
-__global__ __launch_bounds__(kProbeBlock) void k_mini_clear(const uint32_t *__restrict__ cnt, uint32_t nb,
-                                                            ull *__restrict__ tab) {
-    const uint64_t n = (uint64_t)nb * kMiniSlots;
-    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < n; i += stride)
-        tab[i] = cnt[i / kMiniSlots] > kMiniSlots / 2 ? kMiniOvf : kEmpty;
-}
-// Build pass 3: every key of a bucket that did not overflow into its table.
-__global__ __launch_bounds__(kProbeBlock) void k_mini_fill(const ull *__restrict__ slots, uint64_t cap, uint32_t k,
-                                                           uint32_t m, uint32_t nb, const uint32_t *__restrict__ cnt,
-                                                           ull *__restrict__ tab) {
-    const uint64_t stride = (uint64_t)gridDim.x * kProbeBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kProbeBlock + threadIdx.x; i < cap; i += stride) {
-        const ull x = slots[i];
-        if (x == kEmpty) continue;
-        const uint32_t b = key_bucket(x, k, m, nb);
-        if (cnt[b] > kMiniSlots / 2) continue;
-        ull *bt = tab + (uint64_t)b * kMiniSlots;
-        for (uint32_t s = mini_slot(x);; s = (s + 1) & (kMiniSlots - 1))
-            if (atomicCAS(&bt[s], kEmpty, x) == kEmpty) break;  // distinct keys, load <= 1/2: a slot is free
-    }
-}
-
-// Continue a bucket probe whose home slot held neither the key nor a free slot.
-__device__ __noinline__ bool mini_probe_rest(const ull *__restrict__ bt, ull key, uint32_t s) {
-    for (uint32_t i = 1; i < kMiniSlots; ++i) {
-        const ull v = bt[(s + i) & (kMiniSlots - 1)];
-        if (v == key) return true;
-        if (v == kEmpty) return false;
-    }
-    return false;
-}
-
-// k_query_hits over the bucketed set: the thread's 16 windows, their validity
-// as in k_query_hits, the 16 + k - m canonical m-mer hashes they span and each
-// window's minimizer bucket; then every valid window's home slot in its bucket
-// is loaded together (windows of one bucket hit the same two lines), a collision
-// continues inside the bucket, and an overflowed bucket sends the window to
-// the hash set.
-#ifndef OKM_QUERY_MINI_WAVES  // experiment builds: a waves-per-SIMD target for k_query_hits_mini
-#define OKM_QUERY_MINI_WAVES 0
-#endif
-#if OKM_QUERY_MINI_WAVES
-#define OKM_MINI_ATTR __attribute__((amdgpu_waves_per_eu(OKM_QUERY_MINI_WAVES)))
-#else
-#define OKM_MINI_ATTR
-#endif
-template <int K>
-__global__ __launch_bounds__(kProbeBlock) OKM_MINI_ATTR void k_query_hits_mini(const uint8_t *__restrict__ seq, uint64_t n,
-                                                                 const ull *__restrict__ tile_pre, MiniTab t,
-                                                                 uint32_t k_rt, uint32_t *__restrict__ hits,
-                                                                 uint64_t nrec) {
-    __shared__ ull wsum[kProbeBlock / 64];
-    const uint64_t w0 = (uint64_t)blockIdx.x * kQTile + (uint64_t)threadIdx.x * kQSeg;
-    // 64 bytes: the m-mer slices reach one code word past the windows' 48
-    WinWords<kQSeg, 48> ww;
-    load_windows<kQSeg, 48>(seq, n, w0, ww);
-    const uint32_t *w = ww.w;
-    const uint32_t sepm = w0 < n ? sep_mask16(w) : 0u;
-    ull tot;
-    const ull rec0 = tile_pre[blockIdx.x] + block_excl_scan<kProbeBlock>((ull)__popc(sepm), wsum, &tot);
-    if (w0 >= n) return;
-
-    const uint32_t k = K ? (uint32_t)K : k_rt;
-    const uint32_t m = K ? (K < (int)kMiniM ? (uint32_t)K : kMiniM) : t.m;
-    constexpr int NP = WinWords<kQSeg, 48>::kLoad / 16;
-    Codes<NP> c;
-    make_codes<NP, true>(w, c);  // query.rs: raw bytes, U invalid
-    const uint32_t vmask = ~invalid_windows<kQSeg, NP>(c, k) & 0xFFFFu;
-    // minimizer bucket of every window
-    const uint32_t span = k - m;  // a window's m-mers: j .. j + span
-    const uint32_t mmask = m >= 16 ? ~0u : ((1u << (2 * m)) - 1u);
-    auto mmer_hash = [&](int i) {  // hash of the canonical m-mer at base i
-        const uint32_t f = fwd32(c, 2 * i) >> (32 - 2 * m);
-        const uint32_t r = rc32(c, 2 * i) & mmask;
-        return mini_hash(f < r ? f : r);
-    };
-    ull first[kQSeg];
-    if constexpr (K >= 30) {
-        // window j's minimizer is the least of m-mers j .. j + SP (SP >= 15):
-        // suffix minima S of m-mers 0 .. SP and a running minimum P of
-        // SP + 1 .. SP + j, so each window's bucket -- and its slot load -- is
-        // ready in order while only S stays live (the loads of the first
-        // windows are in flight while the later buckets are computed)
-        constexpr int SP = K - (int)kMiniM;
-        uint32_t S[SP + 1];
-#pragma unroll
-        for (int i = 0; i <= SP; ++i) S[i] = mmer_hash(i);
-#pragma unroll
-        for (int i = SP - 1; i >= 0; --i) S[i] = min(S[i], S[i + 1]);
-        uint32_t P = ~0u;
-#pragma unroll
-        for (int j = 0; j < kQSeg; ++j) {
-            if (j > 0) P = min(P, mmer_hash(SP + j));
-            const uint32_t b = mini_bucket(min(S[j], P), t.nb);
-            first[j] = (vmask >> j) & 1u ? t.tab[(uint64_t)b * kMiniSlots + mini_slot(window_key_nv(c, j, k))] : kEmpty;
-        }
-    } else {
-        uint32_t bk[kQSeg];
-        {
-            uint32_t h[kQSeg + 17];  // span <= 32 - 15
-#pragma unroll
-            for (int i = 0; i < kQSeg + 17; ++i) {
-                if ((uint32_t)i > kQSeg - 1 + span) break;
-                h[i] = mmer_hash(i);
-            }
-#pragma unroll
-            for (int j = 0; j < kQSeg; ++j) {
-                uint32_t mn = h[j];
-                if (K) {
-#pragma unroll
-                    for (uint32_t d = 1; d <= (K > (int)kMiniM ? (uint32_t)K - kMiniM : 0u); ++d) mn = min(mn, h[j + d]);
-                } else {
-                    for (uint32_t d = 1; d <= span; ++d) mn = min(mn, h[j + d]);
-                }
-                bk[j] = mini_bucket(mn, t.nb);
-            }
-        }
-        // every valid window's home slot load in flight together (only the
-        // loaded words stay live: keys are recomputed, buckets too on the rare
-        // collision)
-#pragma unroll
-        for (int j = 0; j < kQSeg; ++j)
-            first[j] = (vmask >> j) & 1u ? t.tab[(uint64_t)bk[j] * kMiniSlots + mini_slot(window_key_nv(c, j, k))]
-                                         : kEmpty;
-    }
-    opaque_codes(c);
-    uint32_t hitm = 0;  // bit j: window j's key is in the set
-#pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        if (first[j] == kEmpty) continue;  // invalid window, or a free home slot
-        const ull key = window_key_nv(c, j, k);
-        bool hit = first[j] == key;
-        if (!hit) {
-            if (first[j] == kMiniOvf)
-                hit = set_contains(t.set, key);
-            else
-                hit = mini_probe_rest(t.tab + (uint64_t)key_bucket(key, k, m, t.nb) * kMiniSlots, key, mini_slot(key));
-        }
-        hitm |= (hit ? 1u : 0u) << j;
-    }
-    ull rec = rec0;
-    uint32_t cur = 0;
-#pragma unroll
-    for (int j = 0; j < kQSeg; ++j) {
-        if ((sepm >> j) & 1u) {  // window j starts a new record (and is itself invalid)
-            flush_hits(hits, nrec, rec, cur);
-            cur = 0;
-            ++rec;
-        }
-        cur += (hitm >> j) & 1u;
-    }
-    flush_hits(hits, nrec, rec, cur);
-}
-
-// ---------------------------------------------------------------------------
 // classify: map of the filtered input counts, probed by every reference key
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kProbeBlock) void k_map_build(MapTab t, const ull *__restrict__ keys,
@@ -681,16 +441,8 @@ struct okm_kset {
     ull *d_ctr = nullptr;  // [0]: new keys of the last insert
     Scratch keys, batch, tiles, hits;
     std::vector<uint8_t> host_batch;
-    // minimizer-bucketed copy of the keys (query): built at the first query
-    // after an insert; mini_ok false when there is none (no keys, >= 2^32 keys)
-    Scratch mini_tab, mini_cnt;  // the bucket tables; keys per bucket (build)
-    uint32_t mini_nb = 0;
-    bool mini_built = false, mini_ok = false;
 
     SetTab tab() const { return SetTab{slots, cap - 1, 64u - log2_exact(cap)}; }
-    MiniTab mini() const {
-        return MiniTab{(const ull *)mini_tab.p, tab(), mini_nb, k < kMiniM ? (uint32_t)k : kMiniM};
-    }
 };
 
 struct okm_classifier {
@@ -739,7 +491,6 @@ okm_status set_reserve(okm_kset *s, uint64_t n) {
 }
 
 okm_status set_insert_device(okm_kset *s, const uint64_t *d_keys, uint64_t n, uint64_t *n_new) {
-    s->mini_built = false;
     PTRY(set_reserve(s, n));
     PHIP(hipMemsetAsync(s->d_ctr, 0, sizeof(ull), s->st));
     hipLaunchKernelGGL(k_set_insert, dim3(grid_for(n)), dim3(kProbeBlock), 0, s->st, s->tab(),
@@ -760,53 +511,6 @@ void launch_query_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pr
                        (uint32_t)s->k, d_hits, nrec);
 }
 
-// OKM_QUERY_MINI: 0 (default) the hash-set probe kernel, 1 the bucketed copy,
-// 2 the bucketed copy or an error (tests: the index path must be the one run).
-// The bucketed copy halves the HBM lines a C2 query fetches but runs no faster
-// (9.46 vs 8.91 ms: at 91 VGPRs, 5 waves per SIMD, it is bound by the probes
-// in flight, where the hash kernel at 64 VGPRs is bound by HBM lines).
-int query_mini_mode() {
-    const char *e = getenv("OKM_QUERY_MINI");
-    return e && *e ? atoi(e) : 0;
-}
-
-// The minimizer-bucketed copy of the set: keys per bucket, the buckets'
-// tables cleared (or marked overflowed), every key inserted into its bucket.
-// OKM_QUERY_MINI_KPB (tests): keys per bucket on average (more: overflows).
-okm_status mini_build(okm_kset *s) {
-    s->mini_built = true;
-    s->mini_ok = false;
-    if (s->size == 0) return OKM_OK;
-    const char *e = getenv("OKM_QUERY_MINI_KPB");
-    const uint64_t kpb = e && atoi(e) > 0 ? (uint64_t)atoi(e) : kMiniKeysPerBucket;
-    const uint32_t m = s->k < kMiniM ? s->k : kMiniM;
-    const uint64_t nb64 = std::max<uint64_t>(1, (s->size + kpb - 1) / kpb);
-    if (nb64 >= 0xFFFFFFFFull) return OKM_OK;
-    const uint32_t nb = (uint32_t)nb64;
-    PTRY(s->mini_tab.ensure((size_t)nb * kMiniSlots * sizeof(ull)));
-    PTRY(s->mini_cnt.ensure((size_t)nb * sizeof(uint32_t)));
-    uint32_t *cnt = (uint32_t *)s->mini_cnt.p;
-    ull *tab = (ull *)s->mini_tab.p;
-    PHIP(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(uint32_t), s->st));
-    hipLaunchKernelGGL(k_mini_count, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
-                       s->cap, (uint32_t)s->k, m, nb, cnt);
-    hipLaunchKernelGGL(k_mini_clear, dim3(grid_for((uint64_t)nb * kMiniSlots)), dim3(kProbeBlock), 0, s->st,
-                       (const uint32_t *)cnt, nb, tab);
-    hipLaunchKernelGGL(k_mini_fill, dim3(grid_for(s->cap)), dim3(kProbeBlock), 0, s->st, (const ull *)s->slots,
-                       s->cap, (uint32_t)s->k, m, nb, (const uint32_t *)cnt, tab);
-    PHIP(hipGetLastError());
-    s->mini_nb = nb;
-    s->mini_ok = true;
-    return OKM_OK;
-}
-
-template <int K>
-void launch_query_mini_k(okm_kset *s, const uint8_t *d_seq, uint64_t n, const ull *pre, uint32_t *d_hits,
-                         uint64_t nrec, uint32_t ntiles) {
-    hipLaunchKernelGGL(k_query_hits_mini<K>, dim3(ntiles), dim3(kProbeBlock), 0, s->st, d_seq, n, pre, s->mini(),
-                       (uint32_t)s->k, d_hits, nrec);
-}
-
 okm_status query_device(okm_kset *s, const uint8_t *d_seq, uint64_t n, uint64_t nrec, uint32_t *d_hits) {
     PHIP(hipMemsetAsync(d_hits, 0, nrec * sizeof(uint32_t), s->st));
     if (n == 0 || s->size == 0) return OKM_OK;
@@ -817,21 +521,6 @@ okm_status query_device(okm_kset *s, const uint8_t *d_seq, uint64_t n, uint64_t 
     ull *cnt = (ull *)s->tiles.p, *pre = cnt + ntiles, *scr = pre + ntiles;
     hipLaunchKernelGGL(k_sep_count, dim3((uint32_t)ntiles), dim3(kProbeBlock), 0, s->st, d_seq, n, cnt);
     launch_exclusive_scan(s->st, cnt, pre, ntiles, scr);
-    const int mode = query_mini_mode();
-    if (mode && !s->mini_built) PTRY(mini_build(s));
-    if (mode == 2 && !s->mini_ok) return fail(OKM_E_STATE, "okm_query_hits: no minimizer index (OKM_QUERY_MINI=2)");
-    if (mode && s->mini_ok) {
-        switch (s->k) {
-        case 21: launch_query_mini_k<21>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        case 25: launch_query_mini_k<25>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        case 27: launch_query_mini_k<27>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        case 31: launch_query_mini_k<31>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        case 32: launch_query_mini_k<32>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        default: launch_query_mini_k<0>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
-        }
-        PHIP(hipGetLastError());
-        return OKM_OK;
-    }
     switch (s->k) {
     case 21: launch_query_k<21>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
     case 25: launch_query_k<25>(s, d_seq, n, pre, d_hits, nrec, (uint32_t)ntiles); break;
@@ -882,8 +571,6 @@ void okm_kset_destroy(okm_kset *s) {
     s->batch.release();
     s->tiles.release();
     s->hits.release();
-    s->mini_tab.release();
-    s->mini_cnt.release();
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_size_t,
+from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_int64, c_size_t,
                     c_uint8, c_uint32, c_uint64, c_void_p)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -56,7 +56,8 @@ class EngineInfo(Structure):
     _fields_ = [("kmers", c_uint64), ("distinct", c_uint64), ("l1_bits", c_uint32),
                 ("l2_bits", c_uint32), ("levels", c_uint32), ("work_items", c_uint32),
                 ("max_partition", c_uint64), ("device_bytes", c_uint64), ("groups", c_uint32),
-                ("folds", c_uint32)]
+                ("folds", c_uint32), ("device_peak_bytes", c_uint64), ("host_bytes", c_uint64),
+                ("spills", c_uint32), ("pad", c_uint32)]
 
 
 class Key128(Structure):
@@ -164,6 +165,8 @@ PROTOTYPES = {
     "okm_group_write_counts_tsv": (c_int, [c_void_p, c_char_p, c_uint64, _P64]),
     "okm_synth_reads_device": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_double,
                                        c_double, c_void_p, c_int]),
+    "okm_test_set": (None, [c_int, c_int64]),
+    "okm_test_get": (c_int64, [c_int]),
     "okm_synth_long_reads": (c_int, [c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_double, c_double, c_uint32,
                                      c_uint32, c_double, c_double, c_double, POINTER(c_void_p), _P64, c_void_p,
                                      c_int]),

@@ -34,6 +34,18 @@ def built_libraries():
     yield
 
 
+@pytest.fixture(autouse=True)
+def _reset_test_knobs():
+    """Every engine test hook (okm.testing) back to its product default after
+    each test, whatever the test set."""
+    yield
+    try:
+        from okm import testing
+        testing.reset_all()
+    except Exception:  # no library (a pure-Python test on a bare checkout)
+        pass
+
+
 @pytest.fixture(scope="session")
 def golden_cases():
     import json

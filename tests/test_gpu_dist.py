@@ -13,6 +13,7 @@ import pytest
 
 import okm
 import restate as R
+from okm import testing
 from oracle import OracleCounter
 
 pytestmark = pytest.mark.gpu
@@ -60,8 +61,8 @@ def test_merge_owned_single_rank_equals_local(comm1, genome):
 @pytest.mark.parametrize("piece", [4096, 1 << 20])
 def test_merge_owned_rccl_multi_piece(comm1, monkeypatch, piece):
     """Real RCCL at one rank with every message cut into many pieces
-    (OKM_RCCL_PIECE): keys, count bytes and escapes of the self slice."""
-    monkeypatch.setenv("OKM_RCCL_PIECE", str(piece))
+    (test knob piece_bytes): keys, count bytes and escapes of the self slice."""
+    testing.set_knob("piece_bytes", piece)
     k = 31
     b = _batch(200_000, 3_000_000, 8)
     b.reshape(200_000, 151)[::50, :150] = ord("A")  # a hot key: counts past the one-byte escape
@@ -129,7 +130,7 @@ def test_merge_owned_wide_rccl(comm1, monkeypatch, piece):
     """k = 63 (K128 keys): the slices cross RCCL as u64 word pairs, the owner
     counts them; exact against the restatement (one rank: self send/recv)."""
     if piece:
-        monkeypatch.setenv("OKM_RCCL_PIECE", piece)
+        testing.set_knob("piece_bytes", int(piece))
     from oracle import OracleCounterWide
     k = 63
     b = _batch(30_000, 200_000, 9)
@@ -208,11 +209,11 @@ def test_group_pipelined_count(n_gpus):
 @pytest.mark.parametrize("ext,chunk", [("tsv", "1500"), ("tsv", ""), ("tsv.gz", "4096"), ("tsv.zst", "")])
 def test_group_write_counts_tsv_streamed(tmp_path, monkeypatch, ext, chunk):
     """okm_group_write_counts_tsv: the table streamed off the GPU in chunks
-    (OKM_TSV_CHUNK entries) equals count.rs:127-135's TSV of the oracle table,
+    (test knob tsv_chunk: entries) equals count.rs:127-135's TSV of the oracle table,
     filtered by min_count, also when it overwrites a LONGER existing file
     (written in place, then cut to length)."""
     if chunk:
-        monkeypatch.setenv("OKM_TSV_CHUNK", chunk)
+        testing.set_knob("tsv_chunk", int(chunk))
     k = 21
     batches = [_batch(20_000, 300_000, 50 + i) for i in range(3)]
     ref = OracleCounter(k)

@@ -16,11 +16,19 @@ import numpy as np
 import pytest
 
 import okm
+from okm import testing
 from oracle import OracleCounter
 
 pytestmark = pytest.mark.gpu
 # a rank that never reaches a collective ends it after a minute, not five
-os.environ.setdefault("OKM_LOOPBACK_TIMEOUT_S", "60")
+
+
+@pytest.fixture(autouse=True)
+def _loopback_timeout():
+    """A rank that never arrives ends a collective after 60 s, not 300 (the
+    conftest resets every knob after each test)."""
+    testing.set_knob("loopback_timeout_ms", 60_000)
+    yield
 
 
 def run_ranks(P, fn):
@@ -169,9 +177,9 @@ def test_loopback_merge_set_mode(P):
 
 @pytest.mark.parametrize("piece", [4096, 65536])
 def test_loopback_merge_multi_piece(monkeypatch, piece):
-    """OKM_RCCL_PIECE small: every message (keys, count bytes, escapes) splits
+    """Tiny message pieces (knob piece_bytes): every message (keys, count bytes, escapes) splits
     into many pieces, grouped by piece index on every rank."""
-    monkeypatch.setenv("OKM_RCCL_PIECE", str(piece))
+    testing.set_knob("piece_bytes", piece)
     k, P = 31, 3
     recs = _records(40_000, 250_000, 24, hot_every=30)
     ek, ec = _oracle(recs, k)
@@ -227,14 +235,14 @@ def test_loopback_owner_takes_more_input_after_merge():
 
 
 def test_loopback_failure_agreement(monkeypatch):
-    """A rank failing between collectives (OKM_DIST_FAIL_RANK: out of memory
+    """A rank failing between collectives (knob fail_rank: out of memory
     while sizing its receive buffers) makes EVERY rank return an error, and the
     communicator still merges afterwards."""
     k, P = 21, 3
     recs = _records(10_000, 100_000, 27)
     shards = _shards(recs, P)
     comms = okm.Comm.init_loopback(P, 0)
-    monkeypatch.setenv("OKM_DIST_FAIL_RANK", "1")
+    testing.set_knob("fail_rank", 1)
 
     def attempt(r):
         with okm.KmerCounter(k) as local, okm.KmerCounter(k) as owner:
@@ -252,7 +260,7 @@ def test_loopback_failure_agreement(monkeypatch):
         st = run_ranks(P, attempt)
         assert st[1] == okm._lib.OKM_E_NOMEM
         assert st[0] == st[2] == okm._lib.OKM_E_COMM
-        monkeypatch.delenv("OKM_DIST_FAIL_RANK")
+        testing.set_knob("fail_rank", -1)
         assert run_ranks(P, attempt) == [None] * P
     finally:
         for c in comms:
@@ -262,7 +270,7 @@ def test_loopback_failure_agreement(monkeypatch):
 def test_loopback_missing_rank_times_out(monkeypatch):
     """A rank that never joins the collective ends it with OKM_E_COMM on the
     others (no hang), and the aborted communicator refuses later merges."""
-    monkeypatch.setenv("OKM_LOOPBACK_TIMEOUT_S", "2")
+    testing.set_knob("loopback_timeout_ms", 2000)
     comms = okm.Comm.init_loopback(2, 0)
     try:
         with okm.KmerCounter(15) as local, okm.KmerCounter(15) as owner:
@@ -322,7 +330,7 @@ def test_loopback_distributed_compare(P):
 @pytest.mark.parametrize("P", [2, 8])
 @pytest.mark.parametrize("sparse", [False, True])
 def test_loopback_wire_formats(monkeypatch, P, sparse):
-    """Keys on the wire as u64 and as 5-byte deltas (OKM_WIRE_DELTAS forced),
+    """Keys on the wire as u64 and as 5-byte deltas (knob wire_deltas forced),
     with key escapes for gaps >= 2^40: most gaps of a ~100 K-key table
     escape; counts past the byte escape.  Both formats give the oracle's
     table."""
@@ -331,7 +339,7 @@ def test_loopback_wire_formats(monkeypatch, P, sparse):
                     hot_every=0 if sparse else 35)
     ek, ec = _oracle(recs, k)
     for deltas in ("1", "0"):
-        monkeypatch.setenv("OKM_WIRE_DELTAS", deltas)
+        testing.set_knob("wire_deltas", int(deltas))
         res = _merge_case(P, k, _shards(recs, P), "separate")
         _check_ranges(res, ek, ec)
 
@@ -348,10 +356,7 @@ def test_loopback_wire_deltas_dense_table_bytes(monkeypatch, P):
     recs = _records(1_000_000, 10_000_000, 30)
     sent, tables = {}, {}
     for deltas in ("", "0"):
-        if deltas:
-            monkeypatch.setenv("OKM_WIRE_DELTAS", deltas)
-        else:
-            monkeypatch.delenv("OKM_WIRE_DELTAS", raising=False)
+        testing.set_knob("wire_deltas", int(deltas) if deltas else -1)
         res = _merge_case(P, k, _shards(recs, P), "separate")
         sent[deltas] = sum(r[3][0] for r in res)
         tables[deltas] = (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
@@ -363,8 +368,8 @@ def test_loopback_wire_deltas_dense_table_bytes(monkeypatch, P):
 
 def test_loopback_wire_deltas_multi_piece_set_mode(monkeypatch):
     """5-byte keys cut into odd-sized pieces (a key straddles two pieces), set mode."""
-    monkeypatch.setenv("OKM_WIRE_DELTAS", "1")
-    monkeypatch.setenv("OKM_RCCL_PIECE", "4104")
+    testing.set_knob("wire_deltas", 1)
+    testing.set_knob("piece_bytes", 4104)
     k, P = 27, 3
     recs = _records(25_000, 500_000, 29)
     ek, _ = _oracle(recs, k)
@@ -411,9 +416,9 @@ def test_loopback_merge_wide_exact(P, k, owner_mode):
 def test_loopback_merge_wide_multi_piece_empty_rank(monkeypatch):
     """Small pieces split every 16-B-key message (a piece boundary may fall
     between a key's two words: the pieces count u64 words), plus an empty rank;
-    OKM_WIRE_DELTAS=1 must not apply to K128 keys."""
-    monkeypatch.setenv("OKM_RCCL_PIECE", "4104")
-    monkeypatch.setenv("OKM_WIRE_DELTAS", "1")
+    wire_deltas = 1 must not apply to K128 keys."""
+    testing.set_knob("piece_bytes", 4104)
+    testing.set_knob("wire_deltas", 1)
     k, P = 63, 3
     recs = _records(15_000, 150_000, 32, hot_every=20)
     ek, ec = _oracle_wide(recs, k)

@@ -4,8 +4,8 @@ owner's merge of per-rank slices, set unions
 (count.rs:52-89).  The runs are split into key-range items by binary search
 (no key moves) and counted by the count kernel (staged slots + compaction,
 the default), the k-way LDS merge kernel of okm_merge.hip
-(OKM_MERGE_KERNEL=1), or the count kernel in two passes straight into the
-exact-size table (OKM_MERGE_KERNEL=2; weighted runs at the memory limit, the
+(test knob sorted_path=1), or the count kernel in two passes straight into the
+exact-size table (sorted_path=2; weighted runs at the memory limit, the
 default for folded tables).  Exact against numpy, for u64 and 128-bit keys,
 weighted and unweighted runs, many runs, dense key ranges, all three."""
 
@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import okm
+from okm import testing
 
 pytestmark = pytest.mark.gpu
 
@@ -56,7 +57,7 @@ def _runs(rng, nruns, n, span, k):
 @pytest.mark.parametrize("merge_kernel", ["", "1", "2"])
 def test_merge_runs_vs_numpy(nruns, n, span, weighted, merge_kernel, monkeypatch):
     if merge_kernel:
-        monkeypatch.setenv("OKM_MERGE_KERNEL", merge_kernel)
+        testing.set_knob("sorted_path", int(merge_kernel))
     rng = np.random.default_rng(nruns * 7 + n)
     k = 31
     runs = _runs(rng, nruns, n, span, k)
@@ -81,8 +82,7 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
     runs = _runs(rng, 6, 400_000, 1 << 62, 31)
     out = []
     for env in (None, "1", "2"):
-        if env:
-            monkeypatch.setenv("OKM_MERGE_KERNEL", env)
+        testing.set_knob("sorted_path", int(env) if env else -1)
         bufs = []
         with okm.KmerCounter(31) as m:
             m.set_timing(True)
@@ -101,7 +101,7 @@ def test_merge_kernel_equals_count_kernel(monkeypatch):
 @pytest.mark.parametrize("merge_kernel", ["", "1", "2"])
 def test_merge_wide_keys(merge_kernel, monkeypatch):
     if merge_kernel:
-        monkeypatch.setenv("OKM_MERGE_KERNEL", merge_kernel)
+        testing.set_knob("sorted_path", int(merge_kernel))
     rng = np.random.default_rng(11)
     k = 45
     runs = []

@@ -21,7 +21,7 @@ import pytest
 import okm
 import restate as R
 from conftest import case_file_bytes, materialize
-from okm import _lib
+from okm import _lib, testing
 from oracle import OracleCounter, OracleCounterWide, count_separated_mt
 
 pytestmark = pytest.mark.gpu
@@ -488,13 +488,13 @@ def test_sampled_placement(genome, cap_mul, part_mul, monkeypatch):
     # batches of >= 64 sampled tiles take the sampled L1 placement (bins sized
     # from every 16th tile's histogram), and >= 4 Mi keys the sampled
     # partition placement (children sized from 1/16 of every chunk);
-    # OKM_L1_CAP_DEBUG / OKM_PART_CAP_DEBUG shrink the capacities so that
-    # some bins overflow and the pass is redone exactly
+    # the knobs l1_cap_permille / part_cap_permille shrink the capacities so
+    # that some bins overflow and the pass is redone exactly
     k = 31
     if cap_mul:
-        monkeypatch.setenv("OKM_L1_CAP_DEBUG", cap_mul)
+        testing.set_knob("l1_cap_permille", round(float(cap_mul) * 1000))
     if part_mul:
-        monkeypatch.setenv("OKM_PART_CAP_DEBUG", part_mul)
+        testing.set_knob("part_cap_permille", round(float(part_mul) * 1000))
     batch = okm.synth_reads(130_000, 150, genome_len=genome, genome_seed=5, seed=31, sub_rate=0.01, n_rate=0.001)
     gk, gc, stats, info = _count_device(batch, k)
     oc = OracleCounter(k)
@@ -528,7 +528,7 @@ def test_sampled_l1_placement_wide():
 
 @pytest.mark.parametrize("k,wide", [(31, False), (21, False), (63, True), (45, True)])
 def test_fan_out_split(k, wide, monkeypatch):
-    # OKM_PART_MAXB caps a partition pass at 3 bits, so a 7 M-key batch leaves
+    # the knob part_max_bits caps a partition pass at 3 bits, so a 7 M-key batch leaves
     # children of ~4-16 Ki keys: each child gets 2^f item slots and the
     # oversized ones are split once more in place on the device (k_fan_split)
     # instead of a host-planned second round (levels stays 1).  The weighted
@@ -536,7 +536,7 @@ def test_fan_out_split(k, wide, monkeypatch):
     from oracle import OracleCounterWide
     # (wide: 9 L1 bits hold children of this batch below one item with 3-bit
     # passes, so the cap is 2 bits there)
-    monkeypatch.setenv("OKM_PART_MAXB", "2" if wide else "3")
+    testing.set_knob("part_max_bits", 2 if wide else 3)
     batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=7, seed=k, sub_rate=0.01,
                             n_rate=0.001)
     gk, gc, stats, info = _count_device(batch, k, wide=wide)
@@ -548,8 +548,8 @@ def test_fan_out_split(k, wide, monkeypatch):
     assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert "fan_split" in stats and info["levels"] == 1, (stats.keys(), info)
     # the weighted table holds fewer entries than the batch has instances: a
-    # 2-bit pass keeps its children oversized at 8 or 9 L1 bits (OKM_L1_BITS)
-    monkeypatch.setenv("OKM_PART_MAXB", "2")
+    # 2-bit pass keeps its children oversized at 8 or 9 L1 bits
+    testing.set_knob("part_max_bits", 2)
     with okm.KmerCounter(k, wide=wide) as m:
         m.set_timing(True)
         m.add_pairs(gk, gc)
@@ -568,7 +568,7 @@ def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
     # a 1-bit pass cap leaves children (~70 Ki keys) too big for one fan-out
     # job (<= 64 Ki): the speculative count is abandoned and the host plans
     # further rounds
-    monkeypatch.setenv("OKM_PART_MAXB", "1")
+    testing.set_knob("part_max_bits", 1)
     k = 31
     batch = okm.synth_reads(300_000, 150, genome_len=3_000_000, genome_seed=8, seed=3, sub_rate=0.01)
     gk, gc, stats, info = _count_device(batch, k)
@@ -583,15 +583,16 @@ def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
                                               (63, True, "A", "2"), (45, True, "B", None)])
 def test_grouped_count(k, wide, mode, maxb, monkeypatch):
     # memory-bounded counting: the L1 parts are counted in key-range groups
-    # (OKM_GROUP_KEYS forces ~1.5 M instances per group), compacted straight
+    # (knob group_keys forces ~1.5 M instances per group), compacted straight
     # into one instance-bound table (A) or into exact per-group tables joined
-    # at the end (B); with OKM_PART_MAXB the groups also take the fan-out path
+    # at the end (B: knob group_exact); with part_max_bits the groups also take
+    # the fan-out path
     # (2 bits for k=63: its 9 L1 bits keep 3-bit children below one item)
     from oracle import OracleCounterWide
-    monkeypatch.setenv("OKM_GROUP_KEYS", "1500000")
-    monkeypatch.setenv("OKM_GROUP_MODE", mode)
+    testing.set_knob("group_keys", 1_500_000)
+    testing.set_knob("group_exact", 1 if mode == "B" else 0)
     if maxb:
-        monkeypatch.setenv("OKM_PART_MAXB", maxb)
+        testing.set_knob("part_max_bits", int(maxb))
     batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=9, seed=k + 1, sub_rate=0.01,
                             n_rate=0.001)
     gk, gc, stats, info = _count_device(batch, k, wide=wide)

@@ -148,10 +148,8 @@ def _reads(rng, genome, n, lo, hi, noise=0.01, lower=0.0):
     return out
 
 
-@pytest.mark.parametrize("mini", ["2", "0"], ids=["minimizer-index", "hash-set"])
 @pytest.mark.parametrize("k", [31, 21, 32, 17, 5, 15, 16, 27])
-def test_query_hits_vs_oracle(k, mini, monkeypatch):
-    monkeypatch.setenv("OKM_QUERY_MINI", mini)
+def test_query_hits_vs_oracle(k):
     rng = np.random.default_rng(100 + k)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000)
     # the DB: the genome's first 60 % as two references
@@ -175,13 +173,9 @@ def _revcomp(b: bytes) -> bytes:
 
 
 @pytest.mark.parametrize("k", [31, 25, 12])
-def test_query_minimizer_index_strands_and_fallback(k, monkeypatch):
-    """The minimizer-bucketed set (okm_probe.hip k_query_hits_mini; OKM_QUERY_MINI=2
-    fails instead of falling back, so the index is what ran) finds a canonical
-    key from either strand of a read; windows whose bucket overflowed (forced
-    here with OKM_QUERY_MINI_KPB, keys per bucket: 32 = many buckets past their
-    32-key limit, 256 = all) probe the hash set instead; every path equals the
-    restatement."""
+def test_query_both_strands_and_rebuild(k):
+    """The device set finds a canonical key from either strand of a read, and
+    a query after more inserts sees them; equal to the restatement."""
     rng = np.random.default_rng(k)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=150_000)
     g = genome.tobytes()
@@ -191,15 +185,12 @@ def test_query_minimizer_index_strands_and_fallback(k, monkeypatch):
     oc.add_records([g[:90_000]])
     db_keys, _ = oc.result(1)
     exp = oracle.query_hits(reads, db_keys, k)
-    for mini, kpb in (("2", ""), ("2", "32"), ("2", "256"), ("0", "")):  # index; mixed; all via the hash set; hash set
-        monkeypatch.setenv("OKM_QUERY_MINI", mini)
-        monkeypatch.setenv("OKM_QUERY_MINI_KPB", kpb)
-        with okm.KmerSet(k, 0, len(db_keys)) as s:
-            s.insert(db_keys)
-            got = s.query_hits(reads)
-            s.insert(db_keys[:10])  # an insert drops the index; the next query rebuilds it
-            again = s.query_hits(reads)
-        assert np.array_equal(got, exp) and np.array_equal(again, exp), (mini, kpb)
+    with okm.KmerSet(k, 0, len(db_keys) // 4) as s:
+        s.insert(db_keys[: len(db_keys) // 2])
+        s.query_hits(reads)
+        s.insert(db_keys)  # grows the table (rehash); the next query sees every key
+        got = s.query_hits(reads)
+    assert np.array_equal(got, exp)
     assert exp[1500:3000].sum() > 0 and exp[3000:4500].sum() > 0  # both strands hit
 
 

@@ -2,8 +2,8 @@
 feed, SURVEY §8 f4: utils.rs:125-152 reads `.gz` through flate2's
 MultiGzDecoder).  CPU only: okm.read_file (okm_read_file) against Python's
 gzip module on FASTQ-like, repetitive, incompressible and fixed-Huffman
-streams, with small chunks so every stream is cut many times;
-OKM_GZ_PARALLEL=2 makes the parallel path's rejection an error instead of a
+streams, with small chunks so every stream is cut many times; the test
+knob gz_strict makes the parallel path's rejection an error instead of a
 serial retry, so these tests see that path's own output."""
 
 import gzip
@@ -14,13 +14,14 @@ import numpy as np
 import pytest
 
 import okm
+from okm import testing
 
 
 @pytest.fixture
-def strict(monkeypatch):
-    monkeypatch.setenv("OKM_GZ_PARALLEL", "2")
-    monkeypatch.setenv("OKM_GZ_PAR_MIN_MB", "0")
-    monkeypatch.setenv("OKM_GZ_CHUNK_KB", "16")
+def strict():
+    testing.set_knob("gz_strict", 1)
+    testing.set_knob("gz_par_min_bytes", 0)
+    testing.set_knob("gz_chunk_bytes", 16 << 10)
 
 
 def _fastq(rng, n, L=150, genome=300_000):
@@ -102,9 +103,8 @@ def test_corrupt_streams_fail(tmp_path, strict):
 def test_serial_retry_without_strict(tmp_path, monkeypatch):
     """Default mode: a member the parallel path rejects is decoded serially,
     which reports the error (or, for good data, gives the same bytes)."""
-    monkeypatch.setenv("OKM_GZ_PAR_MIN_MB", "0")
-    monkeypatch.setenv("OKM_GZ_CHUNK_KB", "16")
-    monkeypatch.delenv("OKM_GZ_PARALLEL", raising=False)
+    testing.set_knob("gz_par_min_bytes", 0)
+    testing.set_knob("gz_chunk_bytes", 16 << 10)
     data = _fastq(np.random.default_rng(7), 6000)
     blob = gzip.compress(data, 1)
     assert _roundtrip(tmp_path, "ok.gz", blob) == data

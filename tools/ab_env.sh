@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of environment settings on one build (box-to-box and
 # process-to-process clocks drift): tools/ab_env.sh REPS "NAME=ENV ..." ...
-# e.g. tools/ab_env.sh 3 "classic=OKM_POOL=classic" "arena=" ; one C2 bench per
+# e.g. tools/ab_env.sh 3 "f8=OKM_FOLD_BYTES=23000000000" "default=" ; one C2 bench per
 # (rep, setting), round-robin; medians per setting at the end.  Extra bench.py
 # arguments in AB_BENCH_ARGS.
 cd "$GRAFT_REPO_ROOT"

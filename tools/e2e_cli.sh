@@ -19,19 +19,19 @@ cat "$D/c2.fastq" > /dev/null
 # five plain runs (the first to a fresh file, then over it): the box's I/O
 # and CPU share vary run to run, so the median is the number to quote
 for i in 1 2 3 4 5; do
-    OKM_CLI_TIMES=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv" 2>&1 | tee -a "$D/plain.txt"
+    OKM_PROFILE_HOST=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv" 2>&1 | tee -a "$D/plain.txt"
 done
 python3 -c "import re,statistics,sys; v=[float(x) for x in re.findall(r'e2e ([0-9.]+) s', open(sys.argv[1]).read())]; print('plain runs', v, 'median', statistics.median(v), 'best', min(v))" "$D/plain.txt"
-OKM_CLI_TIMES=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out2.tsv" -m 2
+OKM_PROFILE_HOST=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out2.tsv" -m 2
 run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out.tsv.gz"
 # the two halves of that run apart: gzip input to a plain table (three runs with
 # the single member inflated on the host threads, okm_inflate.cpp, then one
 # with the serial libdeflate inflate it replaced), plain input to a gzip table
 for i in 1 2 3; do
-    OKM_CLI_TIMES=1 OKM_GZ_PROF=1 run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out_gzin.tsv"
+    OKM_PROFILE_HOST=1 run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out_gzin.tsv"
 done
-OKM_CLI_TIMES=1 OKM_GZ_PARALLEL=0 run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out_gzin_serial.tsv"
-OKM_CLI_TIMES=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out_gzout.tsv.gz"
+OKM_PROFILE_HOST=1 OKM_GZ_PARALLEL=0 run count -k 31 -i "$D/c2.fastq.gz" -o "$D/out_gzin_serial.tsv"
+OKM_PROFILE_HOST=1 run count -k 31 -i "$D/c2.fastq" -o "$D/out_gzout.tsv.gz"
 run -v count -k 31 -i "$D/c2.fastq" -o "$D/out.tsv"
 wc -l "$D/out.tsv" "$D/out2.tsv"
 cmp "$D/out.tsv" <(zcat "$D/out.tsv.gz") && echo "gz output identical"

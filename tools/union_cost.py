@@ -1,12 +1,16 @@
 """Set-mode union of R sorted runs (compare.rs:51-66's get_all_kmers_unified,
 the C5 databases) through the count kernel (default) and the k-way merge
-kernel (OKM_MERGE_KERNEL=1 in the environment): one JSON line per R.
+kernel (--merge-kernel: the test knob sorted_path = 1): one JSON line per R.
 usage: python tools/union_cost.py [R,...] [keys per run]"""
 import json
 import os
 import statistics
 import sys
 import time
+
+MERGE_KERNEL = "--merge-kernel" in sys.argv
+if MERGE_KERNEL:
+    sys.argv.remove("--merge-kernel")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "orion-kmer_amd")]
@@ -37,5 +41,5 @@ with okm.KmerCounter(31, "set") as u:
             u.synchronize()
             times.append((time.perf_counter() - t0) * 1e3)
         print(json.dumps({"runs": R, "keys_in": sum(m for _, m in bufs[:R]), "union": nd,
-                          "merge_kernel": bool(os.environ.get("OKM_MERGE_KERNEL")),
+                          "merge_kernel": MERGE_KERNEL,
                           "ms": round(statistics.median(times[1:]), 2)}))
