@@ -263,9 +263,10 @@ def test_c3_p1_full_size(monkeypatch):
     # ~1.0e9 genomic + ~0.6e9 error k-mers (~1.8e9 expected; measured 1.61e9)
     assert 1.4e9 < nd < 1.9e9
     d1 = _table_digest(keys, counts)
-    # exact parity of the FOLDED table on 12 key ranges against the rolling
+    # exact parity of the FOLDED table on 64 key ranges of 1/4096 of the key
+    # space each (1/64 in all, 16 per first-base quarter) against the rolling
     # range restatement over ALL 167,772,160 reads (count.rs:48,52-89,106-119)
-    _exact_key_ranges(keys, counts, buf, n, stride, k)
+    _exact_key_ranges(keys, counts, buf, n, stride, k, ranges=c3_key_ranges(k, per_quarter=16, width_bits=12))
     del keys, counts
     ctr.close()
     # the same input folded twice as often: the same table
@@ -306,11 +307,11 @@ def c3_key_ranges(k, per_quarter=3, width_bits=13):
     return out
 
 
-def _exact_key_ranges(keys, counts, buf, n_reads, stride, k, threads=None, chunk_reads=4_194_304):
-    """Compare the device table's entries inside c3_key_ranges() exactly with
-    the restatement over every read of the device batch `buf` (streamed to
-    the host in chunks)."""
-    ranges = c3_key_ranges(k)
+def _exact_key_ranges(keys, counts, buf, n_reads, stride, k, threads=None, chunk_reads=4_194_304, ranges=None):
+    """Compare the device table's entries inside `ranges` (default
+    c3_key_ranges()) exactly with the restatement over every read of the
+    device batch `buf` (streamed to the host in chunks)."""
+    ranges = ranges or c3_key_ranges(k)
     thr = threads or max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1),
                                 os.cpu_count() or 1))
     bounds = torch.tensor([v for r in ranges for v in r], dtype=torch.int64, device=keys.device)

@@ -3,9 +3,13 @@ all 64 WGS-shaped samples (okm.workloads.c5_samples: 64 runs of
 data_metagenome.json.gz, <= 256 Mbases each, 11.19 Gbases in all), then
 compare.rs:51-66 of DB1 (samples 0-31) against DB2 (samples 32-63).
 
-Exact against the restatement: the sets of 12 samples of every size class
-(0.1 to 256 Mbases, read lengths 365 to 20,008; oracle/okm_oracle.c over the
-host cores) and the unions / intersection of four of them (numpy).  At the
+Exact against the restatement: EVERY one of the 64 sets on 12 key ranges
+(1/8192 of the key space each, spread over the first-base quarters; the
+range-filtered restatement over every read of every sample), the whole sets
+of 12 samples of every size class (0.1 to 256 Mbases, read lengths 365 to
+20,008; oracle/okm_oracle.c over the host cores), the unions / intersection
+of four of them (numpy), and |A|, |B|, |A ∩ B| of the full compare restricted
+to the 12 ranges against the oracle-built sets.  At the
 full workload: |A|, |B|, |A ∩ B| and the Jaccard f64 of the one-GPU compare
 (set unions of sorted runs + device intersection) equal numpy's union1d /
 intersect1d of all 64 device sets on the host, and the distributed compare
@@ -21,7 +25,8 @@ import pytest
 
 import okm
 from okm import workloads
-from oracle import count_separated_mt
+from oracle import count_separated_mt, count_separated_ranges_mt
+from test_gpu_c3 import c3_key_ranges, dev_tensor
 
 pytestmark = pytest.mark.gpu
 K = 31
@@ -52,11 +57,15 @@ def c5_sets():
     # + 8 samples across the size classes and read lengths (0.7 to 256 Mbases;
     # 256 Mbases at 365 bp and at 20,008 bp reads)
     exact = smallest + [7, 15, 24, 58, 57, 53, 0, 49]
-    sets, kept, bases = [], {}, 0
+    sets, kept, bases, ranged = [], {}, 0, []
+    ranges = c3_key_ranges(K)
     with okm.KmerCounter(K, "set") as ctx:
         for s in range(64):
             b = workloads.c5_sample(s)
             bases += len(b) - int((b == 10).sum())
+            # the oracle's set of this sample on the 12 key ranges (every read)
+            ek, _, _ = count_separated_ranges_mt([b], K, ranges, _threads())
+            ranged.append(ek)
             d = okm.DeviceBuffer(len(b))
             d.upload(b)
             ctx.reset()
@@ -66,11 +75,29 @@ def c5_sets():
             sets.append(keys)
             if s in exact:
                 kept[s] = b
-    return sets, kept, bases, smallest
+    return sets, kept, bases, smallest, ranged
+
+
+def _in_ranges(keys, ranges):
+    cut = [np.searchsorted(keys, np.uint64(v)) for r in ranges for v in r]
+    return np.concatenate([keys[cut[2 * i]:cut[2 * i + 1]] for i in range(len(ranges))])
+
+
+def test_c5_every_sample_set_exact_on_key_ranges(c5_sets):
+    """build.rs:50-58: each of the 64 device sets, restricted to the 12 key
+    ranges, equals the restatement's set of that sample on those ranges."""
+    sets, _, _, _, ranged = c5_sets
+    ranges = c3_key_ranges(K)
+    total = 0
+    for s in range(64):
+        got = _in_ranges(sets[s], ranges)
+        assert np.array_equal(got, ranged[s]), s
+        total += len(got)
+    assert total > 100_000
 
 
 def test_c5_sample_sets_exact_subset_and_properties(c5_sets):
-    sets, kept, bases, smallest = c5_sets
+    sets, kept, bases, smallest, _ = c5_sets
     assert 11.0e9 < bases < 11.4e9  # the stated workload: 11.19 Gbases
     assert len(kept) == 12
     for s, b in kept.items():  # exact sets (build.rs:50-58 DashSet) vs the restatement
@@ -97,7 +124,8 @@ def test_c5_sample_sets_exact_subset_and_properties(c5_sets):
 
 
 def _one_gpu_compare(sets):
-    """compare.rs:51-66 on one GPU: each DB's union of sorted runs, |A ∩ B|."""
+    """compare.rs:51-66 on one GPU: each DB's union of sorted runs, |A ∩ B|;
+    also the two unions restricted to the 12 key ranges (host copies)."""
     bufs, res = [], []
     for h in (0, 1):
         u = okm.KmerCounter(K, "set")
@@ -111,7 +139,18 @@ def _one_gpu_compare(sets):
     pa, _, _ = res[0][0].result_device()
     pb, _, _ = res[1][0].result_device()
     inter = okm.set_intersection_size_device(pa, res[0][1], pb, res[1][1])
-    out = (res[0][1], res[1][1], inter)
+    ranges = c3_key_ranges(K)
+
+    def in_ranges_device(ptr, n):  # the union's keys inside the ranges, sliced on the device
+        import torch
+        keys = dev_tensor(ptr, n)
+        bounds = torch.tensor([v for r in ranges for v in r], dtype=torch.int64, device=keys.device)
+        cut = torch.searchsorted(keys, bounds).cpu().tolist()  # keys < 2^62: signed order is unsigned order
+        return np.concatenate([keys[cut[2 * i]:cut[2 * i + 1]].cpu().numpy() for i in range(len(ranges))]).view(
+            np.uint64)
+
+    unions_in_ranges = (in_ranges_device(pa, res[0][1]), in_ranges_device(pb, res[1][1]))
+    out = (res[0][1], res[1][1], inter, unions_in_ranges)
     for u, _ in res:
         u.close()
     for d in bufs:
@@ -147,7 +186,7 @@ def c5_compare(c5_sets):
 def test_c5_compare_exact_vs_host_unions(c5_sets, c5_compare):
     """|A|, |B|, |A ∩ B| and the Jaccard f64 (compare.rs:58-66) of the one-GPU
     compare over all 64 device sets equal numpy's on the host."""
-    na, nb, inter = c5_compare
+    na, nb, inter, _ = c5_compare
     ha, hb, hi = _host_compare(c5_sets[0], _threads())
     assert (na, nb, inter) == (ha, hb, hi)
     union = na + nb - inter
@@ -155,9 +194,22 @@ def test_c5_compare_exact_vs_host_unions(c5_sets, c5_compare):
     assert 0 < inter < min(na, nb)
 
 
+def test_c5_compare_on_key_ranges_vs_oracle_sets(c5_sets, c5_compare):
+    """compare.rs:51-66 restricted to the 12 key ranges: the device unions A
+    and B (over all 32 + 32 device sets) equal the unions of the ORACLE's
+    per-sample range sets, and so do |A|, |B|, |A ∩ B| there."""
+    ranged = c5_sets[4]
+    ua, ub = c5_compare[3]
+    oa = np.unique(np.concatenate(ranged[:32]))
+    ob = np.unique(np.concatenate(ranged[32:]))
+    assert np.array_equal(ua, oa) and np.array_equal(ub, ob)
+    inter = len(np.intersect1d(ua, ub, assume_unique=True))
+    assert inter == len(np.intersect1d(oa, ob, assume_unique=True)) > 0
+
+
 def test_c5_distributed_compare_p8_equals_one_gpu(c5_sets, c5_compare):
     sets = c5_sets[0]
-    want = c5_compare
+    want = c5_compare[:3]
     na, nb, inter = want
     assert 0 < inter < min(na, nb)  # the two halves share half of their genomes
     P = 8

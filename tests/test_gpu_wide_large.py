@@ -119,10 +119,11 @@ def test_k63_c4_size_properties_memory_and_exact_ranges():
         lo, hi = keys[idx, 0], keys[idx, 1]
         rlo, rhi = _rc128(lo, hi, K)
         assert not bool(_u128_lt(rlo, rhi, lo, hi).any()), "a key above its reverse complement"
-        # exact on six key ranges of 1/256 of the key space each, spread over the
-        # first-base quarters (canonical keys are dense in the low ones, sparse
-        # in the last), each against a range-filtered restatement of every read
-        ranges = [(3, 4), (45, 46), (90, 91), (130, 131), (170, 171), (200, 201)]
+        # exact on 16 key ranges of 1/256 of the key space each (1/16 in all),
+        # spread over the first-base quarters (canonical keys are dense in the
+        # low ones, sparse in the last), each against a range-filtered
+        # restatement of every read (the 16 scans run on the host threads at once)
+        ranges = [(b, b + 1) for b in (3, 20, 35, 45, 60, 75, 90, 105, 120, 130, 145, 160, 170, 185, 200, 230)]
         def below(bin_):  # keys whose top 8 bits are < bin_ (they are sorted)
             return sum(int(((keys[a:a + step, 1] >> (2 * K - 64 - 8)) < bin_).sum().item()) for a in range(0, n, step))
 
