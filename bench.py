@@ -422,7 +422,7 @@ def main():
     if c3 is not None:
         out["c3"] = ({k: c3[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                          "scaling", "config", "exchange_impl", "phase_ms_per_step_rank0",
-                                         "survey_roofline")}
+                                         "survey_roofline", "memory")}
                      if "value" in c3 else c3)
     emit(out)
     if comm is not None:
@@ -612,6 +612,12 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
                                     "merge": round(xt[2] / steps * 1e3, 2)},
         "kernels": kernels,
         "engine": info,
+        # rank 0's device memory: what its arena mapped at the end of the timed
+        # jobs (device_bytes, idle cached chunks included) and the most it held
+        # in use at once (device_peak_bytes); the result itself is 16 B / key
+        "memory": {"device_bytes": int(info["device_bytes"]), "device_peak_bytes": int(info["device_peak_bytes"]),
+                   "host_bytes": int(info["host_bytes"]), "spills": int(info["spills"]),
+                   "result_bytes": int(n_last) * 16},
     }
     return out
 

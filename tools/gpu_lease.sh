@@ -52,7 +52,7 @@ case "$TASK" in
 suite)
     K=()
     [ -n "$1" ] && K=(-k "$1")
-    timeout -k 10 1500 $PY -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+    timeout -k 10 1500 $PY -m pytest tests -m gpu -x -v --durations=30 --timeout 300 --timeout-method thread "${K[@]}" \
         > "$OUT/suite.log" 2>&1
     rc=$?
     tail -30 "$OUT/suite.log"
