@@ -792,12 +792,12 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     hs[3 * P] = st != OKM_OK;
     HIP_TRY(hipMemcpyAsync(m->sizes.p, hs.data(), row * sizeof(ull), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->sizes.as<ull>() + P, 0, 2 * P * sizeof(ull), s));
-    if (!set && st == OKM_OK && pblocks) {
+    if (!set && st == OKM_OK && pblocks && n_sent) {  // (n_sent == 0: nothing leaves this rank)
         hipLaunchKernelGGL(k_pack_counts<false>, dim3((uint32_t)pblocks), dim3(256), 0, s, dc, n, m->cut.as<ull>(), P,
                            m->low.as<uint8_t>(), m->sizes.as<ull>() + P, nullptr, nullptr, skip0, skip1);
         HIP_TRY(hipGetLastError());
     }
-    if (deltas && st == OKM_OK && dblocks) {
+    if (deltas && st == OKM_OK && dblocks && n_sent) {
         hipLaunchKernelGGL(k_pack_deltas<false>, dim3((uint32_t)dblocks), dim3(256), 0, s, dk, n, m->cut.as<ull>(), P,
                            m->k5.as<uint8_t>(), m->sizes.as<ull>() + 2 * P, nullptr, nullptr, skip0, skip1);
         HIP_TRY(hipGetLastError());

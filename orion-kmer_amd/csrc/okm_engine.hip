@@ -61,15 +61,21 @@ static constexpr size_t kArenaChunk = size_t(1) << 30;  // 1 GiB: 64 MiB chunks 
 // other contexts'), and an allocation that still does not fit fails with
 // OKM_E_NOMEM -- which the counting paths plan around (key-range groups,
 // folding, tables moved to host memory: DESIGN.md §5).
-static double parse_budget(const char *e, double total) {
-    if (!e || !*e) return 0.9 * total;
+// A byte count: "28.8e9", "24G" (K/M/G/T: powers of 1024); < 0 when unparsable.
+static double parse_bytes(const char *e) {
     char *end = nullptr;
     double v = strtod(e, &end);
-    if (!(v > 0)) return 0.9 * total;
+    if (end == e || !(v >= 0)) return -1.0;
     if (end && *end) {
         const char u = (char)(*end | 0x20);
         v *= u == 'k' ? 1024.0 : u == 'm' ? 1048576.0 : u == 'g' ? 1073741824.0 : u == 't' ? 1099511627776.0 : 1.0;
     }
+    return v;
+}
+static double parse_budget(const char *e, double total) {
+    if (!e || !*e) return 0.9 * total;
+    const double v = parse_bytes(e);
+    if (!(v > 0)) return 0.9 * total;
     return v <= 1.0 ? v * total : std::min(v, total);
 }
 static double device_total_bytes(int device) {
@@ -2042,6 +2048,8 @@ static okm_status count_spilled(okm_ctx *c) {
 // + LDS counting + compaction.
 static okm_status count_general(okm_ctx *c) {
     const uint32_t twok = 2u * c->k;
+    bool weighted = false;
+    for (auto &r : c->runs) weighted |= (r.counts != nullptr);
     // sort-mode items hold at most count_item_capacity() instances; items with
     // at most count_dense_bits() remaining key bits are counted by direct
     // address and may be any size (okm_count.hip)
@@ -2052,8 +2060,6 @@ static okm_status count_general(okm_ctx *c) {
     // pass holds is still counted exactly, in several passes (okm_count.hip).
     const uint64_t target = item_max * 3 / 4;          // aim below it after a split (canonical-key density
                                                        // gradients and line padding must still fit)
-    bool weighted = false;
-    for (auto &r : c->runs) weighted |= (r.counts != nullptr);
     uint32_t maxb = log2_floor(part_max_bins(weighted, c->wide));  // bits one pass can split
     if (const int64_t e = test_knob(OKM_TEST_PART_MAX_BITS); e > 0)  // tests: small passes (fan-out, host rounds)
         maxb = std::max<uint32_t>(1, std::min<uint32_t>(maxb, (uint32_t)e));
@@ -2093,11 +2099,15 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                               const CountPlan &cp, const ResDst *dst) {
     const uint32_t twok = cp.twok, capbits = cp.capbits, maxb = cp.maxb;
     const uint64_t item_max = cp.item_max, target = cp.target;
-    auto plan = [&](uint32_t i) -> uint32_t {  // bits to split part i by (0: keep)
+    // bits to split part i by (0: keep).  eager (the host rounds, which only
+    // see parts the device round could not bring to one item -- mostly a hot
+    // key, which no split shrinks): a whole pass, so that the key bits run out
+    // in ~(2k - 11) / maxb rounds rather than one bit per round
+    auto plan = [&](uint32_t i, bool eager) -> uint32_t {
         const Part &p = parts[i];
         const uint32_t rem = twok - p.consumed;
         if (p.len <= item_max || rem <= capbits) return 0;
-        uint32_t b = 1;
+        uint32_t b = eager ? maxb : 1;
         while (b < maxb && (p.len >> b) > target) ++b;
         return std::min(b, rem);
     };
@@ -2116,7 +2126,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
         bool any = false;
         for (uint32_t i = 0; i < parts.size(); ++i) {
             all.push_back(i);
-            bits.push_back(plan(i));
+            bits.push_back(plan(i, false));
             any |= bits.back() != 0;
         }
         if (any) {
@@ -2243,7 +2253,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
     for (int round = 1; round < 64; ++round) {
         std::vector<uint32_t> todo, bits;
         for (uint32_t i = 0; i < parts.size(); ++i) {
-            const uint32_t b = plan(i);
+            const uint32_t b = plan(i, true);
             if (!b) continue;
             todo.push_back(i);
             bits.push_back(b);
@@ -2555,7 +2565,8 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
         // bytes of working set; C3 on one GPU: 8 % 596 ms, 10 % 569 ms; 12 % needs
         // key-range groups: 2.5 s)
         const char *fe = getenv("OKM_FOLD_BYTES");
-        c->fold_bytes = fe ? (uint64_t)atoll(fe) : (uint64_t)(hbm_budget(device) / 9.0);
+        const double fv = fe && *fe ? parse_bytes(fe) : -1.0;
+        c->fold_bytes = fv >= 0 ? (uint64_t)fv : (uint64_t)(hbm_budget(device) / 9.0);
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->flag, 2 * sizeof(unsigned long long)) != hipSuccess ||
