@@ -130,6 +130,18 @@ __device__ __forceinline__ uint32_t home_of(const K128 &key, uint32_t r) {
 __device__ __forceinline__ uint32_t half_shift(uint32_t h) { return (h & 1u) << 4; }
 __device__ __forceinline__ uint32_t half_of(uint32_t word, uint32_t h) { return (word >> half_shift(h)) & 0xFFFFu; }
 
+// Where an item's sorted (key, count) run goes: its slot of the staging array
+// at out_off, or -- out_keys == nullptr, "in place" -- over its own input: a
+// single-segment item in a level array (okm_engine.hip count_parts) reads all
+// its keys before it writes any and has at least as many instances as it
+// writes keys, so its run replaces its keys (counts stay at out_counts +
+// out_off).  No other item reads that range.
+template <typename KT>
+__device__ __forceinline__ KT *out_slot_keys(const DevItem &it, uint64_t *out_keys) {
+    return out_keys ? reinterpret_cast<KT *>(out_keys) + it.out_off
+                    : const_cast<KT *>(reinterpret_cast<const KT *>(it.keys0));
+}
+
 // Instances of an item (scalar loop over its segments: block-uniform).
 __device__ __forceinline__ uint64_t item_total(const DevItem &it, const DevSeg *__restrict__) {
     return it.total;
@@ -283,7 +295,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
-    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
+    KT *okeys = out_slot_keys<KT>(it, out_keys_raw);
     KT *sk = reinterpret_cast<KT *>(lds);
     ull *sw = reinterpret_cast<ull *>(sk + kCapI);
     uint32_t *hc = reinterpret_cast<uint32_t *>(sw + (W ? kCapI : 0));
@@ -400,7 +412,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     lds_sync();
     for (uint32_t p = t; p < (nowrite ? 0u : D); p += kCB) {
         const uint32_t b = first[p], e = first[p + 1];
-        out_keys[out_off + p] = sk[b];
+        okeys[p] = sk[b];
         ull c = 0;
         if (W)
             for (uint32_t i = b; i < e; ++i) c += sw[i];
@@ -423,6 +435,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
                                              uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts) {
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
+    ull *okeys = out_slot_keys<ull>(it, out_keys);
     typedef Lds<W> L;
     typedef typename CountType<W>::T CT;
     const uint32_t t = threadIdx.x;
@@ -584,7 +597,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
         for (int q = 0; q < kHomesPer; ++q) {
             if (!NW && tg[q] != kEmptyKey) {
                 const uint64_t o = out_off + ho[q] + lq[q];
-                out_keys[o] = tg[q];
+                okeys[o - out_off] = tg[q];
                 const uint64_t cq = W ? (uint64_t)tw[q] : (uint64_t)nq[q];
                 store_count<W>(out_counts, o, cq);
             }
@@ -602,7 +615,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             const uint32_t h = home_of(x, r);
             const uint32_t tag_below = prange[k] >> 31;
             const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + tag_below;
-            out_keys[o] = x;
+            okeys[o - out_off] = x;
             store_count<W>(out_counts, o, (uint64_t)pc[k]);
         }
     }
@@ -626,7 +639,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
     const uint32_t r = it.rem_bits;
     const uint32_t nslots = 1u << r;
     const ull mask = (ull)nslots - 1ull;
-    KT *out_keys = reinterpret_cast<KT *>(out_keys_raw);
+    KT *okeys = out_slot_keys<KT>(it, out_keys_raw);
     KT *slot_key = reinterpret_cast<KT *>(lds);               // [kHomes]
     CT *cnt = reinterpret_cast<CT *>(slot_key + kHomes);      // [kHomes]
     lds_sync();  // the previous item's LDS state is dead
@@ -665,7 +678,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
     for (uint32_t q = 0; q < kHomesPer; ++q) {
         const uint32_t j = t * kHomesPer + q;
         if (!nowrite && j < nslots && cnt[j] != 0) {
-            out_keys[o] = slot_key[j];
+            okeys[o - it.out_off] = slot_key[j];
             store_count<W>(out_counts, o, (uint64_t)cnt[j]);
             ++o;
         }

@@ -608,20 +608,26 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
     const uint32_t nw = gridDim.x * 4u - 1u;
     uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (item >= nw) return;  // the last wave: its items belong to wave 0
+    // sk == nullptr: the items' runs were staged in place (over their input,
+    // okm_count.hip out_slot_keys), the counts at sc + out_off
     uint64_t n = 0, src = 0, dst = 0;
+    const KT *kb = nullptr;
     if (item < nitems) {
         n = n_out[item];
         src = items[item].out_off;
         dst = dense_off[item];
+        kb = sk ? sk + src : reinterpret_cast<const KT *>(items[item].keys0);
     }
     const uint32_t *sc32 = reinterpret_cast<const uint32_t *>(sc);
     for (; item < nitems; item += nw) {
         const uint32_t nxt = item + nw;
         uint64_t nn = 0, ns = 0, nd = 0;
+        const KT *nkb = nullptr;
         if (nxt < nitems) {
             nn = n_out[nxt];
             ns = items[nxt].out_off;
             nd = dense_off[nxt];
+            nkb = sk ? sk + ns : reinterpret_cast<const KT *>(items[nxt].keys0);
         }
         uint64_t j = lane;
         for (; j + 192 < n; j += 256) {
@@ -629,7 +635,7 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
             uint64_t c[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                k[q] = sk[src + j + 64 * q];
+                k[q] = kb[j + 64 * q];
                 c[q] = NARROW ? (uint64_t)sc32[src + j + 64 * q] : sc[src + j + 64 * q];
             }
 #pragma unroll
@@ -639,12 +645,13 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
             }
         }
         for (; j < n; j += 64) {
-            dk[dst + j] = sk[src + j];
+            dk[dst + j] = kb[j];
             dc[dst + j] = NARROW ? (uint64_t)sc32[src + j] : sc[src + j];
         }
         n = nn;
         src = ns;
         dst = nd;
+        kb = nkb;
     }
 }
 

@@ -911,6 +911,8 @@ static okm_status fold(okm_ctx *c) {
     OKM_TRY(spill_tables(c, 4.5 * uncounted_bytes(c)));
     OKM_TRY(count_unsorted_to_table(c));
     c->folds += 1;
+    if (c->hprof.on)
+        fprintf(stderr, "[okm fold] #%u counted: peak in use so far %.1f GB\n", c->folds + 0u, c->pool.peak() / 1e9);
     // A context that folds takes 10 L1 bits from here on (and after okm_reset):
     // a fold counts ~3.6 G instances, whose 9-bit parts are too big for one
     // 2048-child pass and go through the fan-out split; 10-bit parts do not
@@ -963,8 +965,10 @@ static okm_status fold(okm_ctx *c) {
             tb += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
             tn += r.n;
         }
-        fprintf(stderr, "[okm fold] #%u: %zu runs of %.3f G keys holding %.1f GB; pool held %.1f GB, cached %.1f GB\n",
-                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held() / 1e9, c->pool.cached() / 1e9);
+        fprintf(stderr, "[okm fold] #%u: %zu runs of %.3f G keys holding %.1f GB; pool held %.1f GB, cached %.1f GB; "
+                        "peak in use so far %.1f GB\n",
+                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held() / 1e9, c->pool.cached() / 1e9,
+                c->pool.peak() / 1e9);
     }
     return OKM_OK;
 }
@@ -1346,12 +1350,12 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     std::vector<void *> &level_bufs, const unsigned long long *guard = nullptr,
                                     unsigned long long *hguard = nullptr, bool *aborted = nullptr,
                                     const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr,
-                                    bool last_use = false) {
+                                    bool last_use = false, bool in_place = false) {
     uint64_t *sk = nullptr, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
     // staged counts: u64 for weighted launches, u32 otherwise (okm_count.hip store_count)
     const uint64_t sc_words = weighted ? std::max<uint64_t>(out_total, 1) : (std::max<uint64_t>(out_total, 1) + 1) / 2;
-    if (last_use && c->may_take_runs && !dst) {
+    if (last_use && c->may_take_runs && !dst && !in_place) {
         const size_t need = std::max<uint64_t>(out_total, 1) * 8 * c->kw;
         size_t best = 0;
         for (auto &r : c->runs) {
@@ -1368,7 +1372,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             if (on) c->input_lost = true;
         }
     } lost{c, false};
-    if (!donated) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
+    if (!donated && !in_place) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
     OKM_TRY(pool_get(c->pool, sc_words, &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
@@ -1377,7 +1381,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     OKM_TRY(pool_get(c->pool, nitems, &defer));
     auto release_own = [&]() {
         for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer})
-            if (!(donated && p == (void *)sk)) c->pool.put(p);
+            if (p && !(donated && p == (void *)sk)) c->pool.put(p);
     };
     auto release_level = [&]() {
         for (void *p : level_bufs) c->pool.put(p);
@@ -1437,21 +1441,36 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         if (dst) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
     }
     // nothing is in flight: the level arrays (and the item flags the kernels
-    // read) are dead, and their blocks may hold the result
+    // read) are dead -- unless they hold the in-place runs the compaction
+    // reads -- and their blocks may hold the result; in place, a dead run
+    // block may (the runs' last use: their keys went into the level arrays)
     const size_t kpad = (std::max<uint64_t>(nd, 1) * 8 * c->kw + 255) & ~(size_t)255;
+    const size_t need = kpad + std::max<uint64_t>(nd, 1) * 8;
     uint8_t *blk = nullptr;
-    if (!dst && c->share_result) {  // the smallest level block that holds keys and counts
+    if (!dst && in_place && last_use && c->may_take_runs) {  // the smallest run block that holds keys and counts
+        Run *best_r = nullptr;
+        size_t best = 0;
+        for (auto &r : c->runs) {
+            const size_t b = r.borrowed || r.host ? 0 : c->pool.size_of(r.keys);
+            if (b >= need && (!best || b < best)) best = b, best_r = &r;
+        }
+        if (best_r) {
+            blk = reinterpret_cast<uint8_t *>(best_r->keys);
+            best_r->keys = nullptr;  // the result's now (the run is released after the count)
+            c->took_runs = true;
+        }
+    } else if (!dst && !in_place && c->share_result) {  // the smallest level block that holds keys and counts
         size_t best = 0, at = 0;
         for (size_t i = 0; i < level_bufs.size(); ++i) {
             const size_t b = c->pool.size_of(level_bufs[i]);
-            if (b >= kpad + std::max<uint64_t>(nd, 1) * 8 && (!best || b < best)) best = b, at = i;
+            if (b >= need && (!best || b < best)) best = b, at = i;
         }
         if (best) {
             blk = static_cast<uint8_t *>(level_bufs[at]);
             level_bufs.erase(level_bufs.begin() + at);
         }
     }
-    release_level();
+    if (!in_place) release_level();
     if (!dst) {
         if (blk) {
             c->res_keys = reinterpret_cast<uint64_t *>(blk);
@@ -1467,6 +1486,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         HIP_TRY(hipGetLastError());
     }
     OKM_TRY(sync(c));  // the result is complete (and a group's buffers may serve the next group)
+    if (in_place) release_level();
     c->pool.put(d_items);
     release_own();
     lost.on = false;
@@ -2224,8 +2244,10 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 unsigned long long hf[3] = {0, 0, 0};
                 bool aborted = false;
                 // every item lies in the level arrays: the runs are not read again
+                // every item is one child in a level array (lk, or fk after the
+                // fan-out): its sorted run is staged in place, over its keys
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
-                                          hf, &aborted, d_nitems, dst, true));
+                                          hf, &aborted, d_nitems, dst, true, true));
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;
