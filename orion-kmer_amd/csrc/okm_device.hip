@@ -596,8 +596,14 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
                                                        uint64_t *__restrict__ dc,
                                                        const ull *__restrict__ guard,
                                                        const ull *__restrict__ err,
-                                                       const ull *__restrict__ d_nitems) {
+                                                       const ull *__restrict__ d_nitems,
+                                                       const ull *__restrict__ d_base) {
     if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
+    if (d_base) {  // the table's next free entry, known on the device only (pipelined key-range groups)
+        const ull b = *d_base;
+        dk += b;
+        dc += b;
+    }
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     // One wave per item (an item holds ~600 entries at C2: a 256-thread block
     // per item left most lanes idle behind three dependent descriptor loads);
@@ -655,11 +661,25 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
     }
 }
 
+// After a group's compaction: *d_base += the group's distinct keys (the
+// exclusive scan's total), unless the launch was abandoned (guard / err).
+__global__ void k_advance_base(ull *__restrict__ d_base, const ull *__restrict__ total, const ull *__restrict__ guard,
+                               const ull *__restrict__ err) {
+    if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
+    *d_base += *total;
+}
+
+void launch_advance_base(void *stream, unsigned long long *d_base, const unsigned long long *total,
+                         const unsigned long long *guard, const unsigned long long *err) {
+    hipLaunchKernelGGL(k_advance_base, dim3(1), dim3(1), 0, (hipStream_t)stream, d_base, total, guard, err);
+}
+
 void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const unsigned long long *n_out, const unsigned long long *dense_off,
                           const uint64_t *src_keys, const uint64_t *src_counts, uint64_t *dst_keys,
                           uint64_t *dst_counts, bool wide, bool narrow, const unsigned long long *guard,
-                          const unsigned long long *err, const unsigned long long *d_nitems) {
+                          const unsigned long long *err, const unsigned long long *d_nitems,
+                          const unsigned long long *d_base) {
     if (!nitems) return;
     constexpr uint32_t cap = 4096;  // grids of 2048 / 8192 measured the same (profiles/AB_LOG.md round 4)
     const dim3 g(nitems / 4u + 1u < cap ? nitems / 4u + 1u : cap), b(256);  // one wave per item
@@ -670,16 +690,16 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
     ull *dk1 = reinterpret_cast<ull *>(dst_keys);
     if (wide && narrow)
         hipLaunchKernelGGL((k_compact_items<K128, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk2, src_counts,
-                           dk2, dst_counts, guard, err, d_nitems);
+                           dk2, dst_counts, guard, err, d_nitems, d_base);
     else if (wide)
         hipLaunchKernelGGL((k_compact_items<K128, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk2,
-                           src_counts, dk2, dst_counts, guard, err, d_nitems);
+                           src_counts, dk2, dst_counts, guard, err, d_nitems, d_base);
     else if (narrow)
         hipLaunchKernelGGL((k_compact_items<ull, true>), g, b, 0, s, items, nitems, n_out, dense_off, sk1, src_counts,
-                           dk1, dst_counts, guard, err, d_nitems);
+                           dk1, dst_counts, guard, err, d_nitems, d_base);
     else
         hipLaunchKernelGGL((k_compact_items<ull, false>), g, b, 0, s, items, nitems, n_out, dense_off, sk1,
-                           src_counts, dk1, dst_counts, guard, err, d_nitems);
+                           src_counts, dk1, dst_counts, guard, err, d_nitems, d_base);
 }
 
 __global__ __launch_bounds__(256) void k_item_flags(const DevItem *__restrict__ items, uint32_t n,

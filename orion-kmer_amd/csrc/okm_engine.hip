@@ -233,6 +233,10 @@ struct DevPool {
         std::lock_guard<std::mutex> g(mu);
         return arena.mapped;
     }
+    size_t in_use() {
+        std::lock_guard<std::mutex> g(mu);
+        return arena.in_use;
+    }
     size_t peak() {
         std::lock_guard<std::mutex> g(mu);
         return peak_in_use;
@@ -1327,6 +1331,11 @@ static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, u
 struct ResDst {
     uint64_t *keys, *counts;
     uint64_t off;
+    // pipelined groups: the table's next entry lives on the device (d_base),
+    // and the count's readback words land in hslot ([0] distinct, [1] error
+    // word, [2..4] guard words) without a host sync (count_grouped)
+    unsigned long long *d_base = nullptr;
+    unsigned long long *hslot = nullptr;
 };
 
 // Count the items in LDS (okm_count.hip), then gather their sorted runs into
@@ -1388,6 +1397,15 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         level_bufs.clear();
         c->pool.put(d_segs);
     };
+    if (c->hprof.on) {
+        uint64_t rb = 0;
+        for (auto &r : c->runs) rb += run_device_bytes(c, r);
+        size_t lb = 0;
+        for (void *p : level_bufs) lb += c->pool.size_of(p);
+        fprintf(stderr, "[okm count] %u items, %.3f G keys: in use %.1f GB (runs %.1f, level %.1f, staged counts %.1f, "
+                        "staged keys %.1f GB)\n", nitems, in_total / 1e9, c->pool.in_use() / 1e9, rb / 1e9, lb / 1e9,
+                c->pool.size_of(sc) / 1e9, (sk && !donated ? c->pool.size_of(sk) : 0) / 1e9);
+    }
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     // items past a device-side count (d_nitems) must scan as empty
     HIP_TRY(hipMemsetAsync(d_nitems ? n_out : n_out + nitems, 0,
@@ -1403,10 +1421,33 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     HIP_TRY(hipGetLastError());
     if (dst) {  // a key-range group: straight into the caller's table (sized by the instance bound)
         c->timer.begin(c->stream);
-        launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, dst->keys + dst->off * c->kw,
-                             dst->counts + dst->off, c->wide, !weighted, guard, c->flag, d_nitems);
+        if (dst->d_base)
+            launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, dst->keys, dst->counts, c->wide,
+                                 !weighted, guard, c->flag, d_nitems, dst->d_base);
+        else
+            launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, dst->keys + dst->off * c->kw,
+                                 dst->counts + dst->off, c->wide, !weighted, guard, c->flag, d_nitems);
         c->timer.end(c->stream, "compact_items", 0.0);  // bytes added once the total is known
         HIP_TRY(hipGetLastError());
+    }
+    if (dst && dst->d_base) {
+        // pipelined group: the table's next entry advances on the device, the
+        // readback waits for the groups' one sync, and every buffer goes back
+        // to the pool now (the next group's kernels reuse them in stream order)
+        launch_advance_base(c->stream, dst->d_base, dense_off + nitems, guard, c->flag);
+        HIP_TRY(hipGetLastError());
+        unsigned long long *hs = dst->hslot;
+        for (int i = 0; i < 6; ++i) hs[i] = 0;
+        HIP_TRY(hipMemcpyAsync(&hs[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&hs[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        if (guard) HIP_TRY(hipMemcpyAsync(&hs[2], guard, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        lost.on = false;  // (groups never write into a run)
+        release_own();
+        release_level();
+        c->pool.put(d_items);
+        if (aborted) *aborted = false;  // (known at the sync: count_grouped recounts every group then)
+        c->n_res = 0;
+        return OKM_OK;
     }
     // [0] distinct, [1] error word, [2..4] guard words, [5] items kept (d_nitems)
     unsigned long long *hv = c->hres + kHresCount;
@@ -1447,18 +1488,18 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     const size_t kpad = (std::max<uint64_t>(nd, 1) * 8 * c->kw + 255) & ~(size_t)255;
     const size_t need = kpad + std::max<uint64_t>(nd, 1) * 8;
     uint8_t *blk = nullptr;
-    if (!dst && in_place && last_use && c->may_take_runs) {  // the smallest run block that holds keys and counts
-        Run *best_r = nullptr;
-        size_t best = 0;
+    if (!dst && in_place && last_use && c->may_take_runs) {
+        // the runs are dead (their keys were partitioned into the level
+        // arrays, where the compaction reads the staged runs): their blocks go
+        // back to the pool before the result is allocated, and neighbouring
+        // ones coalesce (a fold's table then fits where its batches were)
         for (auto &r : c->runs) {
-            const size_t b = r.borrowed || r.host ? 0 : c->pool.size_of(r.keys);
-            if (b >= need && (!best || b < best)) best = b, best_r = &r;
+            if (r.borrowed || r.host) continue;
+            c->pool.put(r.keys);
+            c->pool.put(r.counts);
+            r.keys = r.counts = nullptr;
         }
-        if (best_r) {
-            blk = reinterpret_cast<uint8_t *>(best_r->keys);
-            best_r->keys = nullptr;  // the result's now (the run is released after the count)
-            c->took_runs = true;
-        }
+        c->took_runs = true;  // (the runs are released after the count)
     } else if (!dst && !in_place && c->share_result) {  // the smallest level block that holds keys and counts
         size_t best = 0, at = 0;
         for (size_t i = 0; i < level_bufs.size(); ++i) {
@@ -2246,8 +2287,13 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 // every item lies in the level arrays: the runs are not read again
                 // every item is one child in a level array (lk, or fk after the
                 // fan-out): its sorted run is staged in place, over its keys
+#ifdef OKM_EXP_NO_INPLACE
+                OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
+                                          hf, &aborted, d_nitems, dst, true, false));
+#else
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
                                           hf, &aborted, d_nitems, dst, true, true));
+#endif
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;
@@ -2290,7 +2336,9 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
     std::vector<DevItem> items;
     nitems = (uint32_t)parts.size();
     items.resize(nitems);
+    bool one_seg = true;  // every part one child in a level array: its run is staged in place
     for (uint32_t i = 0; i < nitems; ++i) {
+        one_seg &= parts[i].seg_count == 1;
         // distinct <= instances, and <= 2^remaining-bits
         const uint32_t rem = twok - parts[i].consumed;
         const uint64_t bound = rem >= 63 ? parts[i].len : std::min<uint64_t>(parts[i].len, 1ull << rem);
@@ -2314,8 +2362,10 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
     OKM_TRY(h2d(c, d_segs, segtab.data(), segtab.size() * sizeof(DevSeg)));
     OKM_TRY(h2d(c, d_items, items.data(), nitems * sizeof(DevItem)));
     c->hprof.mark("items.build");
+    // (parts that never took part in a split round keep their run segments:
+    // those are staged in a separate array)
     return count_and_compact(c, d_items, d_segs, nitems, out_total, in_total, weighted, level_bufs, nullptr, nullptr,
-                             nullptr, nullptr, dst);
+                             nullptr, nullptr, dst, false, one_seg && !level_bufs.empty());
 }
 
 // Memory-bounded counting.  The working set of a count (level array, fan-out
@@ -2331,9 +2381,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
                                 const CountPlan &cp) {
     uint64_t total = 0;
     for (const Part &p : parts) total += p.len;
-    // per instance: level + fan-out copy + staged keys (+ slack) + staged counts
-    // (u32 unweighted) (+ weights of both levels)
-    const double ws_key = 8.0 * c->kw * 4 + (weighted ? 8.0 : 4.0) + (weighted ? 16.0 : 0.0);
+    // per instance: level + fan-out copy (+ slack) + staged counts (u32
+    // unweighted) (+ weights of both levels); the keys' runs are staged in
+    // place, over the level array
+    const double ws_key = 8.0 * c->kw * 3 + (weighted ? 8.0 : 4.0) + (weighted ? 16.0 : 0.0);
     const double res_key = 8.0 * c->kw + 8.0;     // result entry (instance bound)
     // one group: the exact result is allocated after the level arrays went
     // back to the pool, beside the staged runs only (count_and_compact)
@@ -2413,33 +2464,87 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &d.counts));
     }
-    okm_engine_info agg = c->info;
+    const okm_engine_info info0 = c->info;
+    okm_engine_info agg = info0;
     agg.work_items = 0;
     agg.max_partition = 0;
     uint32_t ngroups = 0;
+    std::vector<size_t> cuts{0};  // group g: parts [cuts[g], cuts[g + 1])
     for (size_t g0 = 0; g0 < parts.size();) {
         size_t g1 = g0;
         uint64_t keys = 0;
         while (g1 < parts.size() && (g1 == g0 || keys + parts[g1].len <= group_keys)) keys += parts[g1++].len;
-        std::vector<Part> sub(parts.begin() + g0, parts.begin() + g1);
-        c->info.levels = 0;
-        c->info.l2_bits = 0;
-        OKM_TRY(count_parts(c, segtab, sub, weighted, cp, mode == 1 ? &d : nullptr));
-        agg.levels = std::max(agg.levels, c->info.levels);
-        agg.l2_bits = std::max(agg.l2_bits, c->info.l2_bits);
-        agg.work_items += c->info.work_items;
-        agg.max_partition = std::max(agg.max_partition, c->info.max_partition);
-        if (mode == 1) {
-            d.off += c->n_res;
-        } else {
+        cuts.push_back(g1);
+        g0 = g1;
+    }
+    // Mode 1, pipelined: every group's kernels queue behind the previous
+    // group's with no host sync in between (the table's next entry advances
+    // on the device); one sync at the end reads every group's words.  A group
+    // whose speculative count was abandoned (a sampled slot overflowed, a
+    // child too big for one item) left nothing in the table and moved nothing:
+    // then every group is counted again, one sync each (the runs are intact:
+    // groups never write into them).
+    struct Slots {
+        okm_ctx *c;
+        unsigned long long *p = nullptr, *d_base = nullptr;
+        ~Slots() {
+            host_pinned_free(p);
+            c->pool.put(d_base);
+        }
+    } slots{c};
+    unsigned long long *&d_base = slots.d_base;
+    const size_t G = cuts.size() - 1;
+    bool pipelined = mode == 1 && G > 1;
+    if (pipelined) {
+        slots.p = static_cast<unsigned long long *>(host_pinned_alloc(G * 8 * sizeof(unsigned long long)));
+        pipelined = slots.p && pool_get(c->pool, 1, &d_base) == OKM_OK;
+        if (pipelined) HIP_TRY(hipMemsetAsync(d_base, 0, sizeof(unsigned long long), c->stream));
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        bool redo = false;
+        d.off = 0;
+        d.d_base = pipelined ? d_base : nullptr;
+        agg = info0;
+        agg.work_items = 0;
+        agg.max_partition = 0;
+        ngroups = 0;
+        for (size_t g = 0; g < G; ++g) {
+            std::vector<Part> sub(parts.begin() + cuts[g], parts.begin() + cuts[g + 1]);
+            c->info.levels = 0;
+            c->info.l2_bits = 0;
+            if (pipelined) d.hslot = slots.p + 8 * g;
+            OKM_TRY(count_parts(c, segtab, sub, weighted, cp, mode == 1 ? &d : nullptr));
+            agg.levels = std::max(agg.levels, c->info.levels);
+            agg.l2_bits = std::max(agg.l2_bits, c->info.l2_bits);
+            agg.work_items += c->info.work_items;
+            agg.max_partition = std::max(agg.max_partition, c->info.max_partition);
+            if (mode == 1) {
+                d.off += c->n_res;
+            } else {
             // keep the group's table at its exact size: the bound-sized one goes
             // back to the pool and serves the next group
-            OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.0));
-            tabs.push_back(Tab{c->res_keys, c->res_counts, c->n_res});
-            c->res_keys = c->res_counts = nullptr;
+                OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.0));
+                tabs.push_back(Tab{c->res_keys, c->res_counts, c->n_res});
+                c->res_keys = c->res_counts = nullptr;
+            }
+            ++ngroups;
         }
-        ++ngroups;
-        g0 = g1;
+        if (!pipelined) break;
+        unsigned long long base = 0;
+        HIP_TRY(hipMemcpyAsync(&c->hres[kHresCount], d_base, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               c->stream));
+        OKM_TRY(sync(c));
+        base = c->hres[kHresCount];
+        for (size_t g = 0; g < G; ++g) {
+            const unsigned long long *hs = slots.p + 8 * g;
+            if (hs[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hs[1]) + ")");
+            redo |= (hs[2] | hs[3]) != 0;
+            agg.max_partition = std::max<uint64_t>(agg.max_partition, hs[4]);
+        }
+        d.off = base;
+        if (!redo) break;
+        c->hprof.mark("groups.redo");
+        pipelined = false;  // every group again, one sync each
     }
     uint64_t nd = d.off;
     if (mode == 1) {

@@ -254,7 +254,12 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           const uint64_t *src_keys, const uint64_t *src_counts,
                           uint64_t *dst_keys, uint64_t *dst_counts, bool wide, bool narrow,
                           const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr,
-                          const unsigned long long *d_nitems = nullptr);
+                          const unsigned long long *d_nitems = nullptr, const unsigned long long *d_base = nullptr);
+// d_base (pipelined key-range groups): the compaction writes at dst + *d_base,
+// and launch_advance_base then adds the group's distinct keys (*total) to it
+// -- nothing of either when a guard word or *err is set.
+void launch_advance_base(void *stream, unsigned long long *d_base, const unsigned long long *total,
+                         const unsigned long long *guard, const unsigned long long *err);
 // Drop the empty fan-out slots of items[0, nslots) (order kept) into out;
 // *d_nitems (= pos[nslots]) receives the number kept.  flags/pos: nslots + 1
 // words each, scan_tmp: scan_tmp_elems(nslots + 1).

@@ -615,6 +615,29 @@ def test_grouped_count(k, wide, mode, maxb, monkeypatch):
             assert np.array_equal(fk, xk) and np.array_equal(fc, xc), mc
 
 
+@pytest.mark.parametrize("cap", [None, 0.5])
+def test_grouped_count_pipelined_and_redo(cap):
+    """Key-range groups in one instance-bound table, pipelined: every group's
+    kernels queue behind the previous group's with no host sync and the
+    table's next entry advances on the device.  Groups of >= 4 Mi keys take
+    the sampled partition placement; with part_cap_permille = 500 their
+    sampled slots overflow, the speculative counts are abandoned, and every
+    group is counted again one sync at a time.  Exact both ways."""
+    k = 31
+    testing.set_knob("group_keys", 5_000_000)
+    testing.set_knob("group_exact", 0)
+    if cap:
+        testing.set_knob("part_cap_permille", round(cap * 1000))
+    batch = okm.synth_reads(130_000, 150, genome_len=20_000_000, genome_seed=12, seed=4, sub_rate=0.01)
+    gk, gc, stats, info = _count_device(batch, k)
+    oc = OracleCounter(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["groups"] >= 3 and info["distinct"] == len(ec), info
+    assert "part_sample" in stats, stats.keys()
+
+
 def test_c1_cli_full_size(tmp_path):
     """BASELINE configs[0] (C1) through the CLI: byte-identical TSV with the
     restatement's (tests/golden/c1_k21.json), for -m 1 and -m 2."""
