@@ -108,14 +108,18 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
     return wbase + inc - v;
 }
 
-// Per-item output counts: u64 for weighted launches, u32 otherwise (every
-// count of an unweighted launch is < 2^32; the compaction widens them).
+// Per-item output counts: u32 (the compaction widens them) -- every count of
+// an unweighted launch is < 2^32; a weighted launch stages u32 too when
+// `narrow` (the caller redoes it with u64 counts if a count did not fit:
+// ctl[0] bit 8) -- else u64.
 template <bool W>
-__device__ __forceinline__ void store_count(uint64_t *out_counts, uint64_t o, uint64_t c) {
-    if (W)
+__device__ __forceinline__ void store_count(uint64_t *out_counts, uint64_t o, uint64_t c, bool narrow, ull *ctl) {
+    if (W && !narrow) {
         out_counts[o] = c;
-    else
-        reinterpret_cast<uint32_t *>(out_counts)[o] = (uint32_t)c;
+        return;
+    }
+    if (W && c > 0xFFFFFFFFull) atomicOr(reinterpret_cast<unsigned int *>(ctl), 8u);
+    reinterpret_cast<uint32_t *>(out_counts)[o] = (uint32_t)c;
 }
 
 // Top kHomeBits of the r remaining bits (r > kHomeBits): monotone in the key.
@@ -288,7 +292,7 @@ template <bool W, typename KT, int HB = kHomeBits>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
                                               const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
                                               uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
-                                              bool nowrite) {
+                                              bool nowrite, bool narrow, ull *ctl) {
     constexpr uint32_t kH = 1u << HB;         // homes (key sub-ranges in order)
     constexpr uint32_t kHW = kH / 2 / kCB;    // u16-pair counter words per thread (2 or 4)
     static_assert(kHW >= 1 && kH / 2 == kHW * kCB, "whole counter words per thread");
@@ -418,7 +422,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             for (uint32_t i = b; i < e; ++i) c += sw[i];
         else
             c = e - b;
-        store_count<W>(out_counts, out_off + p, c);
+        store_count<W>(out_counts, out_off + p, c, narrow, ctl);
     }
     return __builtin_amdgcn_readfirstlane(D);
 }
@@ -432,7 +436,8 @@ constexpr uint32_t kDeferred = ~0u;
 template <bool W, bool NW = false>
 __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__restrict__ segs, uint32_t nrows,
                                              const ull (&kk)[kPer], const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
-                                             uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts) {
+                                             uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts,
+                                             bool narrow, ull *ctl) {
     const uint32_t r = it.rem_bits;
     const uint64_t out_off = it.out_off;
     ull *okeys = out_slot_keys<ull>(it, out_keys);
@@ -599,7 +604,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
                 const uint64_t o = out_off + ho[q] + lq[q];
                 okeys[o - out_off] = tg[q];
                 const uint64_t cq = W ? (uint64_t)tw[q] : (uint64_t)nq[q];
-                store_count<W>(out_counts, o, cq);
+                store_count<W>(out_counts, o, cq, narrow, ctl);
             }
         }
     }
@@ -616,7 +621,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
             const uint32_t tag_below = prange[k] >> 31;
             const uint64_t o = out_off + half_of(hd[h >> 1], h) + less + tag_below;
             okeys[o - out_off] = x;
-            store_count<W>(out_counts, o, (uint64_t)pc[k]);
+            store_count<W>(out_counts, o, (uint64_t)pc[k], narrow, ctl);
         }
     }
     // late reset: everything but the home offsets (hd, cleared in the next
@@ -633,7 +638,7 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 template <bool W, typename KT>
 __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *__restrict__ segs,
                                                uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
-                                               ull *lds, uint32_t *wsum, bool nowrite) {
+                                               ull *lds, uint32_t *wsum, bool nowrite, bool narrow, ull *ctl) {
     typedef typename CountType<W>::T CT;
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
@@ -679,7 +684,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
         const uint32_t j = t * kHomesPer + q;
         if (!nowrite && j < nslots && cnt[j] != 0) {
             okeys[o - it.out_off] = slot_key[j];
-            store_count<W>(out_counts, o, (uint64_t)cnt[j]);
+            store_count<W>(out_counts, o, (uint64_t)cnt[j], narrow, ctl);
             ++o;
         }
     }
@@ -691,7 +696,7 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
 // after it: separate kernels keep the rare paths' registers out of this one.
 // NW (weighted launches only): count each item's distinct keys into n_out and
 // write nothing -- the first pass of an exact-size two-pass count.
-template <bool W, bool NW = false>
+template <bool W, bool NW = false, bool NARROW = !W>
 __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(W ? 1 : kCountWpe)))
 void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const DevSeg *__restrict__ segs,
                    uint64_t *__restrict__ out_keys, uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
@@ -730,7 +735,7 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
             else
                 load_item<W>(it, segs, kk, ww);
             const uint32_t nrows = (uint32_t)((total + kCB - 1) / kCB);  // rows of kk in use (block-uniform)
-            written = tag_item<W, NW>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts);
+            written = tag_item<W, NW>(it, segs, nrows, kk, ww, lds, wsum, out_keys, out_counts, NARROW, ctl);
         }
         if (t == 0) {
             if (written == kDeferred)
@@ -751,7 +756,7 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                                                     ull *__restrict__ ctl, const uint32_t *__restrict__ defer,
                                                     const ull *__restrict__ guard, const ull *__restrict__ d_nitems,
-                                                    bool nowrite) {
+                                                    bool nowrite, bool narrow) {
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     constexpr int kHB = sizeof(KT) > 8 ? kFullHomeBitsW : kHomeBits;  // full-mode home bits
@@ -787,10 +792,10 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
             continue;
         }
         if (it.rem_bits <= (uint32_t)kDenseBits) {
-            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite);
+            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite, narrow, ctl);
         } else if (total <= (uint64_t)kCapI) {
             written = full_item<W, KT, kHB>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
-                                       out_counts, nowrite);
+                                       out_counts, nowrite, narrow, ctl);
         } else if (threadIdx.x == 0) {
             atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
         }
@@ -802,7 +807,8 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
 void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
-                        const unsigned long long *guard, const unsigned long long *d_nitems, bool nowrite) {
+                        const unsigned long long *guard, const unsigned long long *d_nitems, bool nowrite,
+                        bool narrow) {
     if (!nitems) return;
     hipStream_t s = (hipStream_t)stream;
     // wide (full-mode) count: 8191 workgroups against 4095, k=63 at 1 Gbases
@@ -813,10 +819,10 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
         const uint32_t grid = nitems < wide_cap ? nitems : wide_cap;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite, narrow);
         else
             hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite);
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite, narrow);
         return;
     }
     // workgroups of the unweighted tag kernel (odd, so fan-out slots spread
@@ -832,16 +838,19 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
         if (nowrite)
             hipLaunchKernelGGL((k_count_items<true, true>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
                                out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
-        else
-            hipLaunchKernelGGL((k_count_items<true, false>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
+        else if (narrow)
+            hipLaunchKernelGGL((k_count_items<true, false, true>), dim3(wgrid), dim3(kCB), 0, s, items, nitems, segs,
                                out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
+        else
+            hipLaunchKernelGGL((k_count_items<true, false, false>), dim3(wgrid), dim3(kCB), 0, s, items, nitems,
+                               segs, out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow);
     }
 }
 

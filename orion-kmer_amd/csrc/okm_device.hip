@@ -173,6 +173,7 @@ constexpr int kFanBins = 16;  // <= 4 bits per job
 constexpr int kFanSmallBlock = 512, kFanSmallMax = 16384;
 constexpr int kFanBigBlock = 1024, kFanBigMax = 65536;
 uint64_t fan_split_max() { return (uint64_t)kFanBigMax; }
+uint64_t fan_split_max_in_place() { return (uint64_t)kFanSmallJob; }
 static_assert(kFanSmallMax == kFanSmallJob, "the job list's small/large cut is the small variants' capacity");
 
 template <typename KT, bool W, int FB, int FMAX>

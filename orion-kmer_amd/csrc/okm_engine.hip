@@ -1362,8 +1362,12 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     bool last_use = false, bool in_place = false) {
     uint64_t *sk = nullptr, *sc;
     unsigned long long *n_out, *dense_off, *scan_tmp;
-    // staged counts: u64 for weighted launches, u32 otherwise (okm_count.hip store_count)
-    const uint64_t sc_words = weighted ? std::max<uint64_t>(out_total, 1) : (std::max<uint64_t>(out_total, 1) + 1) / 2;
+    // staged counts: u32 (okm_count.hip store_count) -- for weighted launches
+    // too when their input survives the count (no in-place staging, no
+    // caller's table), which is then redone with u64 counts in the rare case
+    // that one does not fit (a C3 merge of four folded tables: 17 GB less)
+    bool narrow = !weighted || (!in_place && !dst);
+    const uint64_t sc_words = narrow ? (std::max<uint64_t>(out_total, 1) + 1) / 2 : std::max<uint64_t>(out_total, 1);
     if (last_use && c->may_take_runs && !dst && !in_place) {
         const size_t need = std::max<uint64_t>(out_total, 1) * 8 * c->kw;
         size_t best = 0;
@@ -1414,7 +1418,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     c->hprof.mark("items.h2d");
     lost.on = donated;
     launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
-                       d_nitems);
+                       d_nitems, false, narrow);
     c->timer.end(c->stream, "count_items", (8.0 * c->kw + (weighted ? 8.0 : 0.0)) * (double)in_total);
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
@@ -1467,6 +1471,25 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             return OKM_OK;
         }
     }
+    if (weighted && narrow && hv[1] == 8) {
+        // a count past 2^32 in the u32 staging: count again with u64 counts
+        // (the input is intact: staging was separate, nothing was compacted)
+        c->hprof.mark("count.narrow_overflow");
+        c->pool.put(sc);
+        sc = nullptr;
+        narrow = false;
+        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
+        HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
+        HIP_TRY(hipMemsetAsync(d_nitems ? n_out : n_out + nitems, 0,
+                               (d_nitems ? nitems + 1 : 1) * sizeof(unsigned long long), c->stream));
+        launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
+                           d_nitems, false, false);
+        HIP_TRY(hipGetLastError());
+        launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
+        HIP_TRY(hipMemcpyAsync(&hv[0], dense_off + nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&hv[1], c->flag, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        OKM_TRY(sync(c));
+    }
     if (hv[1]) {  // give every buffer of the step back before failing (long-lived contexts)
         release_own();
         release_level();
@@ -1475,7 +1498,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     }
     const uint64_t nd = hv[0];
     const uint32_t nkept = d_nitems ? (uint32_t)std::min<unsigned long long>(nitems, hv[5]) : nitems;
-    const double staged = 8.0 * c->kw + (weighted ? 8.0 : 4.0);  // per distinct key: staged (key, count)
+    const double staged = 8.0 * c->kw + (narrow ? 4.0 : 8.0);  // per distinct key: staged (key, count)
     const double dense = 8.0 * c->kw + 8.0;                      // ... and its dense result entry
     if (!c->timer.stats.empty()) {
         c->timer.stats[c->timer.id_of("count_items")].alg_bytes += staged * (double)nd;
@@ -1522,7 +1545,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         }
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nkept, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide,
-                             !weighted, nullptr, nullptr, nullptr);
+                             narrow, nullptr, nullptr, nullptr);
         c->timer.end(c->stream, "compact_items", (staged + dense) * (double)nd);
         HIP_TRY(hipGetLastError());
     }
@@ -2199,6 +2222,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
             // twice the average child of the biggest part (canonical keys are
             // not uniform inside a part).
             FanOut fan;
+            const bool fan_in_place = !weighted && !c->wide;
             {
                 uint32_t fb = 0;
                 for (uint32_t i = 0; i < parts.size(); ++i) {
@@ -2210,7 +2234,10 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 }
                 fan.bits = fb;
                 fan.target = target;
-                fan.split_max = fan_split_max();
+                // unweighted u64 keys: oversized children are split in place
+                // (no second level array: a C3 fold's is ~45 GB); a child too
+                // big for the register variant then takes a host round
+                fan.split_max = fan_in_place ? fan_split_max_in_place() : fan_split_max();
             }
             c->hprof.mark("split.plan");
             uint64_t keys_in = 0;
@@ -2254,10 +2281,12 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 launch_make_items(c->stream, L.d_offs, L.d_ends, L.nout, d_par, (uint32_t)par.size(), L.lk, L.lc,
                                   d_items, d_segs, item_max, capbits, flags, c->kw, fan, doff);
                 HIP_TRY(hipGetLastError());
-                if (fan.bits) {  // oversized children split into a second level array (same offsets)
-                    uint64_t *fk, *fc = nullptr;
-                    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &fk));
-                    level_bufs.push_back(fk);
+                if (fan.bits) {  // oversized children split into a second level array (same offsets), or in place
+                    uint64_t *fk = L.lk, *fc = nullptr;
+                    if (!fan_in_place) {
+                        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &fk));
+                        level_bufs.push_back(fk);
+                    }
                     if (L.lc) {
                         OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &fc));
                         level_bufs.push_back(fc);
@@ -2287,13 +2316,8 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 // every item lies in the level arrays: the runs are not read again
                 // every item is one child in a level array (lk, or fk after the
                 // fan-out): its sorted run is staged in place, over its keys
-#ifdef OKM_EXP_NO_INPLACE
-                OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
-                                          hf, &aborted, d_nitems, dst, true, false));
-#else
                 OKM_TRY(count_and_compact(c, d_items, d_segs, nslots, L.total, L.total, weighted, level_bufs, flags,
                                           hf, &aborted, d_nitems, dst, true, true));
-#endif
                 if (!aborted) {
                     c->info.max_partition = hf[2];
                     return OKM_OK;

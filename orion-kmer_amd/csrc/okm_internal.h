@@ -157,7 +157,8 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                         uint64_t *out_keys, uint64_t *out_counts, unsigned long long *n_out,
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
                         const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr,
-                        bool nowrite = false);  // nowrite: n_out only (weighted or wide launches)
+                        bool nowrite = false,  // nowrite: n_out only (weighted or wide launches)
+                        bool narrow = false);  // weighted: u32 staged counts (ctl[0] |= 8 when one does not fit)
 
 // k-way merge of sorted runs (okm_merge.hip): items as built by
 // launch_sorted_items (each segment of an item a sorted unique run of keys),
@@ -195,6 +196,9 @@ struct FanOut {
     DevFanJob *jobs = nullptr;  // [nout]; job count in flags[3]
 };
 uint64_t fan_split_max();
+// Unweighted jobs of at most this many keys are split in place (dk == sk):
+// the register variant reads a job's keys before it writes any.
+uint64_t fan_split_max_in_place();
 
 // d_nitems (count kernels, compaction): when given, the item count is
 // min(nitems, *d_nitems) -- a count known only on the device.
