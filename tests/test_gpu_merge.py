@@ -143,3 +143,41 @@ def test_merge_hot_range_many_runs():
         gk, gc = m.result(1)
     assert np.array_equal(gk, base)
     assert (gc == np.uint64(64 * 65 // 2)).all()
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_merge_counts_past_u32(wide):
+    """Weighted sorted runs are counted with u32 staged counts first; a key
+    whose merged count passes 2^32 (3e9 + 3e9 here, and a lone 5e9) sends the
+    count back through u64 staging -- exact either way."""
+    rng = np.random.default_rng(5)
+    k = 45 if wide else 31
+    span = 1 << 40
+    runs = _runs(rng, 3, 100_000, span, k)
+    big = np.uint64(3_000_000_000)
+    for i in (0, 1):  # one shared key with a huge count in two runs
+        keys, counts = runs[i]
+        j = len(keys) // 2
+        runs[i] = (keys, counts.copy())
+        runs[i][1][j] = big
+    shared = runs[0][0][len(runs[0][0]) // 2]
+    k1 = runs[1][0]
+    if shared not in set(k1.tolist()):
+        k1 = np.unique(np.append(k1, shared))
+        c1 = np.ones(len(k1), np.uint64)
+        c1[np.searchsorted(k1, shared)] = big
+        runs[1] = (k1, c1)
+    runs[2][1][0] = np.uint64(5_000_000_000)
+    ek, ec = _expected(runs, True)
+    assert int(ec.max()) > (1 << 32)
+    bufs = []
+    with okm.KmerCounter(k, wide=wide) as m:
+        for keys, counts in runs:
+            kk = np.stack([keys, np.zeros_like(keys)], axis=1).reshape(-1) if wide else keys
+            bk, bc = _upload(kk), _upload(counts)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
+        gk, gc = m.result(1)
+    if wide:
+        gk = gk.reshape(-1, 2)[:, 0]
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
