@@ -278,6 +278,76 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 // full mode (fallback): every instance counting-sorted by home
 // ---------------------------------------------------------------------------
 
+// ---------------------------------------------------------------------------
+// direct output (k_count_slow<KT, W, true>): no staging, no compaction
+// ---------------------------------------------------------------------------
+//
+// Items are taken in index (= key) order from a ticket counter, and each one,
+// once it knows its distinct count D, finds its exclusive prefix over the
+// items before it with a decoupled look-back over per-item status words
+// (aggregate D published at once, inclusive prefix once known), then writes
+// its sorted run straight into the caller's table with u64 counts.  A ticket
+// is only taken by a running workgroup, and an item waits only on smaller
+// tickets, so every wait ends.  A look-back that spins past kLookbackSpins
+// (a broken invariant, never expected) flags ctl[0] bit 16 and moves on
+// instead of hanging the device.
+struct Direct {
+    ull *status;               // [nitems], zero before the launch
+    uint64_t *keys, *counts;   // the table (KT keys, u64 counts)
+    const ull *base;           // device-side first entry (pipelined groups) or nullptr
+    uint32_t item;
+    ull *bcast;                // LDS word: the item's first table entry
+};
+constexpr ull kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = kStAgg - 1;
+constexpr uint32_t kLookbackSpins = 1u << 22;
+
+// Block-uniform call (a barrier); returns the item's first table entry.
+__device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull *ctl) {
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {  // wave 0: 64 predecessors' status words per round trip
+        ull *st = dir.status;
+        const uint32_t item = dir.item;
+        if (t == 0)
+            __hip_atomic_store(st + item, (item ? kStAgg : kStPre) | (ull)D, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        ull excl = 0;
+        int64_t hi = (int64_t)item - 1;  // window [hi - 63, hi], lane t reads hi - t
+        uint32_t spins = 0;
+        while (hi >= 0) {
+            const int64_t p = hi - (int64_t)t;
+            const ull v = p >= 0 ? __hip_atomic_load(st + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStPre;
+            const uint64_t pre = __ballot((v >> 62) == 2);
+            const uint64_t wait = __ballot((v >> 62) == 0);
+            const uint64_t upto = ((pre & (~pre + 1)) << 1) - 1;  // lanes up to the nearest prefix (all if none)
+            if (wait & upto) {
+                if (++spins > kLookbackSpins) {
+                    if (t == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 16u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            ull a = ((upto >> t) & 1ull) ? (v & kStVal) : 0ull;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) a += __shfl_xor(a, d, 64);
+            excl += a;
+            if (pre) break;
+            hi -= 64;
+        }
+        if (t == 0) {
+            if (item)
+                __hip_atomic_store(st + item, kStPre | (excl + D), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *dir.bcast = excl + (dir.base ? *dir.base : 0ull);
+        }
+    }
+    lds_sync();
+    const ull o = *dir.bcast;
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Full-mode LDS bytes: keys (+ weights), then the home counters, which the
 // run starts (u16 [kCapI + 1]) reuse once the homes are dead.
 template <bool W, typename KT, int HB>
@@ -292,7 +362,7 @@ template <bool W, typename KT, int HB = kHomeBits>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
                                               const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
                                               uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
-                                              bool nowrite, bool narrow, ull *ctl) {
+                                              bool nowrite, bool narrow, ull *ctl, const Direct *dir = nullptr) {
     constexpr uint32_t kH = 1u << HB;         // homes (key sub-ranges in order)
     constexpr uint32_t kHW = kH / 2 / kCB;    // u16-pair counter words per thread (2 or 4)
     static_assert(kHW >= 1 && kH / 2 == kHW * kCB, "whole counter words per thread");
@@ -414,6 +484,21 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         if (t == 0) first[D] = (uint16_t)ntot;  // ntot <= kCapI fits u16
     }
     lds_sync();
+    if (dir) {  // straight into the table at the item's prefix
+        const uint64_t o0 = lookback(*dir, D, ctl);
+        KT *dk = reinterpret_cast<KT *>(dir->keys) + o0;
+        for (uint32_t p = t; p < D; p += kCB) {
+            const uint32_t b = first[p], e = first[p + 1];
+            dk[p] = sk[b];
+            ull c = 0;
+            if (W)
+                for (uint32_t i = b; i < e; ++i) c += sw[i];
+            else
+                c = e - b;
+            dir->counts[o0 + p] = c;
+        }
+        return __builtin_amdgcn_readfirstlane(D);
+    }
     for (uint32_t p = t; p < (nowrite ? 0u : D); p += kCB) {
         const uint32_t b = first[p], e = first[p + 1];
         okeys[p] = sk[b];
@@ -638,7 +723,8 @@ __device__ __forceinline__ uint32_t tag_item(const DevItem &it, const DevSeg *__
 template <bool W, typename KT>
 __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *__restrict__ segs,
                                                uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
-                                               ull *lds, uint32_t *wsum, bool nowrite, bool narrow, ull *ctl) {
+                                               ull *lds, uint32_t *wsum, bool nowrite, bool narrow, ull *ctl,
+                                               const Direct *dir = nullptr) {
     typedef typename CountType<W>::T CT;
     const uint32_t t = threadIdx.x;
     const uint32_t r = it.rem_bits;
@@ -680,6 +766,19 @@ __device__ __forceinline__ uint32_t dense_item(const DevItem &it, const DevSeg *
     }
     uint32_t D;
     uint64_t o = it.out_off + block_excl_scan32(d, wsum, &D);
+    if (dir) {  // straight into the table at the item's prefix
+        o += lookback(*dir, D, ctl) - it.out_off;
+        KT *dk = reinterpret_cast<KT *>(dir->keys);
+        for (uint32_t q = 0; q < kHomesPer; ++q) {
+            const uint32_t j = t * kHomesPer + q;
+            if (j < nslots && cnt[j] != 0) {
+                dk[o] = slot_key[j];
+                dir->counts[o] = (uint64_t)cnt[j];
+                ++o;
+            }
+        }
+        return __builtin_amdgcn_readfirstlane(D);
+    }
     for (uint32_t q = 0; q < kHomesPer; ++q) {
         const uint32_t j = t * kHomesPer + q;
         if (!nowrite && j < nslots && cnt[j] != 0) {
@@ -749,14 +848,18 @@ void k_count_items(const DevItem *__restrict__ items, uint32_t nitems, const Dev
 // Deferred items (defer != nullptr: the ctl[1] items listed there), or every
 // item (defer == nullptr: wide keys, which have no tag mode — LDS has no
 // 128-bit CAS): dense mode, or full mode (every instance counting-sorted).
-template <typename KT, bool W>
+// DIRECT (defer == nullptr): items by ticket (ctl[1]) in order, each run
+// written straight into the table (fin_*) at its look-back prefix.
+template <typename KT, bool W, bool DIRECT = false>
 __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeof(KT) > 8) ? 1 : 4))) void k_count_slow(const DevItem *__restrict__ items, uint32_t nitems,
                                                     const DevSeg *__restrict__ segs,
                                                     uint64_t *__restrict__ out_keys,
                                                     uint64_t *__restrict__ out_counts, ull *__restrict__ n_out,
                                                     ull *__restrict__ ctl, const uint32_t *__restrict__ defer,
                                                     const ull *__restrict__ guard, const ull *__restrict__ d_nitems,
-                                                    bool nowrite, bool narrow) {
+                                                    bool nowrite, bool narrow, ull *__restrict__ status,
+                                                    uint64_t *__restrict__ fin_keys, uint64_t *__restrict__ fin_counts,
+                                                    const ull *__restrict__ fin_base) {
     if (guard && (guard[0] | guard[1])) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     constexpr int kHB = sizeof(KT) > 8 ? kFullHomeBitsW : kHomeBits;  // full-mode home bits
@@ -774,7 +877,15 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
         DevItem it;
         uint64_t total;
     };
-    for (uint32_t j = blockIdx.x; j < ndefer; j += gridDim.x) {
+    __shared__ uint32_t s_ticket;
+    __shared__ ull s_bcast;
+    auto next_ticket = [&]() -> uint32_t {
+        lds_sync();  // every thread has read the previous ticket
+        if (threadIdx.x == 0) s_ticket = atomicAdd(reinterpret_cast<unsigned int *>(ctl + 1), 1u);
+        lds_sync();
+        return __builtin_amdgcn_readfirstlane(s_ticket);  // (see DESIGN.md on the structuriser)
+    };
+    for (uint32_t j = DIRECT ? next_ticket() : blockIdx.x; j < ndefer; j = DIRECT ? next_ticket() : j + gridDim.x) {
         Next cur;
         cur.item = defer ? defer[j] : j;
         cur.it = items[cur.item];
@@ -786,18 +897,22 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
         const uint32_t item = cur.item;
         const DevItem it = cur.it;
         const uint64_t total = cur.total;
+        const Direct dsc{status, fin_keys, fin_counts, fin_base, item, &s_bcast};
+        const Direct *dir = DIRECT ? &dsc : nullptr;
         uint32_t written = 0;
         if (total == 0) {  // an empty fan-out slot (block-uniform)
             if (threadIdx.x == 0) n_out[item] = 0;
+            if (DIRECT) (void)lookback(dsc, 0, ctl);  // its successors wait for its status
             continue;
         }
         if (it.rem_bits <= (uint32_t)kDenseBits) {
-            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite, narrow, ctl);
+            written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite, narrow, ctl, dir);
         } else if (total <= (uint64_t)kCapI) {
             written = full_item<W, KT, kHB>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
-                                       out_counts, nowrite, narrow, ctl);
-        } else if (threadIdx.x == 0) {
-            atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
+                                       out_counts, nowrite, narrow, ctl, dir);
+        } else {
+            if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
+            if (DIRECT) (void)lookback(dsc, 0, ctl);
         }
         if (threadIdx.x == 0) n_out[item] = written;
         lds_sync();  // LDS reuse by the next item
@@ -819,10 +934,12 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
         const uint32_t grid = nitems < wide_cap ? nitems : wide_cap;  // odd: fan-out slots spread over blocks
         if (weighted)
             hipLaunchKernelGGL((k_count_slow<K128, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite, narrow);
+                               out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite, narrow,
+                               (ull *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr, (const ull *)nullptr);
         else
             hipLaunchKernelGGL((k_count_slow<K128, false>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
-                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite, narrow);
+                               out_keys, out_counts, n_out, ctl, (const uint32_t *)nullptr, guard, d_nitems, nowrite,
+                               narrow, (ull *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr, (const ull *)nullptr);
         return;
     }
     // workgroups of the unweighted tag kernel (odd, so fan-out slots spread
@@ -845,13 +962,38 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
             hipLaunchKernelGGL((k_count_items<true, false, false>), dim3(wgrid), dim3(kCB), 0, s, items, nitems,
                                segs, out_keys, out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, true>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow,
+                           (ull *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr, (const ull *)nullptr);
     } else {
         hipLaunchKernelGGL(k_count_items<false>, dim3(grid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
                            out_counts, n_out, ctl, defer, guard, d_nitems);
         hipLaunchKernelGGL((k_count_slow<ull, false>), dim3(sgrid), dim3(kCB), 0, s, items, nitems, segs, out_keys,
-                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow);
+                           out_counts, n_out, ctl, (const uint32_t *)defer, guard, d_nitems, nowrite, narrow,
+                           (ull *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr, (const ull *)nullptr);
     }
+}
+
+// Wide keys straight into a caller's table (no staging, no compaction):
+// fin_keys / fin_counts are the table at its next entry, or its start when
+// fin_base holds the next entry on the device; status: nitems words, zeroed
+// by the caller (as is ctl[0..1]).
+void launch_count_direct(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
+                         unsigned long long *n_out, unsigned long long *ctl, bool weighted,
+                         const unsigned long long *guard, const unsigned long long *d_nitems,
+                         unsigned long long *status, uint64_t *fin_keys, uint64_t *fin_counts,
+                         const unsigned long long *fin_base) {
+    if (!nitems) return;
+    hipStream_t s = (hipStream_t)stream;
+    // a workgroup takes items until the tickets run out: about the resident count
+    const uint32_t grid = nitems < 2048u ? nitems : 2048u;
+    if (weighted)
+        hipLaunchKernelGGL((k_count_slow<K128, true, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
+                           (uint64_t *)nullptr, (uint64_t *)nullptr, n_out, ctl, (const uint32_t *)nullptr, guard,
+                           d_nitems, false, false, status, fin_keys, fin_counts, fin_base);
+    else
+        hipLaunchKernelGGL((k_count_slow<K128, false, true>), dim3(grid), dim3(kCB), 0, s, items, nitems, segs,
+                           (uint64_t *)nullptr, (uint64_t *)nullptr, n_out, ctl, (const uint32_t *)nullptr, guard,
+                           d_nitems, false, false, status, fin_keys, fin_counts, fin_base);
 }
 
 }  // namespace okm

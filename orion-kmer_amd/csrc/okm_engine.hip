@@ -1360,13 +1360,17 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
                                     unsigned long long *hguard = nullptr, bool *aborted = nullptr,
                                     const unsigned long long *d_nitems = nullptr, const ResDst *dst = nullptr,
                                     bool last_use = false, bool in_place = false) {
-    uint64_t *sk = nullptr, *sc;
+    uint64_t *sk = nullptr, *sc = nullptr;
     unsigned long long *n_out, *dense_off, *scan_tmp;
+    // wide keys into a caller's table: the count kernel writes the table
+    // itself (okm_count.hip launch_count_direct: items in order, each at its
+    // look-back prefix) -- no staged runs, no compaction pass
+    const bool direct = dst && c->wide;
     // staged counts: u32 (okm_count.hip store_count) -- for weighted launches
     // too when their input survives the count (no in-place staging, no
     // caller's table), which is then redone with u64 counts in the rare case
     // that one does not fit (a C3 merge of four folded tables: 17 GB less)
-    bool narrow = !weighted || (!in_place && !dst);
+    bool narrow = !direct && (!weighted || (!in_place && !dst));
     const uint64_t sc_words = narrow ? (std::max<uint64_t>(out_total, 1) + 1) / 2 : std::max<uint64_t>(out_total, 1);
     if (last_use && c->may_take_runs && !dst && !in_place) {
         const size_t need = std::max<uint64_t>(out_total, 1) * 8 * c->kw;
@@ -1385,15 +1389,20 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             if (on) c->input_lost = true;
         }
     } lost{c, false};
-    if (!donated && !in_place) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
-    OKM_TRY(pool_get(c->pool, sc_words, &sc));
+    if (!donated && !in_place && !direct) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
+    if (!direct) OKM_TRY(pool_get(c->pool, sc_words, &sc));
     OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
     OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
     OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
-    uint32_t *defer;
-    OKM_TRY(pool_get(c->pool, nitems, &defer));
+    uint32_t *defer = nullptr;             // deferred items (tag kernel)
+    unsigned long long *status = nullptr;  // per-item look-back words (direct)
+    if (direct)
+        OKM_TRY(pool_get(c->pool, nitems, &status));
+    else
+        OKM_TRY(pool_get(c->pool, nitems, &defer));
     auto release_own = [&]() {
-        for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer})
+        for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer,
+                        (void *)status})
             if (p && !(donated && p == (void *)sk)) c->pool.put(p);
     };
     auto release_level = [&]() {
@@ -1414,16 +1423,22 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     // items past a device-side count (d_nitems) must scan as empty
     HIP_TRY(hipMemsetAsync(d_nitems ? n_out : n_out + nitems, 0,
                            (d_nitems ? nitems + 1 : 1) * sizeof(unsigned long long), c->stream));
+    if (direct) HIP_TRY(hipMemsetAsync(status, 0, (size_t)nitems * sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     c->hprof.mark("items.h2d");
     lost.on = donated;
-    launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
-                       d_nitems, false, narrow);
+    if (direct)
+        launch_count_direct(c->stream, d_items, nitems, d_segs, n_out, c->flag, weighted, guard, d_nitems, status,
+                            dst->d_base ? dst->keys : dst->keys + dst->off * c->kw,
+                            dst->d_base ? dst->counts : dst->counts + dst->off, dst->d_base);
+    else
+        launch_count_items(c->stream, d_items, nitems, d_segs, sk, sc, n_out, c->flag, defer, weighted, c->wide, guard,
+                           d_nitems, false, narrow);
     c->timer.end(c->stream, "count_items", (8.0 * c->kw + (weighted ? 8.0 : 0.0)) * (double)in_total);
     HIP_TRY(hipGetLastError());
     launch_exclusive_scan(c->stream, n_out, dense_off, nitems + 1, scan_tmp);
     HIP_TRY(hipGetLastError());
-    if (dst) {  // a key-range group: straight into the caller's table (sized by the instance bound)
+    if (dst && !direct) {  // a key-range group: straight into the caller's table (sized by the instance bound)
         c->timer.begin(c->stream);
         if (dst->d_base)
             launch_compact_items(c->stream, d_items, nitems, n_out, dense_off, sk, sc, dst->keys, dst->counts, c->wide,
@@ -1501,8 +1516,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     const double staged = 8.0 * c->kw + (narrow ? 4.0 : 8.0);  // per distinct key: staged (key, count)
     const double dense = 8.0 * c->kw + 8.0;                      // ... and its dense result entry
     if (!c->timer.stats.empty()) {
-        c->timer.stats[c->timer.id_of("count_items")].alg_bytes += staged * (double)nd;
-        if (dst) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
+        c->timer.stats[c->timer.id_of("count_items")].alg_bytes += (direct ? dense : staged) * (double)nd;
+        if (dst && !direct) c->timer.add_bytes("compact_items", (staged + dense) * (double)nd);
     }
     // nothing is in flight: the level arrays (and the item flags the kernels
     // read) are dead -- unless they hold the in-place runs the compaction

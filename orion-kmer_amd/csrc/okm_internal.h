@@ -158,7 +158,16 @@ void launch_count_items(void *stream, const DevItem *items, uint32_t nitems, con
                         unsigned long long *ctl, uint32_t *defer, bool weighted, bool wide,
                         const unsigned long long *guard = nullptr, const unsigned long long *d_nitems = nullptr,
                         bool nowrite = false,  // nowrite: n_out only (weighted or wide launches)
-                        bool narrow = false);  // weighted: u32 staged counts (ctl[0] |= 8 when one does not fit)
+                        bool narrow = false);
+// Wide keys straight into a caller's table (okm_count.hip: items by ticket,
+// each run at its look-back prefix; no staging, no compaction).  status:
+// nitems words and ctl[0..1] zeroed by the caller; fin_keys / fin_counts at
+// the table's next entry, or at its start when fin_base (device) holds it.
+void launch_count_direct(void *stream, const DevItem *items, uint32_t nitems, const DevSeg *segs,
+                         unsigned long long *n_out, unsigned long long *ctl, bool weighted,
+                         const unsigned long long *guard, const unsigned long long *d_nitems,
+                         unsigned long long *status, uint64_t *fin_keys, uint64_t *fin_counts,
+                         const unsigned long long *fin_base);  // weighted: u32 staged counts (ctl[0] |= 8 when one does not fit)
 
 // k-way merge of sorted runs (okm_merge.hip): items as built by
 // launch_sorted_items (each segment of an item a sorted unique run of keys),

@@ -615,27 +615,59 @@ def test_grouped_count(k, wide, mode, maxb, monkeypatch):
             assert np.array_equal(fk, xk) and np.array_equal(fc, xc), mc
 
 
+@pytest.mark.parametrize("k", [31, 63])
 @pytest.mark.parametrize("cap", [None, 0.5])
-def test_grouped_count_pipelined_and_redo(cap):
+def test_grouped_count_pipelined_and_redo(cap, k):
     """Key-range groups in one instance-bound table, pipelined: every group's
     kernels queue behind the previous group's with no host sync and the
     table's next entry advances on the device.  Groups of >= 4 Mi keys take
     the sampled partition placement; with part_cap_permille = 500 their
     sampled slots overflow, the speculative counts are abandoned, and every
-    group is counted again one sync at a time.  Exact both ways."""
-    k = 31
+    group is counted again one sync at a time.  Exact both ways.  k = 63:
+    the count kernel writes the table itself (items in order, each at its
+    look-back prefix: okm_count.hip launch_count_direct), no compaction."""
+    from oracle import OracleCounterWide
+    wide = k > 32
     testing.set_knob("group_keys", 5_000_000)
     testing.set_knob("group_exact", 0)
     if cap:
         testing.set_knob("part_cap_permille", round(cap * 1000))
     batch = okm.synth_reads(130_000, 150, genome_len=20_000_000, genome_seed=12, seed=4, sub_rate=0.01)
-    gk, gc, stats, info = _count_device(batch, k)
-    oc = OracleCounter(k)
+    gk, gc, stats, info = _count_device(batch, k, wide=wide)
+    oc = OracleCounterWide(k) if wide else OracleCounter(k)
     oc.add_separated(batch)
     ek, ec = oc.result(1)
-    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    if wide:
+        gk = gk.reshape(-1, 2)
+    assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert info["groups"] >= 3 and info["distinct"] == len(ec), info
     assert "part_sample" in stats, stats.keys()
+    assert ("compact_items" in stats) == (not wide), stats.keys()
+
+
+def test_grouped_count_wide_weighted():
+    """Weighted wide keys in key-range groups (a counted table's pairs beside
+    raw reads): the direct count sums the weights into the table.  Exact."""
+    from oracle import OracleCounterWide
+    k = 63
+    testing.set_knob("group_keys", 1_500_000)
+    testing.set_knob("group_exact", 0)
+    batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=9, seed=6, sub_rate=0.01)
+    recs = [r for r in batch.tobytes().split(b"\n") if r]
+    with okm.KmerCounter(k, wide=True) as c:
+        c.add_records(recs[: len(recs) // 2], normalized=True)
+        tk, tc = c.result(1)
+    with okm.KmerCounter(k, wide=True) as m:
+        m.add_pairs(tk, tc)
+        m.add_records(recs[len(recs) // 2:], normalized=True)
+        mk, mc = m.result(1)
+        info = m.engine_info()
+    oc = OracleCounterWide(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    mk = mk.reshape(-1, 2)
+    assert mk.shape == ek.shape and np.array_equal(mk, ek) and np.array_equal(mc, ec)
+    assert info["groups"] >= 2, info
 
 
 def test_c1_cli_full_size(tmp_path):
