@@ -90,12 +90,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
     return v;
 }
 
-// Block-wide exclusive scan (u32); returns the block total in *total.  Two barriers.
+// Block-wide exclusive scan (u32); returns the block total in *total.  Two
+// barriers (LDS-only ones when LDS_ONLY: see lds_only_sync).
+__device__ __forceinline__ void lds_only_sync();
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum, uint32_t *total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_scan32(v);
     if (lane == 63) wsum[wid] = inc;
-    lds_sync();
+    if (LDS_ONLY) lds_only_sync(); else lds_sync();
     uint32_t wbase = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kCB / 64; ++w) {
@@ -103,7 +106,7 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *wsum
         wbase += w < wid ? s : 0u;
         tot += s;
     }
-    lds_sync();
+    if (LDS_ONLY) lds_only_sync(); else lds_sync();
     *total = tot;
     return wbase + inc - v;
 }
@@ -301,21 +304,44 @@ struct Direct {
 constexpr ull kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = kStAgg - 1;
 constexpr uint32_t kLookbackSpins = 1u << 22;
 
-// Block-uniform call (a barrier); returns the item's first table entry.
-__device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull *ctl) {
-    const uint32_t t = threadIdx.x;
-    if (t < 64) {  // wave 0: 64 predecessors' status words per round trip
-        ull *st = dir.status;
-        const uint32_t item = dir.item;
-        if (t == 0)
-            __hip_atomic_store(st + item, (item ? kStAgg : kStPre) | (ull)D, __ATOMIC_RELAXED,
+// A barrier that orders LDS only (a workgroup fence on the local address
+// space): a look-back load issued before it stays in flight across it.
+__device__ __forceinline__ void lds_only_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ ull status_window(const Direct &dir, int64_t hi) {
+    const int64_t p = hi - (int64_t)(threadIdx.x & 63u);  // lane t reads hi - t
+    return p >= 0 ? __hip_atomic_load(dir.status + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStPre;
+}
+
+// Look-back, first half (wave 0): publish the item's aggregate D and put the
+// nearest 64 predecessors' status words in flight.  Other waves get 0.
+__device__ __forceinline__ ull lookback_begin(const Direct &dir, uint32_t D) {
+    ull v = 0;
+    if (threadIdx.x < 64) {
+        if (threadIdx.x == 0)
+            __hip_atomic_store(dir.status + dir.item, (dir.item ? kStAgg : kStPre) | (ull)D, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        v = status_window(dir, (int64_t)dir.item - 1);
+    }
+    return v;
+}
+
+// Second half: sum the window's aggregates back to the nearest inclusive
+// prefix (64 predecessors per round trip, waiting on any not yet published),
+// publish this item's prefix.  Block-uniform call (a barrier); returns the
+// item's first table entry.
+__device__ __forceinline__ uint64_t lookback_end(const Direct &dir, uint32_t D, ull v, ull *ctl) {
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {
+        const uint32_t item = dir.item;
         ull excl = 0;
-        int64_t hi = (int64_t)item - 1;  // window [hi - 63, hi], lane t reads hi - t
+        int64_t hi = (int64_t)item - 1;
         uint32_t spins = 0;
         while (hi >= 0) {
-            const int64_t p = hi - (int64_t)t;
-            const ull v = p >= 0 ? __hip_atomic_load(st + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStPre;
             const uint64_t pre = __ballot((v >> 62) == 2);
             const uint64_t wait = __ballot((v >> 62) == 0);
             const uint64_t upto = ((pre & (~pre + 1)) << 1) - 1;  // lanes up to the nearest prefix (all if none)
@@ -325,6 +351,7 @@ __device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull 
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
+                v = status_window(dir, hi);
                 continue;
             }
             ull a = ((upto >> t) & 1ull) ? (v & kStVal) : 0ull;
@@ -333,10 +360,12 @@ __device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull 
             excl += a;
             if (pre) break;
             hi -= 64;
+            v = status_window(dir, hi);
         }
         if (t == 0) {
             if (item)
-                __hip_atomic_store(st + item, kStPre | (excl + D), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(dir.status + item, kStPre | (excl + D), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             *dir.bcast = excl + (dir.base ? *dir.base : 0ull);
         }
     }
@@ -346,6 +375,10 @@ __device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull 
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32));
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o);
     return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull *ctl) {
+    return lookback_end(dir, D, lookback_begin(dir, D), ctl);
 }
 
 // Full-mode LDS bytes: keys (+ weights), then the home counters, which the
@@ -358,7 +391,10 @@ constexpr int full_lds_bytes() {
 // HB: home bits.  K128 items (k > 32, ~all keys distinct) take 4096 homes, so
 // a home holds ~1 key and each instance's rank scan reads ~1 key (random
 // 16-B LDS reads are the kernel's most bank-conflicted accesses).
-template <bool W, typename KT, int HB = kHomeBits>
+// DIRECT (dir): the item's distinct count is taken from the rank pass, so its
+// aggregate is published and the look-back's first loads fly while the
+// sorted run is built (LDS-only barriers until the run is written).
+template <bool W, typename KT, int HB = kHomeBits, bool DIRECT = false>
 __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows, const KT (&kk)[kPer],
                                               const ull (&ww)[kPer], ull *lds, uint32_t *wsum,
                                               uint64_t *__restrict__ out_keys_raw, uint64_t *__restrict__ out_counts,
@@ -377,6 +413,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     lds_sync();  // the previous item's LDS state is dead
 #pragma unroll
     for (uint32_t q = 0; q < kHW; ++q) hc[kHW * t + q] = 0;
+    if (DIRECT && t == 0) wsum[kCB / 64] = 0;  // first occurrences (the rank pass)
     lds_sync();
     uint32_t hp[kPer];  // home << 16 | pos
 #pragma unroll
@@ -430,6 +467,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
     // order, so this sorts the item; loops run over one home's keys (~2 at
     // k=63, whose keys are ~98 % distinct) instead of a thread's whole slice
     uint32_t dst[kPer];
+    uint32_t nfirst = 0;  // DIRECT: instances with no equal key before them (= distinct keys)
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         dst[u] = ~0u;
@@ -440,14 +478,29 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             const uint32_t he = h + 1 < kH ? half_of(hc[(h + 1) >> 1], h + 1) : ntot;
             const uint32_t me = hs + (hp[u] & 0xFFFFu);
             uint32_t rank = hs;
+            bool dup = false;
             for (uint32_t q = hs; q < he; ++q) {
                 const KT y = sk[q];
-                rank += (KeyOps<KT>::lt(y, kk[u]) || (q < me && KeyOps<KT>::eq(y, kk[u]))) ? 1u : 0u;
+                const bool before = q < me && KeyOps<KT>::eq(y, kk[u]);
+                rank += (KeyOps<KT>::lt(y, kk[u]) || before) ? 1u : 0u;
+                dup = dup || before;
             }
             dst[u] = rank;
+            nfirst += dup ? 0u : 1u;
         }
     }
+    if (DIRECT) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) nfirst += __shfl_xor(nfirst, d, 64);
+        if ((t & 63u) == 0) atomicAdd(&wsum[kCB / 64], nfirst);
+    }
     lds_sync();  // every read of the home-ordered keys is done
+    uint32_t De = 0;
+    ull lbv = 0;
+    if (DIRECT) {
+        De = __builtin_amdgcn_readfirstlane(wsum[kCB / 64]);
+        lbv = lookback_begin(*dir, De);
+    }
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         if ((uint32_t)u >= nrows) break;
@@ -456,7 +509,7 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
             if (W) sw[dst[u]] = ww[u];
         }
     }
-    lds_sync();
+    if (DIRECT) lds_only_sync(); else lds_sync();
     // count.rs:33: a key's count = its run's length (weight); flag run starts.
     // The flags are taken in rows of lane-contiguous positions (conflict-free
     // LDS reads; a thread's own 8 consecutive keys sit 128 B apart from its
@@ -472,20 +525,21 @@ __device__ __forceinline__ uint32_t full_item(const DevItem &it, uint32_t nrows,
         const uint64_t b = __ballot(f);
         if ((t & 63u) == 0) fm[(uint32_t)i * (kCB / 64) + (t >> 6)] = b;
     }
-    lds_sync();
+    if (DIRECT) lds_only_sync(); else lds_sync();
     const uint32_t rp = p0 % kCB;
     m = (uint32_t)(fm[(p0 / kCB) * (kCB / 64) + rp / 64] >> (rp % 64)) & 0xFFu;
     uint32_t D;
     {
-        uint32_t q = block_excl_scan32((uint32_t)__builtin_popcount(m), wsum, &D);
+        uint32_t q = block_excl_scan32<DIRECT>((uint32_t)__builtin_popcount(m), wsum, &D);
 #pragma unroll
         for (int j = 0; j < kPerT; ++j)
             if (m & (1u << j)) first[q++] = (uint16_t)(p0 + j);
         if (t == 0) first[D] = (uint16_t)ntot;  // ntot <= kCapI fits u16
     }
-    lds_sync();
-    if (dir) {  // straight into the table at the item's prefix
-        const uint64_t o0 = lookback(*dir, D, ctl);
+    if (DIRECT) lds_only_sync(); else lds_sync();
+    if (DIRECT) {  // straight into the table at the item's prefix
+        if (De != D && t == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 32u);  // never: both count runs
+        const uint64_t o0 = lookback_end(*dir, De, lbv, ctl);
         KT *dk = reinterpret_cast<KT *>(dir->keys) + o0;
         for (uint32_t p = t; p < D; p += kCB) {
             const uint32_t b = first[p], e = first[p + 1];
@@ -908,8 +962,8 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
         if (it.rem_bits <= (uint32_t)kDenseBits) {
             written = dense_item<W, KT>(it, segs, out_keys, out_counts, lds, wsum, nowrite, narrow, ctl, dir);
         } else if (total <= (uint64_t)kCapI) {
-            written = full_item<W, KT, kHB>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum, out_keys,
-                                       out_counts, nowrite, narrow, ctl, dir);
+            written = full_item<W, KT, kHB, DIRECT>(it, (uint32_t)((total + kCB - 1) / kCB), kk, ww, lds, wsum,
+                                                    out_keys, out_counts, nowrite, narrow, ctl, dir);
         } else {
             if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 2u);  // planner invariant broken
             if (DIRECT) (void)lookback(dsc, 0, ctl);
