@@ -1475,8 +1475,13 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     if (guard)
         HIP_TRY(hipMemcpyAsync(&hv[2], guard, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     if (d_nitems) HIP_TRY(hipMemcpyAsync(&hv[5], d_nitems, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    if (c->hprof.on)  // deferred items (tag kernel) / tickets taken (direct)
+        HIP_TRY(hipMemcpyAsync(&hv[6], c->flag + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     c->hprof.mark("count+scan+sync");
+    if (c->hprof.on && !c->wide)
+        fprintf(stderr, "[okm count] %u items, %llu deferred to the slow kernel\n", nitems,
+                (unsigned long long)(hv[6] & 0xFFFFFFFFull));
     if (guard) {
         for (int i = 0; i < 3; ++i) hguard[i] = hv[2 + i];
         *aborted = (hv[2] | hv[3]) != 0;
