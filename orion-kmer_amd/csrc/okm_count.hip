@@ -278,10 +278,6 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 }
 
 // ---------------------------------------------------------------------------
-// full mode (fallback): every instance counting-sorted by home
-// ---------------------------------------------------------------------------
-
-// ---------------------------------------------------------------------------
 // direct output (k_count_slow<KT, W, true>): no staging, no compaction
 // ---------------------------------------------------------------------------
 //
@@ -380,6 +376,10 @@ __device__ __forceinline__ uint64_t lookback_end(const Direct &dir, uint32_t D, 
 __device__ __forceinline__ uint64_t lookback(const Direct &dir, uint32_t D, ull *ctl) {
     return lookback_end(dir, D, lookback_begin(dir, D), ctl);
 }
+
+// ---------------------------------------------------------------------------
+// full mode (fallback): every instance counting-sorted by home
+// ---------------------------------------------------------------------------
 
 // Full-mode LDS bytes: keys (+ weights), then the home counters, which the
 // run starts (u16 [kCapI + 1]) reuse once the homes are dead.
