@@ -645,6 +645,27 @@ def test_grouped_count_pipelined_and_redo(cap, k):
     assert ("compact_items" in stats) == (not wide), stats.keys()
 
 
+@pytest.mark.parametrize("k", [33, 63])
+def test_grouped_count_wide_hot_keys(k):
+    """Wide keys in key-range groups with hot keys (poly-A reads and a
+    period-4 record): their parts split down to direct-address (dense) items,
+    which the direct count writes at their look-back prefix too.  Exact."""
+    testing.set_knob("group_keys", 300_000)
+    testing.set_knob("group_exact", 0)
+    g = okm.synth_reads(4_000, 150, genome_len=400_000, genome_seed=3, seed=k, sub_rate=0.01)
+    recs = [r for r in g.tobytes().split(b"\n") if r] + [b"A" * 150] * 3_000 + [b"ACGT" * 40_000]
+    oc = OracleCounterWide(k)
+    oc.add_records(recs)
+    ek, ec = oc.result(1)
+    with okm.KmerCounter(k, wide=True) as ctr:
+        ctr.add_records(recs)
+        gk, gc = ctr.result(1)
+        info = ctr.engine_info()
+    gk = gk.reshape(-1, 2)
+    assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert info["groups"] >= 2 and info["levels"] >= 2, info  # (the hot parts split further)
+
+
 def test_grouped_count_wide_weighted():
     """Weighted wide keys in key-range groups (a counted table's pairs beside
     raw reads): the direct count sums the weights into the table.  Exact."""
