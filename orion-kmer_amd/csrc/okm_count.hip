@@ -178,7 +178,7 @@ __device__ __forceinline__ void load_item(const DevItem &it, const DevSeg *__res
         }
         return;
     }
-    if (it.seg_count <= 4) {  // merged sibling children (k_make_items): the <= 4 descriptors load together
+    if (it.seg_count <= 4) {  // a key range of <= 4 sorted runs (k_sorted_items): the descriptors load together
         const uint32_t R = it.seg_count;
         const KT *kb[4];
         const uint64_t *cb[4];

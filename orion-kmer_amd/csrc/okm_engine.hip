@@ -1872,7 +1872,7 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     // 27.0 vs 53.4 ms), but it needs instance-bound slots and result (~2 x 16 B
     // per pair) where the merge kernel writes the table once at its exact size:
     // the merge kernel when that does not fit (the last folds of C3 on one GPU),
-    // or on request (OKM_MERGE_KERNEL=1)
+    // or on request (test hook OKM_TEST_SORTED_PATH = 1)
     // The staged path holds 16 B of staged pairs per instance and then the
     // exact table beside them; a context's own folded tables take it too when
     // that fits (C3 on one GPU, two merges of ~5 G pairs: 497 vs 559 ms per
