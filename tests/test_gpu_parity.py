@@ -674,17 +674,20 @@ def test_grouped_count_wide_weighted():
     testing.set_knob("group_keys", 1_500_000)
     testing.set_knob("group_exact", 0)
     batch = okm.synth_reads(60_000, 150, genome_len=3_000_000, genome_seed=9, seed=6, sub_rate=0.01)
-    recs = [r for r in batch.tobytes().split(b"\n") if r]
+    # + poly-A reads on both sides: a hot key whose weighted part splits down
+    # to a direct-address item
+    recs = [b"A" * 150] * 1_000 + [r for r in batch.tobytes().split(b"\n") if r] + [b"A" * 150] * 1_000
+    half = len(recs) // 2
     with okm.KmerCounter(k, wide=True) as c:
-        c.add_records(recs[: len(recs) // 2], normalized=True)
+        c.add_records(recs[:half], normalized=True)
         tk, tc = c.result(1)
     with okm.KmerCounter(k, wide=True) as m:
         m.add_pairs(tk, tc)
-        m.add_records(recs[len(recs) // 2:], normalized=True)
+        m.add_records(recs[half:], normalized=True)
         mk, mc = m.result(1)
         info = m.engine_info()
     oc = OracleCounterWide(k)
-    oc.add_separated(batch)
+    oc.add_records(recs, normalized=True)
     ek, ec = oc.result(1)
     mk = mk.reshape(-1, 2)
     assert mk.shape == ek.shape and np.array_equal(mk, ek) and np.array_equal(mc, ec)
