@@ -2470,7 +2470,12 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         }
         group_keys = std::max<uint64_t>(group_keys, 1);
     }
-    if (mode == 0 || group_keys >= total) return count_parts(c, segtab, parts, weighted, cp, nullptr);
+    // wide keys that fit beside an instance-bound table count straight into
+    // it as one group (the direct count: no staged runs, no compaction pass),
+    // and the table then gives its tail back
+    const bool direct_one = c->wide && mode == 0 && (double)total * (ws_key + res_key) <= avail;
+    if (direct_one) mode = 1;
+    if (mode == 0 || (group_keys >= total && !direct_one)) return count_parts(c, segtab, parts, weighted, cp, nullptr);
     // every group reads the runs: none may hold a group's staged keys
     struct Keep {
         okm_ctx *c;
@@ -2595,6 +2600,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         guard.armed = false;
         c->res_keys = d.keys;
         c->res_counts = d.counts;
+        if (direct_one) {
+            OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, nd, 1.0));
+            ngroups = 0;  // (one pass: no grouping)
+        }
     } else {
         nd = 0;
         for (auto &t : tabs) nd += t.n;
