@@ -564,6 +564,24 @@ def test_fan_out_split(k, wide, monkeypatch):
     assert "fan_split" in mstats
 
 
+@pytest.mark.parametrize("k", [45, 63])
+def test_fan_out_large_jobs_direct(k):
+    """Wide keys with 1-bit partition passes: children of ~17-40 Ki keys go
+    through the fan-out's large-job variant (1024 threads, ranks in LDS) and
+    the direct count (one group beside an instance-bound table).  Exact
+    against the oracle."""
+    from oracle import OracleCounterWide
+    testing.set_knob("part_max_bits", 1)
+    batch = okm.synth_reads(200_000, 150, genome_len=20_000_000, genome_seed=11, seed=k, sub_rate=0.01)
+    gk, gc, stats, info = _count_device(batch, k, wide=True)
+    oc = OracleCounterWide(k)
+    oc.add_separated(batch)
+    ek, ec = oc.result(1)
+    gk = gk.reshape(-1, 2)
+    assert gk.shape == ek.shape and np.array_equal(gk, ek) and np.array_equal(gc, ec)
+    assert "fan_split" in stats and "compact_items" not in stats and info["levels"] == 1, (stats.keys(), info)
+
+
 def test_fan_out_overflow_falls_back_to_host_rounds(monkeypatch):
     # a 1-bit pass cap leaves children (~70 Ki keys) too big for one fan-out
     # job (<= 64 Ki): the speculative count is abandoned and the host plans
