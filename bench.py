@@ -71,7 +71,7 @@ import numpy as np  # noqa: E402
 
 import okm  # noqa: E402
 from okm import _lib  # noqa: E402
-from okm.pipeline import OwnedCountPipeline, agree_or_raise  # noqa: E402
+from okm.pipeline import OwnedCountPipeline, agree_or_raise, comm_audit  # noqa: E402
 
 # Load the engine (and the HIP runtime it links) before torch, so the process
 # has exactly one HIP runtime.
@@ -369,6 +369,14 @@ def main():
             log(f"[rank {rank}] C3 measurement failed: {e!r}")
             c3 = {"error": repr(e)}
 
+    # what ran at N>1: every rank's communicator (size, RCCL's own rank count,
+    # device PCI bus id), gathered over gloo; collective, so before the rank split
+    audit = None
+    if dist_on:
+        infos = [None] * world
+        dist.all_gather_object(infos, comm.info())
+        audit = comm_audit(infos, world)
+
     if rank != 0:
         if comm is not None:
             comm.close()
@@ -415,6 +423,7 @@ def main():
         "engine": info,
     }
     if dist_on:
+        out["comm"] = audit
         out["config"]["owned_distinct_rank0"] = int(n_owned)
         out["exchange_ms_per_step_rank0"] = {"exchange": round(pipe.phase_ms["exchange"] / args.steps, 3),
                                              "merge": round(pipe.phase_ms["merge"] / args.steps, 3)}
@@ -566,6 +575,11 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
         dbuf.download(host)
         cpu, cpu_mt = cpu_baselines(host, m, min(args.cpu_mt_reads, nreads), device, "the C3 shard")
 
+    audit = None
+    if comm is not None:  # collective: every rank's communicator, gathered over gloo
+        infos = [None] * world
+        dist.all_gather_object(infos, comm.info())
+        audit = comm_audit(infos, world)
     ctr.close()
     dbuf.free()
     if rank != 0:
@@ -612,6 +626,7 @@ def c3_run(args, world, rank, device, comm, dist_on, steps, warmup, baselines):
                                     "merge": round(xt[2] / steps * 1e3, 2)},
         "kernels": kernels,
         "engine": info,
+        "comm": audit,
         # rank 0's device memory: what its arena mapped at the end of the timed
         # jobs (device_bytes, idle cached chunks included) and the most it held
         # in use at once (device_peak_bytes); the result itself is 16 B / key

@@ -272,6 +272,18 @@ okm_status okm_comm_init_loopback(okm_comm **out, int n, int device);
 void okm_comm_destroy(okm_comm *comm);
 int okm_comm_rank(const okm_comm *comm);
 int okm_comm_size(const okm_comm *comm);
+/* What a communicator is, for audit lines (bench.py's N>1 `comm` object): the
+ * ranks / rank / device it was created with, what the transport itself
+ * reports (RCCL: ncclCommCount, ncclCommUserRank, ncclCommCuDevice; the
+ * loopback transport: its virtual ranks, device -1), and the PCI bus id of
+ * the device (hipDeviceGetPCIBusId), so N ranks can be shown to be N GPUs. */
+typedef struct okm_comm_info {
+    int size, rank, device;
+    int transport_ranks, transport_rank, transport_device;  /* -1: not reported */
+    char transport[16];                                     /* "rccl" | "loopback" */
+    char pci_bus_id[32];                                    /* "0000:05:00.0"; empty when unknown */
+} okm_comm_info;
+okm_status okm_comm_get_info(const okm_comm *comm, okm_comm_info *info);
 /* Collective over every rank of `comm`: `local` (counted or not) holds this
  * rank's shard; afterwards `owner` (reset first) holds this rank's key range
  * of the union of all ranks' tables, counted and sorted, and *n_owned its

@@ -287,9 +287,10 @@ __device__ __forceinline__ void tag_reset(ull *lds) {
 // (aggregate D published at once, inclusive prefix once known), then writes
 // its sorted run straight into the caller's table with u64 counts.  A ticket
 // is only taken by a running workgroup, and an item waits only on smaller
-// tickets, so every wait ends.  A look-back that spins past kLookbackSpins
-// (a broken invariant, never expected) flags ctl[0] bit 16 and moves on
-// instead of hanging the device.
+// tickets, so every wait ends.  A look-back that has waited on one
+// predecessor for kLookbackTicks of the device's constant-rate wall clock
+// (~15 s at its 100 MHz: a broken invariant, never a slow predecessor) flags
+// ctl[0] bit 16 and moves on instead of hanging the device.
 struct Direct {
     ull *status;               // [nitems], zero before the launch
     uint64_t *keys, *counts;   // the table (KT keys, u64 counts)
@@ -298,7 +299,7 @@ struct Direct {
     ull *bcast;                // LDS word: the item's first table entry
 };
 constexpr ull kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = kStAgg - 1;
-constexpr uint32_t kLookbackSpins = 1u << 22;
+constexpr uint64_t kLookbackTicks = 1500000000ull;
 
 // A barrier that orders LDS only (a workgroup fence on the local address
 // space): a look-back load issued before it stays in flight across it.
@@ -336,13 +337,18 @@ __device__ __forceinline__ uint64_t lookback_end(const Direct &dir, uint32_t D, 
         const uint32_t item = dir.item;
         ull excl = 0;
         int64_t hi = (int64_t)item - 1;
-        uint32_t spins = 0;
+        uint64_t wait_from = 0;  // wall clock at the first wait on the current window
+        bool waiting = false;
         while (hi >= 0) {
             const uint64_t pre = __ballot((v >> 62) == 2);
             const uint64_t wait = __ballot((v >> 62) == 0);
             const uint64_t upto = ((pre & (~pre + 1)) << 1) - 1;  // lanes up to the nearest prefix (all if none)
             if (wait & upto) {
-                if (++spins > kLookbackSpins) {
+                const uint64_t now = wall_clock64();
+                if (!waiting) {
+                    waiting = true;
+                    wait_from = now;
+                } else if (now - wait_from > kLookbackTicks) {
                     if (t == 0) atomicOr(reinterpret_cast<unsigned int *>(ctl), 16u);
                     break;
                 }
@@ -350,6 +356,7 @@ __device__ __forceinline__ uint64_t lookback_end(const Direct &dir, uint32_t D, 
                 v = status_window(dir, hi);
                 continue;
             }
+            waiting = false;
             ull a = ((upto >> t) & 1ull) ? (v & kStVal) : 0ull;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) a += __shfl_xor(a, d, 64);

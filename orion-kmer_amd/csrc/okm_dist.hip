@@ -77,6 +77,10 @@ struct Rccl {
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
+    // what a communicator reports about itself (okm_comm_get_info; optional)
+    ncclResult_t (*CommCount)(const ncclComm_t, int *) = nullptr;
+    ncclResult_t (*CommUserRank)(const ncclComm_t, int *) = nullptr;
+    ncclResult_t (*CommCuDevice)(const ncclComm_t, int *) = nullptr;
     bool ok = false;
     std::string why;
 };
@@ -116,6 +120,9 @@ static Rccl load_rccl() {
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.GetErrorString, "ncclGetErrorString");
     r.ok = all;
+    r.CommCount = reinterpret_cast<decltype(r.CommCount)>(dlsym(h, "ncclCommCount"));
+    r.CommUserRank = reinterpret_cast<decltype(r.CommUserRank)>(dlsym(h, "ncclCommUserRank"));
+    r.CommCuDevice = reinterpret_cast<decltype(r.CommCuDevice)>(dlsym(h, "ncclCommCuDevice"));
     return r;
 }
 
@@ -370,6 +377,9 @@ class Transport {
     // after a failure inside a collective: peers blocked in one return an error
     virtual void abort() = 0;
     virtual const char *name() const = 0;
+    // ranks, this rank and its device as the transport itself reports them
+    // (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice); -1 unknown
+    virtual void self_report(int *count, int *rank, int *device) const = 0;
     // true: send buffers must be plain hipMalloc memory of the communicator
     // (the counting contexts' tables live in a virtual-memory arena, which
     // RCCL's peer-to-peer paths are not given to register or map)
@@ -409,6 +419,13 @@ class RcclTransport final : public Transport {
         nc_ = nullptr;
     }
     const char *name() const override { return "rccl"; }
+    void self_report(int *count, int *rank, int *device) const override {
+        *count = *rank = *device = -1;
+        if (!nc_) return;
+        if (rccl().CommCount && rccl().CommCount(nc_, count) != ncclSuccess) *count = -1;
+        if (rccl().CommUserRank && rccl().CommUserRank(nc_, rank) != ncclSuccess) *rank = -1;
+        if (rccl().CommCuDevice && rccl().CommCuDevice(nc_, device) != ncclSuccess) *device = -1;
+    }
 
   private:
     ncclComm_t nc_;
@@ -533,6 +550,11 @@ class LoopTransport final : public Transport {
     }
     void abort() override { hub_->abort(); }
     const char *name() const override { return "loopback"; }
+    void self_report(int *count, int *rank, int *device) const override {
+        *count = hub_->P;
+        *rank = me_;
+        *device = -1;  // every virtual rank shares the caller's device (okm_comm_get_info: device)
+    }
 
   private:
     okm_status lost() { return fail(OKM_E_COMM, "loopback communicator aborted (a peer rank failed or timed out)"); }
@@ -567,30 +589,37 @@ using namespace okm;
 // Communicator
 // ---------------------------------------------------------------------------
 namespace {
+// A communicator's device buffer (plain hipMalloc, outside the contexts'
+// arenas): its bytes count against the per-device budget (OKM_HBM_CAP), so
+// the contexts on the device see that much less room.  Past the budget the
+// contexts' idle arena chunks are unmapped first.
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    int dev = 0;
     okm_status ensure(size_t bytes) {
         if (bytes <= cap) return OKM_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         const size_t want = std::max<size_t>(bytes + bytes / 8, 4096);
+        (void)hipGetDevice(&dev);
+        if (device_over_budget(dev, want)) trim_device_pools(dev);
         if (hipMalloc(&p, want) != hipSuccess) {
             // HBM held by the contexts' cached (idle) arena chunks: give it back, once
             (void)hipGetLastError();
-            int dev = 0;
-            (void)hipGetDevice(&dev);
             trim_device_pools(dev);
             p = nullptr;
             HIP_TRY(hipMalloc(&p, want));
         }
         cap = want;
+        device_bytes_add(dev, (int64_t)cap);
         return OKM_OK;
     }
     template <typename T> T *as() const { return static_cast<T *>(p); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            device_bytes_add(dev, -(int64_t)cap);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -1159,6 +1188,21 @@ void okm_comm_destroy(okm_comm *m) {
 }
 
 int okm_comm_rank(const okm_comm *m) { return m ? m->rank : -1; }
+
+okm_status okm_comm_get_info(const okm_comm *m, okm_comm_info *info) {
+    if (!m || !info) return fail(OKM_E_ARG, "null argument");
+    *info = okm_comm_info{};
+    info->size = m->size;
+    info->rank = m->rank;
+    info->device = m->device;
+    m->tp->self_report(&info->transport_ranks, &info->transport_rank, &info->transport_device);
+    snprintf(info->transport, sizeof(info->transport), "%s", m->tp->name());
+    if (hipDeviceGetPCIBusId(info->pci_bus_id, (int)sizeof(info->pci_bus_id), m->device) != hipSuccess) {
+        (void)hipGetLastError();
+        info->pci_bus_id[0] = 0;
+    }
+    return OKM_OK;
+}
 int okm_comm_size(const okm_comm *m) { return m ? m->size : 0; }
 
 okm_status okm_comm_last_times(const okm_comm *m, double *ms4) {

@@ -53,6 +53,12 @@ struct DevPool;
 static std::mutex g_pools_mu;
 static std::vector<DevPool *> g_pools;  // every live context's pool (cross-pool trim, the budget)
 static constexpr size_t kArenaChunk = size_t(1) << 30;  // 1 GiB: 64 MiB chunks cost the streaming kernels TLB reach
+// Per device: the bytes every pool has mapped plus the communicators' device
+// buffers (okm_dist.hip DevBuf) -- what the budget compares against.  An
+// atomic, so that a pool holding its own lock never takes g_pools_mu (the
+// lock order is g_pools_mu, then a pool's mu: trim_others / trim_device_pools).
+static std::atomic<int64_t> g_dev_bytes[64];
+void device_bytes_add(int device, int64_t delta) { g_dev_bytes[device & 63].fetch_add(delta, std::memory_order_relaxed); }
 
 // The device memory the process's contexts may map together: OKM_HBM_CAP, a
 // fraction of HBM (<= 1, default 0.9) or a byte count (> 1; "16e9" or with a
@@ -124,13 +130,14 @@ struct DevPool {
         const char *q = static_cast<const char *>(p);
         return arena.base && q >= arena.base && q < arena.base + arena.reserved;
     }
-    // Bytes every pool on this device has mapped.
+    // Bytes every pool on this device has mapped (+ communicator buffers); lock-free.
     static size_t device_mapped(int device) {
-        std::lock_guard<std::mutex> g(g_pools_mu);
-        size_t b = 0;
-        for (DevPool *o : g_pools)
-            if (o->device == device) b += o->mapped_bytes.load(std::memory_order_relaxed);
-        return b;
+        const int64_t b = g_dev_bytes[device & 63].load(std::memory_order_relaxed);
+        return b > 0 ? (size_t)b : 0;
+    }
+    void set_mapped(size_t m) {
+        const size_t old = mapped_bytes.exchange(m, std::memory_order_relaxed);
+        device_bytes_add(device, (int64_t)m - (int64_t)old);
     }
     // Would `bytes` more mapped memory take the device's pools past the budget?
     bool over_budget(size_t bytes) const { return (double)device_mapped(device) + (double)bytes > hbm_budget(device); }
@@ -161,7 +168,7 @@ struct DevPool {
             if (over_budget(need) && arena.idle()) {
                 (void)hipDeviceSynchronize();
                 arena.unmap_idle(need);
-                mapped_bytes = arena.mapped;
+                set_mapped(arena.mapped);
             }
             if (over_budget(need)) {  // other contexts' idle chunks (their locks, not ours)
                 mu.unlock();
@@ -175,7 +182,7 @@ struct DevPool {
                 (void)hipGetLastError();
                 (void)hipDeviceSynchronize();
                 arena.unmap_idle(~size_t(0));
-                mapped_bytes = arena.mapped;
+                set_mapped(arena.mapped);
                 mu.unlock();
                 trim_others();
                 mu.lock();
@@ -183,7 +190,7 @@ struct DevPool {
                 for (size_t i = c0; i <= c1 && e == hipSuccess; ++i)
                     if (!arena.chunks[i].mapped) e = arena.map_chunk(i);
             }
-            mapped_bytes = arena.mapped;
+            set_mapped(arena.mapped);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 undo();
@@ -255,7 +262,7 @@ struct DevPool {
         if (arena.idle()) {
             (void)hipDeviceSynchronize();
             arena.unmap_idle(~size_t(0));
-            mapped_bytes = arena.mapped;
+            set_mapped(arena.mapped);
         }
     }
     void trim_others() {
@@ -266,10 +273,14 @@ struct DevPool {
     void release_all() {
         std::lock_guard<std::mutex> g(mu);
         arena.release();
-        mapped_bytes = 0;
+        set_mapped(0);
         ready = false;
     }
 };
+
+bool device_over_budget(int device, size_t bytes) {
+    return (double)DevPool::device_mapped(device) + (double)bytes > hbm_budget(device);
+}
 
 void trim_device_pools(int device) {
     std::lock_guard<std::mutex> g(g_pools_mu);
@@ -479,6 +490,23 @@ struct okm_ctx {
     // of its own (C2: 1.8 GB fewer held; a table kept later is moved by
     // result_to_folded_run's shrink)
     bool share_result = false;
+    // A count whose items were counted in place (count_parts, one child per
+    // item) leaves its table as the items' sorted runs: keys over the items'
+    // own keys in the level array, u32 / u64 counts at each item's out_off,
+    // n_out[i] entries per item, items in key order (count.rs:106-119's
+    // sorted drain, segment by segment).  The dense (keys, counts) copy is
+    // made by the first reader that needs one (ensure_dense: okm_result_device,
+    // the fetch / drain, folding, the multi-GPU merge), so a count whose table
+    // is only drained pays one gather, not two.
+    struct Pending {
+        bool on = false;
+        DevItem *items = nullptr;
+        uint32_t nitems = 0;
+        unsigned long long *n_out = nullptr, *dense_off = nullptr;
+        uint64_t *sc = nullptr;
+        bool narrow = false;
+        std::vector<void *> hold;  // freed with it: level arrays, segments, items, n_out, offsets, counts
+    } pend;
     uint64_t *res_keys = nullptr, *res_counts = nullptr;
     uint64_t n_res = 0;
     bool res_host = false;     // the result lies in page-locked HOST memory (too big to stay beside its inputs)
@@ -562,7 +590,13 @@ static void host_table_free(okm_ctx *c, uint64_t *keys, uint64_t *counts, uint64
     c->host_bytes -= std::min(c->host_bytes, b);
 }
 
+static void drop_pending(okm_ctx *c) {
+    for (void *p : c->pend.hold) c->pool.put(p);
+    c->pend = okm_ctx::Pending{};
+}
+
 static void invalidate_result(okm_ctx *c) {
+    drop_pending(c);
     if (c->res_host) {
         host_table_free(c, c->res_keys, c->res_counts, c->n_res);
     } else {
@@ -596,6 +630,37 @@ static okm_status sync(okm_ctx *c) {
     HIP_TRY(hipGetLastError());
     c->timer.flush();
     c->hpin_used = 0;  // every copy out of the pinned staging has completed
+    return OKM_OK;
+}
+
+// The dense (keys, counts) copy of a table left as the items' sorted runs
+// (okm_ctx::Pending): one gather in key order (k_compact_items), then the
+// runs' memory goes back to the pool.  A no-op for a dense result.
+static okm_status ensure_dense(okm_ctx *c) {
+    if (!c->pend.on) return OKM_OK;
+    const uint64_t nd = c->n_res;
+    uint64_t *dk = nullptr, *dc = nullptr;
+    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &dk));
+    okm_status st = pool_get(c->pool, std::max<uint64_t>(nd, 1), &dc);
+    if (st != OKM_OK) {
+        c->pool.put(dk);
+        return st;
+    }
+    c->timer.begin(c->stream);
+    launch_compact_items(c->stream, c->pend.items, c->pend.nitems, c->pend.n_out, c->pend.dense_off, nullptr,
+                         c->pend.sc, dk, dc, c->wide, c->pend.narrow, nullptr, nullptr, nullptr);
+    c->timer.end(c->stream, "compact_items", (8.0 * c->kw + (c->pend.narrow ? 4.0 : 8.0) + 8.0 * c->kw + 8.0) * (double)nd);
+    st = hipGetLastError() == hipSuccess ? sync(c) : fail(OKM_E_DEVICE, "compact_items launch");
+    if (st != OKM_OK) {
+        c->pool.put(dk);
+        c->pool.put(dc);
+        return st;
+    }
+    for (void *p : c->pend.hold) c->pool.put(p);
+    c->pend = okm_ctx::Pending{};
+    c->res_keys = dk;
+    c->res_counts = dc;
+    c->hprof.mark("dense");
     return OKM_OK;
 }
 
@@ -771,6 +836,7 @@ static okm_status sorted_run_bins(okm_ctx *c, Run &run) {
 // The counted result becomes a folded run: a sorted weighted table owned by
 // the context, at its exact size (the count sized it by its instances).
 static okm_status result_to_folded_run(okm_ctx *c, Run *out) {
+    OKM_TRY(ensure_dense(c));
     if (!c->res_host) OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.25));
     Run run;
     run.keys = c->res_keys;
@@ -1554,6 +1620,31 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             level_bufs.erase(level_bufs.begin() + at);
         }
     }
+    if (!dst && in_place && !donated && c->share_result) {
+        // the table stays as the items' sorted runs (okm_ctx::Pending): the
+        // dense copy is made by its first reader (ensure_dense)
+        drop_pending(c);
+        okm_ctx::Pending &p = c->pend;
+        p.on = true;
+        p.items = d_items;
+        p.nitems = nkept;
+        p.n_out = n_out;
+        p.dense_off = dense_off;
+        p.sc = sc;
+        p.narrow = narrow;
+        p.hold = level_bufs;
+        for (void *q : {(void *)d_segs, (void *)d_items, (void *)n_out, (void *)dense_off, (void *)sc}) p.hold.push_back(q);
+        level_bufs.clear();
+        sc = nullptr;
+        n_out = dense_off = nullptr;
+        release_own();
+        c->n_res = nd;
+        c->info.distinct = nd;
+        c->counted = true;
+        c->hprof.mark("count (runs kept)");
+        c->hprof.dump("count");
+        return OKM_OK;
+    }
     if (!in_place) release_level();
     if (!dst) {
         if (blk) {
@@ -2091,7 +2182,10 @@ static okm_status count_spilled(okm_ctx *c) {
             c->runs = std::move(grp);
             c->counted = false;
             st = count_all_sorted(c);
-            c->runs.clear();
+            // (borrowed slices are skipped; runs a fallback partitioned into
+            // owned memory go back to the pool)
+            release_runs(c, c->runs);
+            if (st == OKM_OK) st = ensure_dense(c);
             if (st == OKM_OK && c->n_res) {  // the group's table off the device, appended in key order
                 const size_t o = hk.size() / kw;
                 hk.resize((o + c->n_res) * kw);
@@ -2572,6 +2666,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
             } else {
             // keep the group's table at its exact size: the bound-sized one goes
             // back to the pool and serves the next group
+                OKM_TRY(ensure_dense(c));
                 OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, c->n_res, 1.0));
                 tabs.push_back(Tab{c->res_keys, c->res_counts, c->n_res});
                 c->res_keys = c->res_counts = nullptr;
@@ -2659,6 +2754,7 @@ static okm_status l1_batch_or_spill(okm_ctx *c, const uint8_t *d_seq, uint64_t n
 namespace okm {
 okm_status result_view(okm_ctx *c, const uint64_t **keys, const uint64_t **counts, uint64_t *n, bool *on_host) {
     OKM_TRY(okm_count(c, nullptr));
+    OKM_TRY(ensure_dense(c));
     *keys = c->res_keys;
     *counts = c->res_counts;
     *n = c->n_res;
@@ -2941,6 +3037,7 @@ static okm_status result_to_device(okm_ctx *c) {
 okm_status okm_result_device(okm_ctx *c, const uint64_t **d_keys, const uint64_t **d_counts, uint64_t *n) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     OKM_TRY(okm_count(c, nullptr));
+    OKM_TRY(ensure_dense(c));
     OKM_TRY(result_to_device(c));
     if (d_keys) *d_keys = c->res_keys;
     if (d_counts) *d_counts = c->res_counts;
@@ -3006,6 +3103,7 @@ static okm_status fetch_result(okm_ctx *c, uint64_t min_count, uint64_t *keys, u
                                uint64_t *n, bool dst_on_device) {
     *n = 0;
     if (c->n_res == 0) return OKM_OK;
+    OKM_TRY(ensure_dense(c));
     if (!c->res_host)
         return fetch_range(c, c->res_keys, c->res_counts, c->n_res, min_count, keys, counts, cap, n, dst_on_device);
     constexpr uint64_t kSlice = uint64_t(1) << 26;

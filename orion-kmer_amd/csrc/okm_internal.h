@@ -30,6 +30,11 @@ int64_t test_knob(int knob);
 // Give back the idle device memory every context's pool on `device` caches
 // (a hipMalloc outside the pools, e.g. a communicator buffer, retries after it).
 void trim_device_pools(int device);
+// Device bytes held outside the arenas (communicator buffers) count against
+// the per-device budget too: +bytes when allocated, -bytes when freed.
+void device_bytes_add(int device, int64_t delta);
+// Would `bytes` more device memory pass the per-device budget (OKM_HBM_CAP)?
+bool device_over_budget(int device, size_t bytes);
 
 // The counted table where it lies: device memory, or (*on_host) page-locked
 // host memory when count_spilled left it there (okm_group_write_counts_tsv

@@ -469,6 +469,17 @@ class Comm:
     def size(self) -> int:
         return int(lib().okm_comm_size(self.h))
 
+    def info(self) -> Dict[str, object]:
+        """What this rank's communicator is (okm_comm_get_info): the ranks /
+        rank / device it was created with, what the transport itself reports
+        (RCCL: ncclCommCount, ncclCommUserRank, ncclCommCuDevice) and the
+        device's PCI bus id."""
+        ci = _lib.CommInfo()
+        check(lib().okm_comm_get_info(self.h, byref(ci)), "okm_comm_get_info")
+        return {"size": ci.size, "rank": ci.rank, "device": ci.device, "transport": ci.transport.decode(),
+                "transport_ranks": ci.transport_ranks, "transport_rank": ci.transport_rank,
+                "transport_device": ci.transport_device, "pci_bus_id": ci.pci_bus_id.decode()}
+
     def merge_owned(self, local: "KmerCounter", owner: "KmerCounter") -> int:
         """Collective: owner <- this rank's key range of all ranks' tables."""
         n = c_uint64()

@@ -75,6 +75,19 @@ def _killpg(p: subprocess.Popen, sig: int) -> None:
         pass
 
 
+def _stop_all(procs: Sequence[subprocess.Popen], grace_s: float) -> None:
+    live = [p for p in procs if p.poll() is None]
+    for p in live:
+        _killpg(p, signal.SIGTERM)
+    t_end = time.time() + grace_s
+    for p in live:
+        try:
+            p.wait(timeout=max(0.0, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            _killpg(p, signal.SIGKILL)
+            p.wait()
+
+
 def spawn_ranks(cmd: Sequence[str], world: int, grace_s: float = 10.0, poll_s: float = 0.05,
                 stdout=None) -> int:
     """Run `cmd` as `world` ranks (one process each) and wait for all of
@@ -107,30 +120,26 @@ def spawn_ranks(cmd: Sequence[str], world: int, grace_s: float = 10.0, poll_s: f
         raise
     rc = 0
     failed = None
-    while True:
-        alive = 0
-        for r, p in enumerate(procs):
-            s = p.poll()
-            if s is None:
-                alive += 1
-            elif s != 0 and failed is None:
-                failed = r
-                rc = s if s > 0 else 128 - s
-        if failed is not None or alive == 0:
-            break
-        time.sleep(poll_s)
-    if failed is not None:
-        sys.stderr.write(f"launch: rank {failed} exited with status {rc}; stopping the other ranks\n")
-        for p in procs:
-            if p.poll() is None:
-                _killpg(p, signal.SIGTERM)
-        t_end = time.time() + grace_s
-        for p in procs:
-            try:
-                p.wait(timeout=max(0.0, t_end - time.time()))
-            except subprocess.TimeoutExpired:
-                _killpg(p, signal.SIGKILL)
-                p.wait()
+    try:
+        while True:
+            alive = 0
+            for r, p in enumerate(procs):
+                s = p.poll()
+                if s is None:
+                    alive += 1
+                elif s != 0 and failed is None:
+                    failed = r
+                    rc = s if s > 0 else 128 - s
+            if failed is not None or alive == 0:
+                break
+            time.sleep(poll_s)
+        if failed is not None:
+            sys.stderr.write(f"launch: rank {failed} exited with status {rc}; stopping the other ranks\n")
+    finally:
+        # a failing rank, Ctrl-C or any error in this process: every rank still
+        # running is stopped by process group (each rank has its own session, so
+        # the terminal's signal never reaches it), SIGTERM then SIGKILL
+        _stop_all(procs, grace_s)
     if relay is not None:
         relay.join(timeout=grace_s)
     return rc

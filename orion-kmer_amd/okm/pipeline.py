@@ -154,6 +154,35 @@ def agree_or_raise(comm, failure: Optional[BaseException], what: str = "count") 
         raise PeerFailure(f"{bad} peer rank(s) failed their {what}; every rank stops at this step")
 
 
+def comm_audit(infos: Sequence[dict], world: int) -> dict:
+    """The N>1 line's proof of what ran: every rank's ``Comm.info()``
+    (gathered by the caller, rank order) summarised -- the communicator size
+    the library holds (okm_comm_size), the ranks the transport itself
+    reports (RCCL's ncclCommCount / ncclCommUserRank / ncclCommCuDevice) and
+    each rank's device PCI bus id.  ``ok``: `world` ranks, every one agreeing
+    on it, the transport reporting `world` ranks with ranks 0..world-1, and
+    (RCCL) `world` distinct PCI devices -- N ranks were N GPUs."""
+    infos = list(infos)
+    sizes = sorted({int(i["size"]) for i in infos})
+    tranks = sorted({int(i["transport_ranks"]) for i in infos})
+    transports = sorted({str(i["transport"]) for i in infos})
+    pci = [str(i["pci_bus_id"]) for i in infos]
+    distinct = len(set(p for p in pci if p))
+    ok = (len(infos) == world and sizes == [world] and tranks == [world]
+          and sorted(int(i["transport_rank"]) for i in infos) == list(range(world))
+          and sorted(int(i["rank"]) for i in infos) == list(range(world)))
+    if transports == ["rccl"]:
+        ok = ok and distinct == world
+    return {"comm_ranks": sizes[0] if len(sizes) == 1 else sizes,
+            "transport": transports[0] if len(transports) == 1 else transports,
+            "transport_ranks": tranks[0] if len(tranks) == 1 else tranks,
+            "distinct_pci_bus_ids": distinct,
+            "ranks": [{"rank": int(i["rank"]), "device": int(i["device"]), "pci_bus_id": str(i["pci_bus_id"]),
+                       "transport_rank": int(i["transport_rank"]),
+                       "transport_device": int(i["transport_device"])} for i in infos],
+            "ok": bool(ok)}
+
+
 class OwnedCountPipeline:
     """bench.py's N>1 step loop: per step, reset + add this
     rank's batch (``add_batch(counter, step)``) + ``okm_count`` into one of

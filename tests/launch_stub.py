@@ -16,6 +16,7 @@ rank = int(os.environ["RANK"])
 keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
         "HSA_ENABLE_IPC_MODE_LEGACY")
 env = {k: os.environ.get(k) for k in keys}
+env["pid"] = os.getpid()
 fail = os.environ.get("STUB_FAIL_RANK")
 if fail is not None and int(fail) == rank:
     time.sleep(float(os.environ.get("STUB_FAIL_AFTER", "0")))

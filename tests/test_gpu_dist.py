@@ -27,6 +27,19 @@ def comm1():
     c.close()
 
 
+def test_comm_info_rccl_reports_itself(comm1):
+    """okm_comm_get_info over real RCCL: what bench.py's N>1 `comm` object is
+    built from -- RCCL's own rank count / rank / device and the PCI bus id."""
+    from okm.pipeline import comm_audit
+    i = comm1.info()
+    assert i["transport"] == "rccl" and i["size"] == 1 and i["rank"] == 0 and i["device"] == 0
+    assert i["transport_ranks"] == 1 and i["transport_rank"] == 0 and i["transport_device"] == 0
+    assert len(i["pci_bus_id"]) >= 7 and ":" in i["pci_bus_id"]
+    a = comm_audit([i], 1)
+    assert a["ok"] and a["distinct_pci_bus_ids"] == 1
+    assert not comm_audit([i, dict(i, rank=1, transport_rank=1)], 2)["ok"]  # 2 ranks on one GPU: refused
+
+
 def _batch(n, genome, seed):
     return okm.synth_reads(n, 150, genome_len=genome, genome_seed=seed, seed=seed)
 

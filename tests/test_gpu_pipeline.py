@@ -26,7 +26,7 @@ import pytest
 import torch
 
 import okm
-from okm.pipeline import OwnedCountPipeline, PeerFailure, agree_or_raise
+from okm.pipeline import comm_audit, OwnedCountPipeline, PeerFailure, agree_or_raise
 from oracle import OracleCounter, count_separated_ranges_mt
 from test_gpu_c3 import c3_key_ranges, dev_tensor
 
@@ -117,6 +117,13 @@ def test_owned_count_pipeline_loopback_exact(P, workers):
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert all(p.comm.merges == nsteps for p in pipes)
     assert sum(len(o[1]) > 0 for o in out) >= P - 1  # the owners' ranges are balanced, not one rank's
+    # the N>1 line's audit object (bench.py `comm`) over the same communicators
+    infos = [c.info() for c in comms]
+    audit = comm_audit(infos, P)
+    assert audit["ok"] and audit["comm_ranks"] == P and audit["transport"] == "loopback"
+    assert audit["transport_ranks"] == P and [r["transport_rank"] for r in audit["ranks"]] == list(range(P))
+    assert all(r["pci_bus_id"] for r in audit["ranks"]) and audit["distinct_pci_bus_ids"] == 1
+    assert not comm_audit(infos[:-1], P)["ok"]  # a missing rank is caught
     for p in pipes:
         p.close()
     for c in comms:

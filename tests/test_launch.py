@@ -59,6 +59,44 @@ def test_failing_rank_fails_the_run_and_stops_the_others(monkeypatch, tmp_path):
     assert time.time() - t0 < 60
 
 
+def test_interrupted_launcher_stops_every_rank(monkeypatch, tmp_path):
+    """Ctrl-C (or any error) in the launching process must not leave the
+    ranks running: each has its own session, so the terminal's SIGINT never
+    reaches them, and ranks blocked in a collective would hold their GPUs."""
+    _env(monkeypatch, tmp_path, STUB_HANG="1")
+    real_sleep = time.sleep
+
+    def interrupt_once_started(s):
+        if all((tmp_path / f"rank{r}.json").exists() for r in (1, 2)):
+            raise KeyboardInterrupt
+        real_sleep(s)
+
+    monkeypatch.setattr(launch.time, "sleep", interrupt_once_started)
+    t0 = time.time()
+    try:
+        launch.spawn_ranks([sys.executable, STUB], 3, grace_s=5.0, stdout=io.StringIO())
+        raise AssertionError("the interrupt must propagate")
+    except KeyboardInterrupt:
+        pass
+    monkeypatch.setattr(launch.time, "sleep", real_sleep)
+    assert time.time() - t0 < 60
+    for r in (1, 2):
+        with open(tmp_path / f"rank{r}.json") as fh:
+            pid = json.load(fh)["pid"]
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            try:
+                os.kill(pid, 0)  # still there (or a zombie not yet reaped by init)?
+            except ProcessLookupError:
+                break
+            with open(f"/proc/{pid}/stat") as st:
+                if st.read().split()[2] == "Z":
+                    break
+            real_sleep(0.1)
+        else:
+            raise AssertionError(f"rank {r} (pid {pid}) still running after the launcher was interrupted")
+
+
 def test_failing_rank0_fails_the_run(monkeypatch, tmp_path):
     _env(monkeypatch, tmp_path, STUB_FAIL_RANK="0")
     assert launch.spawn_ranks([sys.executable, STUB], 2, grace_s=5.0, stdout=io.StringIO()) == 3
