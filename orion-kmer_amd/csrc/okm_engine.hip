@@ -639,27 +639,56 @@ static okm_status sync(okm_ctx *c) {
 static okm_status ensure_dense(okm_ctx *c) {
     if (!c->pend.on) return OKM_OK;
     const uint64_t nd = c->n_res;
-    uint64_t *dk = nullptr, *dc = nullptr;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &dk));
-    okm_status st = pool_get(c->pool, std::max<uint64_t>(nd, 1), &dc);
-    if (st != OKM_OK) {
+    const uint64_t kb = std::max<uint64_t>(nd, 1) * 8 * c->kw, cb = std::max<uint64_t>(nd, 1) * 8;
+    uint64_t *dk = nullptr, *dc = nullptr, *hk = nullptr, *hc = nullptr;
+    okm_status st = pool_get(c->pool, kb / 8, &dk);
+    if (st == OKM_OK) st = pool_get(c->pool, cb / 8, &dc);
+    if (st == OKM_E_NOMEM) {
+        // no room on the device for the dense copy: the gather writes it
+        // straight into page-locked, device-mapped host memory (the host tier)
         c->pool.put(dk);
-        return st;
+        dk = dc = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&hk), kb, hipHostMallocMapped) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&hc), cb, hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            host_pinned_free(hk);
+            return fail(OKM_E_NOMEM, "the dense copy of a " + std::to_string(nd) +
+                                         "-entry table fits neither the device nor page-locked host memory");
+        }
+        st = OKM_OK;
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&dk), hk, 0) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&dc), hc, 0) != hipSuccess)
+            st = fail(OKM_E_DEVICE, "hipHostGetDevicePointer");
     }
-    c->timer.begin(c->stream);
-    launch_compact_items(c->stream, c->pend.items, c->pend.nitems, c->pend.n_out, c->pend.dense_off, nullptr,
-                         c->pend.sc, dk, dc, c->wide, c->pend.narrow, nullptr, nullptr, nullptr);
-    c->timer.end(c->stream, "compact_items", (8.0 * c->kw + (c->pend.narrow ? 4.0 : 8.0) + 8.0 * c->kw + 8.0) * (double)nd);
-    st = hipGetLastError() == hipSuccess ? sync(c) : fail(OKM_E_DEVICE, "compact_items launch");
+    if (st == OKM_OK) {
+        c->timer.begin(c->stream);
+        launch_compact_items(c->stream, c->pend.items, c->pend.nitems, c->pend.n_out, c->pend.dense_off, nullptr,
+                             c->pend.sc, dk, dc, c->wide, c->pend.narrow, nullptr, nullptr, nullptr);
+        c->timer.end(c->stream, "compact_items",
+                     (8.0 * c->kw + (c->pend.narrow ? 4.0 : 8.0) + 8.0 * c->kw + 8.0) * (double)nd);
+        st = hipGetLastError() == hipSuccess ? sync(c) : fail(OKM_E_DEVICE, "compact_items launch");
+    }
     if (st != OKM_OK) {
-        c->pool.put(dk);
-        c->pool.put(dc);
+        if (hk) {
+            host_pinned_free(hk);
+            host_pinned_free(hc);
+        } else {
+            c->pool.put(dk);
+            c->pool.put(dc);
+        }
         return st;
     }
     for (void *p : c->pend.hold) c->pool.put(p);
     c->pend = okm_ctx::Pending{};
-    c->res_keys = dk;
-    c->res_counts = dc;
+    if (hk) {
+        c->res_keys = hk;
+        c->res_counts = hc;
+        c->res_host = true;
+        c->host_bytes += kb + cb;
+    } else {
+        c->res_keys = dk;
+        c->res_counts = dc;
+    }
     c->hprof.mark("dense");
     return OKM_OK;
 }
@@ -880,8 +909,8 @@ static okm_status before_add(okm_ctx *c) {
 // runs belong to the caller.
 static void free_run(okm_ctx *c, Run &r) {
     if (r.borrowed) return;
-    if (r.host) {
-        host_table_free(c, r.keys, r.counts, r.n);
+    if (r.host) {  // (a batch run moved there by spill_runs: its whole capacity)
+        host_table_free(c, r.keys, r.counts, r.sorted ? r.n : (r.off.empty() ? 0 : r.off.back()));
     } else {
         c->pool.put(r.keys);
         c->pool.put(r.counts);
@@ -897,8 +926,8 @@ static void release_runs(okm_ctx *c, std::vector<Run> &runs) {
 // Count the context's unsorted runs (batches) alone into one sorted table and
 // keep it, as a folded run, beside the sorted runs already there.
 static okm_status count_unsorted_to_table(okm_ctx *c) {
-    std::vector<Run> keep, batches;
-    for (auto &r : c->runs) (r.sorted ? keep : batches).push_back(std::move(r));
+    std::vector<Run> keep, batches;  // (batch runs in host memory stay for count_spilled)
+    for (auto &r : c->runs) (r.sorted || r.host ? keep : batches).push_back(std::move(r));
     c->runs = std::move(batches);
     c->counted = false;
     const bool outer = !c->may_take_runs, shared = c->share_result;
@@ -907,8 +936,15 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
     okm_status st = c->runs.empty() ? OKM_OK : count_general(c);
     if (outer) c->may_take_runs = false;
     c->share_result = shared;
+    if (st != OKM_OK) {
+        // the batches are intact (a count reads them until it succeeds; a
+        // count that wrote into one set input_lost): they stay, so the
+        // caller's fallback (do_count: the host tier) can count them
+        for (auto &r : keep) c->runs.push_back(std::move(r));
+        return st;
+    }
     Run t;
-    if (st == OKM_OK && !c->runs.empty()) st = result_to_folded_run(c, &t);
+    if (!c->runs.empty()) st = result_to_folded_run(c, &t);
     release_runs(c, c->runs);
     for (auto &r : keep) c->runs.push_back(std::move(r));
     if (st != OKM_OK) return st;
@@ -964,6 +1000,38 @@ static okm_status spill_tables(okm_ctx *c, double need) {
         c->host_bytes += kb + cb;
         c->spills += 1;
         c->hprof.mark("spill");
+    }
+    return OKM_OK;
+}
+
+// Move every uncounted batch run (L1-partitioned keys, no table yet) to
+// page-locked host memory: the last resort when even one count's working set
+// does not fit beside them.  count_spilled then counts the key space in
+// groups of L1 bins, each group's slices uploaded and counted on the device.
+static okm_status spill_runs(okm_ctx *c) {
+    for (auto &r : c->runs) {
+        if (r.sorted || r.host || r.borrowed || r.off.empty()) continue;
+        const uint64_t words = r.off.back() * c->kw;
+        const uint64_t kb = words * 8, cb = r.counts ? r.off.back() * 8 : 0;
+        uint64_t *hk = static_cast<uint64_t *>(host_pinned_alloc(std::max<uint64_t>(kb, 8)));
+        uint64_t *hc = cb ? static_cast<uint64_t *>(host_pinned_alloc(cb)) : nullptr;
+        if (!hk || (cb && !hc)) {
+            host_pinned_free(hk);
+            host_pinned_free(hc);
+            return fail(OKM_E_NOMEM, "moving a " + std::to_string(kb + cb) +
+                                         " B batch run off the device: page-locked host allocation failed");
+        }
+        if (kb) HIP_TRY(hipMemcpyAsync(hk, r.keys, kb, hipMemcpyDeviceToHost, c->stream));
+        if (cb) HIP_TRY(hipMemcpyAsync(hc, r.counts, cb, hipMemcpyDeviceToHost, c->stream));
+        OKM_TRY(sync(c));
+        c->pool.put(r.keys);
+        c->pool.put(r.counts);
+        r.keys = hk;
+        r.counts = hc;
+        r.host = true;
+        c->host_bytes += kb + cb;
+        c->spills += 1;
+        c->hprof.mark("spill_run");
     }
     return OKM_OK;
 }
@@ -1050,7 +1118,7 @@ static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
     uint64_t held = 0;
     bool uncounted = false;
     for (auto &r : c->runs) {
-        if (r.borrowed || r.folded) continue;
+        if (r.borrowed || r.folded || r.host) continue;
         held += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);  // allocations, not keys
         uncounted = true;
     }
@@ -2013,11 +2081,14 @@ static okm_status do_count(okm_ctx *c) {
     if (st == OKM_E_NOMEM && !c->input_lost && outer) {
         // out of device memory: every table to host memory, then the key-range
         // grouped count of count_spilled (the reference's map just grows)
-        bool tables = false;
-        for (auto &r : c->runs) tables |= r.folded && !r.host && !r.borrowed;
-        if (tables) {
+        // (batch runs too: with no folded table to move, the batches' L1
+        // runs go to host memory and are counted group by group from there)
+        bool movable = false;
+        for (auto &r : c->runs) movable |= !r.host && !r.borrowed && (r.folded || !r.sorted);
+        if (movable) {
             c->hprof.mark("count_nomem");
             st = spill_tables(c, INFINITY);
+            if (st == OKM_OK) st = spill_runs(c);
             if (st == OKM_OK) st = do_count_runs(c);
         }
     }
@@ -2109,17 +2180,22 @@ static okm_status do_count_runs(okm_ctx *c) {
 }
 
 // okm_count with tables in host memory (spill_tables): the batches are
-// counted into one more table first; then the key space is counted in
-// groups of L1 bins sized to the device's room -- each group's slices of the
-// device tables in place and of the host tables copied in, merged by the
-// sorted-run count -- and the groups' tables, in key order, are the result:
-// on the device when it fits there, else in page-locked host memory
-// (okm_fetch_counts / the TSV writer stream it; okm_result_device uploads it
-// or fails with OKM_E_NOMEM).
+// counted into one more table first -- unless batch runs lie in host memory
+// too (spill_runs: no count's working set fitted beside them), in which case
+// every batch run goes there and is counted group by group with the tables;
+// then the key space is counted in groups of L1 bins sized to the device's
+// room -- each group's slices of the device runs in place and of the host
+// runs copied in, counted (and merged with the tables' slices) on the device
+// -- and the groups' tables, in key order, are the result: on the device when
+// it fits there, else in page-locked host memory (okm_fetch_counts / the TSV
+// writer stream it; okm_result_device uploads it or fails with OKM_E_NOMEM).
 static okm_status count_spilled(okm_ctx *c) {
-    bool any_unsorted = false;
-    for (auto &r : c->runs) any_unsorted |= !r.sorted;
-    if (any_unsorted) {
+    bool unsorted_dev = false, unsorted_host = false;
+    for (auto &r : c->runs)
+        if (!r.sorted) (r.host ? unsorted_host : unsorted_dev) = true;
+    if (unsorted_host) {
+        if (unsorted_dev) OKM_TRY(spill_runs(c));
+    } else if (unsorted_dev) {
         OKM_TRY(spill_tables(c, 4.5 * uncounted_bytes(c)));
         OKM_TRY(count_unsorted_to_table(c));
     }
@@ -2144,7 +2220,7 @@ static okm_status count_spilled(okm_ctx *c) {
         uint32_t b1 = b0;
         uint64_t pairs = 0;
         while (b1 < nb && (b1 == b0 || pairs + binlen[b1] <= gmax)) pairs += binlen[b1++];
-        uint64_t host_pairs = 0;
+        uint64_t host_pairs = 0;  // (batch runs: their bins' capacities, gaps included)
         for (auto &r : all)
             if (r.host) host_pairs += r.off[b1] - r.off[b0];
         uint64_t *uk = nullptr, *uc = nullptr;
@@ -2157,31 +2233,42 @@ static okm_status count_spilled(okm_ctx *c) {
         for (auto &r : all) {
             if (st != OKM_OK) break;
             const uint64_t a = r.off[b0], e = r.off[b1];
-            if (a == e) continue;
+            uint64_t data = 0;  // keys in the group's bins
+            for (uint32_t b = b0; b < b1; ++b) data += r.len(b);
+            if (a == e || data == 0) continue;
             Run t;
-            t.sorted = t.borrowed = true;
-            t.n = e - a;
+            t.sorted = r.sorted;
+            t.borrowed = true;
+            t.n = r.sorted ? e - a : 0;
             if (r.host) {
                 t.keys = uk + at * kw;
                 t.counts = r.counts ? uc + at : nullptr;
-                if (hipMemcpyAsync(t.keys, r.keys + a * kw, t.n * 8 * kw, hipMemcpyHostToDevice, c->stream) !=
+                if (hipMemcpyAsync(t.keys, r.keys + a * kw, (e - a) * 8 * kw, hipMemcpyHostToDevice, c->stream) !=
                         hipSuccess ||
                     (r.counts &&
-                     hipMemcpyAsync(t.counts, r.counts + a, t.n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess))
+                     hipMemcpyAsync(t.counts, r.counts + a, (e - a) * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess))
                     st = fail(OKM_E_DEVICE, "count_spilled: host-to-device copy");
-                at += t.n;
+                at += e - a;
             } else {
                 t.keys = r.keys + a * kw;
                 t.counts = r.counts ? r.counts + a : nullptr;
             }
             t.off.assign(nb + 1, 0);
             for (uint32_t b = 0; b <= nb; ++b) t.off[b] = std::min(std::max(r.off[b], a), e) - a;
+            if (!r.end.empty()) {  // a batch run's bins end before their sampled capacities
+                t.end.assign(nb, 0);
+                for (uint32_t b = 0; b < nb; ++b)
+                    t.end[b] = (b >= b0 && b < b1) ? std::min(std::max(r.end[b], a), e) - a : t.off[b];
+            }
             grp.push_back(std::move(t));
         }
         if (st == OKM_OK && !grp.empty()) {
+            bool grp_sorted = true;
+            for (auto &t : grp) grp_sorted &= t.sorted;
             c->runs = std::move(grp);
             c->counted = false;
-            st = count_all_sorted(c);
+            // (batch slices: partitioned and counted, merged with the tables' slices)
+            st = grp_sorted ? count_all_sorted(c) : do_count_runs(c);
             // (borrowed slices are skipped; runs a fallback partitioned into
             // owned memory go back to the pool)
             release_runs(c, c->runs);
@@ -2741,14 +2828,34 @@ static bool device_ok(int device, std::string *why) {
 
 // l1_batch, once more after making room when the device is out of memory:
 // what is pending is folded into a table and the tables go to host memory.
+// l1_batch, and when its L1 run does not fit: the pending batches folded
+// into a table (or, when even that count does not fit, moved to host memory),
+// the tables moved to host memory, and the batch again; when the batch alone
+// still does not fit (a single batch past the device budget), its two halves
+// one after the other -- the first [0, q + k - 1) holds every window that
+// starts before the 16-B aligned q, the second [q, n) every one from q on, so
+// no window is lost or counted twice (a window needs k bytes: one starting
+// at or past q ends past the first half) -- down to 1 MiB pieces.  The
+// reference's map grows in host RAM (count.rs:48); this never fails for lack
+// of device memory while host memory lasts.
 static okm_status l1_batch_or_spill(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     okm_status st = l1_batch(c, d_seq, n);
     if (st != OKM_E_NOMEM || c->input_lost) return st;
     bool pending = false;
-    for (auto &r : c->runs) pending |= !r.sorted;
-    if (pending) OKM_TRY(fold(c));
+    for (auto &r : c->runs) pending |= !r.sorted && !r.host;
+    if (pending) {
+        st = fold(c);
+        if (st == OKM_E_NOMEM && !c->input_lost) st = spill_runs(c);
+        OKM_TRY(st);
+    }
     OKM_TRY(spill_tables(c, INFINITY));
-    return l1_batch(c, d_seq, n);
+    st = l1_batch(c, d_seq, n);
+    if (st != OKM_E_NOMEM || c->input_lost || n < (uint64_t(1) << 20)) return st;
+    OKM_TRY(spill_runs(c));
+    c->hprof.mark("batch_split");
+    const uint64_t q = (n / 2) & ~uint64_t(15);
+    OKM_TRY(l1_batch_or_spill(c, d_seq, std::min<uint64_t>(n, q + c->k - 1)));
+    return l1_batch_or_spill(c, d_seq + q, n - q);
 }
 
 namespace okm {

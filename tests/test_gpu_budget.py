@@ -113,3 +113,48 @@ def test_budget_8gb_result_stays_in_host_memory():
     assert len(ek) > 10_000 and np.array_equal(sk, ek) and np.array_equal(sc, ec)
     ctr.close()
     buf.free()
+
+
+# ---------------------------------------------------------------------------
+# One batch past the device, with no folded table to move
+# ---------------------------------------------------------------------------
+
+C2_READS = 3_355_443  # BASELINE configs[1]: 1 GiB of 150 bp FASTQ
+
+
+@pytest.mark.parametrize("budget", [6_000_000_000, 2_500_000_000])
+def test_budget_single_c2_batch_past_the_device(budget):
+    """One configs[1] batch under a device budget its count does not fit
+    (6 GB: the L1 run fits, its count's working set and table do not) or
+    its L1 run itself does not fit (2.5 GB: the batch is taken as two
+    halves that overlap by k - 1 bytes, okm_engine.hip l1_batch_or_spill).
+    There is no folded table to move: the batch runs go to host memory and
+    the key space is counted group by group from there (count_spilled).
+    Exact on 12 key ranges against the restatement over every read."""
+    buf = okm.DeviceBuffer(C2_READS * STRIDE)
+    okm.synth_reads_device(buf.address, C2_READS, READ_LEN, genome_len=100_000_000, genome_seed=2, seed=2,
+                           first_read=0, sub_rate=0.001, n_rate=0.0001)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    testing.set_knob("hbm_budget_bytes", budget)
+    ctr = okm.KmerCounter(K)
+    ctr.add_device_batch(buf.address, C2_READS * STRIDE)
+    nd = ctr.count()
+    info = ctr.engine_info()
+    assert info["spills"] >= 1, info  # the host tier was used
+    assert info["device_peak_bytes"] <= 1.02 * budget, info
+    assert info["folds"] == 0, info
+    gk, gc = ctr.result(1)
+    ctr.close()
+    assert 0.9e8 < nd < 1.3e8 and len(gk) == nd and int(gc.sum()) == info["kmers"]
+    assert bool((gk[1:] > gk[:-1]).all())
+    host = np.empty(C2_READS * STRIDE, dtype=np.uint8)
+    buf.download(host)
+    buf.free()
+    ranges = c3_key_ranges(K)
+    ek, ec, w = count_separated_ranges_mt([host], K, ranges, _threads())
+    assert w == info["kmers"]
+    parts = [np.searchsorted(gk, np.uint64(v)) for r in ranges for v in r]
+    sk = np.concatenate([gk[parts[2 * i]:parts[2 * i + 1]] for i in range(len(ranges))])
+    sc = np.concatenate([gc[parts[2 * i]:parts[2 * i + 1]] for i in range(len(ranges))])
+    assert len(ek) > 1000 and np.array_equal(sk, ek) and np.array_equal(sc, ec)
