@@ -296,7 +296,10 @@ okm_status okm_comm_get_info(const okm_comm *comm, okm_comm_info *info);
  * take more input, and local may be reset.  A rank that fails between the
  * collectives (e.g. out of memory) reports it to its peers, so every rank
  * returns an error; a failure inside a send/recv aborts the communicator
- * (later calls: OKM_E_COMM). */
+ * (later calls: OKM_E_COMM).  At one rank (comm size 1, owner != local) the
+ * owner's range is the whole table: it takes local's table as it stands (no
+ * exchange, no copy: the two contexts swap their device memory) and local is
+ * left reset. */
 okm_status okm_merge_owned(okm_ctx *local, okm_comm *comm, okm_ctx *owner, uint64_t *n_owned);
 /* okm_merge_owned for n tables under ONE owner split (balanced over the sum of
  * their histograms), so equal keys of different tables meet on one rank: the

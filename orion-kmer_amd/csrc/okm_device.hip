@@ -459,6 +459,44 @@ __device__ __forceinline__ uint64_t lower_bound_bin(const KT *keys, uint64_t lo,
     return lo;
 }
 
+// lower_bound_bin over [0, n), searched outward from a guess g (galloping):
+// a child's start in a run is near len * c / 2^bits when the keys are spread
+// evenly over the part, so a few probes find it instead of ~log2(n) dependent
+// loads from the whole range's midpoints.
+template <typename KT>
+__device__ __forceinline__ uint64_t lower_bound_bin_from(const KT *keys, uint64_t n, uint32_t shift, uint64_t base,
+                                                         uint64_t target, uint64_t g) {
+    if (n == 0) return 0;
+    auto below = [&](uint64_t j) {
+        return (shift >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(keys[j], shift)) - base < target;
+    };
+    if (g >= n) g = n - 1;
+    uint64_t lo, hi;  // the answer lies in [lo, hi]
+    if (below(g)) {
+        lo = g + 1;
+        uint64_t step = 1, p = g + 1;
+        while (p < n && below(p)) {
+            lo = p + 1;
+            step <<= 1;
+            p = g + step;
+        }
+        hi = p < n ? p : n;
+    } else {
+        hi = g;
+        uint64_t step = 1;
+        bool more = g >= 1;
+        uint64_t p = more ? g - 1 : 0;
+        while (more && !below(p)) {
+            hi = p;
+            step <<= 1;
+            more = g >= step;
+            p = more ? g - step : 0;
+        }
+        lo = more ? p + 1 : 0;
+    }
+    return lower_bound_bin(keys, lo, hi, shift, base, target);
+}
+
 template <typename KT>
 __global__ void k_bin_bounds(const KT *__restrict__ keys, uint64_t n, uint32_t shift, uint32_t nbins,
                              ull *__restrict__ out) {
@@ -504,8 +542,8 @@ __global__ void k_sorted_bounds(const DevSortedPart *__restrict__ parts, uint32_
     const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
     const uint32_t c = i - P.item_base;
     const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
-    bounds[x] = P.bits && c ? lower_bound_bin(reinterpret_cast<const KT *>(rb.keys), 0, rb.len, shift1 - P.bits,
-                                              (uint64_t)P.bin << P.bits, c)
+    bounds[x] = P.bits && c ? lower_bound_bin_from(reinterpret_cast<const KT *>(rb.keys), rb.len, shift1 - P.bits,
+                                                   (uint64_t)P.bin << P.bits, c, (rb.len * c) >> P.bits)
                             : 0;
 }
 
@@ -514,7 +552,7 @@ __global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t
                                const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1, uint32_t kw,
                                DevItem *__restrict__ items, DevSeg *__restrict__ segs, ull *__restrict__ itemtot,
                                uint64_t item_max, uint32_t capbits, ull *__restrict__ flags,
-                               const ull *__restrict__ bounds) {
+                               const ull *__restrict__ bounds, ull *__restrict__ part_max) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nitems) return;
     const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
@@ -551,6 +589,7 @@ __global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t
     itemtot[i] = tot;
     if (tot > item_max && shift > capbits) atomicAdd(&flags[0], 1ull);
     atomicMax(&flags[1], tot);
+    atomicMax(&part_max[P.slot], tot);
 }
 
 __global__ void k_set_out_off(DevItem *__restrict__ items, uint32_t nitems, const ull *__restrict__ off) {
@@ -561,7 +600,7 @@ __global__ void k_set_out_off(DevItem *__restrict__ items, uint32_t nitems, cons
 void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
                          const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
                          unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
-                         bool wide, unsigned long long *bounds) {
+                         bool wide, unsigned long long *bounds, unsigned long long *part_max) {
     if (!nitems) return;
     const dim3 g((nitems + 255) / 256), b(256);
     const dim3 gb((uint32_t)(((uint64_t)nitems * nruns + 255) / 256));
@@ -569,11 +608,11 @@ void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t npar
     if (wide) {
         hipLaunchKernelGGL(k_sorted_bounds<K128>, gb, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, bounds);
         hipLaunchKernelGGL(k_sorted_items<K128>, g, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, 2u, items,
-                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds);
+                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds, part_max);
     } else {
         hipLaunchKernelGGL(k_sorted_bounds<ull>, gb, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, bounds);
         hipLaunchKernelGGL(k_sorted_items<ull>, g, b, 0, s, parts, nparts, nitems, rbins, nruns, shift1, 1u, items,
-                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds);
+                           segs, itemtot, item_max, capbits, flags, (const ull *)bounds, part_max);
     }
 }
 

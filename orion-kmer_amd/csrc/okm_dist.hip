@@ -1062,6 +1062,25 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
 okm_status merge_owned_n(okm_ctx *const *locals, okm_comm *m, okm_ctx *const *owners, int nt, uint64_t *n_owned) {
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(m->device));
+    if (m->size == 1) {
+        // one rank: the owner's range is the whole key space and its only
+        // slice the local table -- handed over, no exchange and no copy
+        // (adopt_result; owner == local, or a local still holding runs, takes
+        // the general path below)
+        bool all = true;
+        for (int i = 0; i < nt && all; ++i) {
+            bool adopted = false;
+            OKM_TRY(adopt_result(owners[i], locals[i], &adopted));
+            if (adopted && n_owned) OKM_TRY(okm_count(owners[i], n_owned + i));  // (counted: returns its size)
+            all = adopted;
+        }
+        if (all) {
+            m->last_ms[0] = m->last_ms[1] = m->last_ms[2] = 0;
+            m->last_ms[3] = ms_since(t0);
+            m->last_bytes[0] = m->last_bytes[1] = 0;
+            return OKM_OK;
+        }
+    }
     const uint32_t k = ctx_k(locals[0]);
     const uint32_t bits = std::min<uint32_t>(16, 2 * k);
     const uint32_t nb = 1u << bits, shift = 2 * k - bits;

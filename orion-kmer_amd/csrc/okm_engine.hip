@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <atomic>
 #include <mutex>
 #include <string>
@@ -446,7 +447,7 @@ struct okm_ctx {
     bool wide = false;   // k > 32: K128 keys (two u64 per key)
     uint32_t kw = 1;     // u64 words per key
 
-    DevPool pool;
+    std::unique_ptr<DevPool> pool{new DevPool};  // heap-held: a merge at one rank hands the whole pool over (adopt_result)
     std::vector<Run> runs;
     KernelTimer timer;
     HostProf hprof;
@@ -503,6 +504,7 @@ struct okm_ctx {
         DevItem *items = nullptr;
         uint32_t nitems = 0;
         unsigned long long *n_out = nullptr, *dense_off = nullptr;
+        uint64_t *sk = nullptr;  // the staged runs' keys (nullptr: staged in place, over the items' own keys)
         uint64_t *sc = nullptr;
         bool narrow = false;
         std::vector<void *> hold;  // freed with it: level arrays, segments, items, n_out, offsets, counts
@@ -591,7 +593,7 @@ static void host_table_free(okm_ctx *c, uint64_t *keys, uint64_t *counts, uint64
 }
 
 static void drop_pending(okm_ctx *c) {
-    for (void *p : c->pend.hold) c->pool.put(p);
+    for (void *p : c->pend.hold) c->pool->put(p);
     c->pend = okm_ctx::Pending{};
 }
 
@@ -600,8 +602,8 @@ static void invalidate_result(okm_ctx *c) {
     if (c->res_host) {
         host_table_free(c, c->res_keys, c->res_counts, c->n_res);
     } else {
-        if (c->res_keys) c->pool.put(c->res_keys);
-        if (c->res_counts) c->pool.put(c->res_counts);
+        if (c->res_keys) c->pool->put(c->res_keys);
+        if (c->res_counts) c->pool->put(c->res_counts);
     }
     c->res_host = false;
     c->res_keys = c->res_counts = nullptr;
@@ -619,7 +621,7 @@ static double device_room(okm_ctx *c) {
         (void)hipGetLastError();
         free_b = 0;
     }
-    const double cached = (double)c->pool.cached();
+    const double cached = (double)c->pool->cached();
     const double room = std::min((double)free_b + cached,
                                  hbm_budget(c->device) - (double)DevPool::device_mapped(c->device) + cached);
     return std::max(room, 0.0);
@@ -641,12 +643,12 @@ static okm_status ensure_dense(okm_ctx *c) {
     const uint64_t nd = c->n_res;
     const uint64_t kb = std::max<uint64_t>(nd, 1) * 8 * c->kw, cb = std::max<uint64_t>(nd, 1) * 8;
     uint64_t *dk = nullptr, *dc = nullptr, *hk = nullptr, *hc = nullptr;
-    okm_status st = pool_get(c->pool, kb / 8, &dk);
-    if (st == OKM_OK) st = pool_get(c->pool, cb / 8, &dc);
+    okm_status st = pool_get(*c->pool, kb / 8, &dk);
+    if (st == OKM_OK) st = pool_get(*c->pool, cb / 8, &dc);
     if (st == OKM_E_NOMEM) {
         // no room on the device for the dense copy: the gather writes it
         // straight into page-locked, device-mapped host memory (the host tier)
-        c->pool.put(dk);
+        c->pool->put(dk);
         dk = dc = nullptr;
         if (hipHostMalloc(reinterpret_cast<void **>(&hk), kb, hipHostMallocMapped) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void **>(&hc), cb, hipHostMallocMapped) != hipSuccess) {
@@ -662,7 +664,7 @@ static okm_status ensure_dense(okm_ctx *c) {
     }
     if (st == OKM_OK) {
         c->timer.begin(c->stream);
-        launch_compact_items(c->stream, c->pend.items, c->pend.nitems, c->pend.n_out, c->pend.dense_off, nullptr,
+        launch_compact_items(c->stream, c->pend.items, c->pend.nitems, c->pend.n_out, c->pend.dense_off, c->pend.sk,
                              c->pend.sc, dk, dc, c->wide, c->pend.narrow, nullptr, nullptr, nullptr);
         c->timer.end(c->stream, "compact_items",
                      (8.0 * c->kw + (c->pend.narrow ? 4.0 : 8.0) + 8.0 * c->kw + 8.0) * (double)nd);
@@ -673,12 +675,12 @@ static okm_status ensure_dense(okm_ctx *c) {
             host_pinned_free(hk);
             host_pinned_free(hc);
         } else {
-            c->pool.put(dk);
-            c->pool.put(dc);
+            c->pool->put(dk);
+            c->pool->put(dc);
         }
         return st;
     }
-    for (void *p : c->pend.hold) c->pool.put(p);
+    for (void *p : c->pend.hold) c->pool->put(p);
     c->pend = okm_ctx::Pending{};
     if (hk) {
         c->res_keys = hk;
@@ -779,7 +781,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     launch_l1_capacity(c->stream, c->Hg, nb, scale, mul, align, limit, cur, c->l1cap);
     HIP_TRY(hipGetLastError());
     Run run;
-    OKM_TRY(pool_get(c->pool, limit * c->kw, &run.keys));
+    OKM_TRY(pool_get(*c->pool, limit * c->kw, &run.keys));
     c->timer.begin(c->stream);
     launch_extract_scatter(c->stream, d_seq, g, nullptr, cur, run.keys, c->l1cap, c->l1cap + 2 * nb + 1);
     c->timer.end(c->stream, "extract_scatter", (double)n);
@@ -792,7 +794,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
                              sizeof(unsigned long long), nb, hipMemcpyDeviceToHost, c->stream));
     OKM_TRY(sync(c));
     if (cap[2 * nb + 1]) {  // some bin outgrew its sampled capacity: redo exactly
-        c->pool.put(run.keys);
+        c->pool->put(run.keys);
         c->hprof.mark("l1.sampled_overflow");
         return OKM_OK;
     }
@@ -807,7 +809,7 @@ static okm_status l1_sampled(okm_ctx *c, const uint8_t *d_seq, uint64_t n, const
     c->l1_ratio = std::max(c->l1_ratio, (double)total / (double)n);
     *placed = true;
     if (total == 0) {
-        c->pool.put(run.keys);
+        c->pool->put(run.keys);
         return OKM_OK;
     }
     c->runs.push_back(std::move(run));
@@ -899,8 +901,8 @@ static okm_status before_add(okm_ctx *c) {
     if (t.n) {
         c->runs.push_back(std::move(t));
     } else {
-        c->pool.put(t.keys);
-        c->pool.put(t.counts);
+        c->pool->put(t.keys);
+        c->pool->put(t.counts);
     }
     return OKM_OK;
 }
@@ -912,8 +914,8 @@ static void free_run(okm_ctx *c, Run &r) {
     if (r.host) {  // (a batch run moved there by spill_runs: its whole capacity)
         host_table_free(c, r.keys, r.counts, r.sorted ? r.n : (r.off.empty() ? 0 : r.off.back()));
     } else {
-        c->pool.put(r.keys);
-        c->pool.put(r.counts);
+        c->pool->put(r.keys);
+        c->pool->put(r.counts);
     }
     r.keys = r.counts = nullptr;
 }
@@ -951,8 +953,8 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
     if (t.n) {
         c->runs.push_back(std::move(t));
     } else if (t.keys) {
-        c->pool.put(t.keys);
-        c->pool.put(t.counts);
+        c->pool->put(t.keys);
+        c->pool->put(t.counts);
     }
     return OKM_OK;
 }
@@ -967,7 +969,7 @@ static okm_status count_unsorted_to_table(okm_ctx *c) {
 // Device bytes a run holds (borrowed and host runs: none).
 static uint64_t run_device_bytes(okm_ctx *c, const Run &r) {
     if (r.borrowed || r.host) return 0;
-    return c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
+    return c->pool->size_of(r.keys) + c->pool->size_of(r.counts);
 }
 
 // Move folded tables to page-locked host memory, oldest first, until the
@@ -992,8 +994,8 @@ static okm_status spill_tables(okm_ctx *c, double need) {
         HIP_TRY(hipMemcpyAsync(hk, r.keys, kb, hipMemcpyDeviceToHost, c->stream));
         if (cb) HIP_TRY(hipMemcpyAsync(hc, r.counts, cb, hipMemcpyDeviceToHost, c->stream));
         OKM_TRY(sync(c));
-        c->pool.put(r.keys);
-        c->pool.put(r.counts);  // (inside the keys' block when shrink_table joined them: ignored)
+        c->pool->put(r.keys);
+        c->pool->put(r.counts);  // (inside the keys' block when shrink_table joined them: ignored)
         r.keys = hk;
         r.counts = hc;
         r.host = true;
@@ -1024,8 +1026,8 @@ static okm_status spill_runs(okm_ctx *c) {
         if (kb) HIP_TRY(hipMemcpyAsync(hk, r.keys, kb, hipMemcpyDeviceToHost, c->stream));
         if (cb) HIP_TRY(hipMemcpyAsync(hc, r.counts, cb, hipMemcpyDeviceToHost, c->stream));
         OKM_TRY(sync(c));
-        c->pool.put(r.keys);
-        c->pool.put(r.counts);
+        c->pool->put(r.keys);
+        c->pool->put(r.counts);
         r.keys = hk;
         r.counts = hc;
         r.host = true;
@@ -1050,7 +1052,7 @@ static okm_status fold(okm_ctx *c) {
     OKM_TRY(count_unsorted_to_table(c));
     c->folds += 1;
     if (c->hprof.on)
-        fprintf(stderr, "[okm fold] #%u counted: peak in use so far %.1f GB\n", c->folds + 0u, c->pool.peak() / 1e9);
+        fprintf(stderr, "[okm fold] #%u counted: peak in use so far %.1f GB\n", c->folds + 0u, c->pool->peak() / 1e9);
     // A context that folds takes 10 L1 bits from here on (and after okm_reset):
     // a fold counts ~3.6 G instances, whose 9-bit parts are too big for one
     // 2048-child pass and go through the fan-out split; 10-bit parts do not
@@ -1100,13 +1102,13 @@ static okm_status fold(okm_ctx *c) {
     if (c->hprof.on) {
         uint64_t tb = 0, tn = 0;
         for (auto &r : c->runs) {
-            tb += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);
+            tb += c->pool->size_of(r.keys) + c->pool->size_of(r.counts);
             tn += r.n;
         }
         fprintf(stderr, "[okm fold] #%u: %zu runs of %.3f G keys holding %.1f GB; pool held %.1f GB, cached %.1f GB; "
                         "peak in use so far %.1f GB\n",
-                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool.held() / 1e9, c->pool.cached() / 1e9,
-                c->pool.peak() / 1e9);
+                c->folds, c->runs.size(), tn / 1e9, tb / 1e9, c->pool->held() / 1e9, c->pool->cached() / 1e9,
+                c->pool->peak() / 1e9);
     }
     return OKM_OK;
 }
@@ -1119,7 +1121,7 @@ static okm_status maybe_fold(okm_ctx *c, uint64_t n) {
     bool uncounted = false;
     for (auto &r : c->runs) {
         if (r.borrowed || r.folded || r.host) continue;
-        held += c->pool.size_of(r.keys) + c->pool.size_of(r.counts);  // allocations, not keys
+        held += c->pool->size_of(r.keys) + c->pool->size_of(r.counts);  // allocations, not keys
         uncounted = true;
     }
     const double w = c->l1_ratio > 0 ? std::min(1.0, c->l1_ratio * 1.03) : 1.0;
@@ -1164,7 +1166,7 @@ static okm_status l1_batch(okm_ctx *c, const uint8_t *d_seq, uint64_t n) {
     c->l1_ratio = std::max(c->l1_ratio, (double)total / (double)n);
     c->hprof.mark("l1.hist+sync");
     if (total == 0) return OKM_OK;
-    OKM_TRY(pool_get(c->pool, run.off.back() * c->kw, &run.keys));
+    OKM_TRY(pool_get(*c->pool, run.off.back() * c->kw, &run.keys));
     c->timer.begin(c->stream);
     launch_extract_scatter(c->stream, d_seq, g, c->HC, c->cursor, run.keys, nullptr, nullptr);
     c->timer.end(c->stream, "extract_scatter", (double)n + 8.0 * c->kw * (double)total);
@@ -1250,10 +1252,10 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     DevSeg *d_segs;
     DevChunk *d_chunks;
     unsigned long long *scan_tmp;
-    OKM_TRY(pool_get(c->pool, psegs.size(), &d_segs));
-    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
-    OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
+    OKM_TRY(pool_get(*c->pool, psegs.size(), &d_segs));
+    OKM_TRY(pool_get(*c->pool, chunks.size(), &d_chunks));
+    OKM_TRY(pool_get(*c->pool, (size_t)nout + 1, &L.d_offs));
+    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
     level_bufs.push_back(d_segs);
     level_bufs.push_back(d_chunks);
     level_bufs.push_back(L.d_offs);
@@ -1275,10 +1277,10 @@ static okm_status split_launch(okm_ctx *c, const std::vector<DevSeg> &segtab, co
     OKM_TRY(sync(c));
     c->hprof.mark("split.hist_sync");
     L.padded = padded;  // bins start on 128-B lines (okm_partition.hip)
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1) * c->kw, &L.lk));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(padded, 1) * c->kw, &L.lk));
     level_bufs.push_back(L.lk);
     if (weighted) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(padded, 1), &L.lc));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(padded, 1), &L.lc));
         level_bufs.push_back(L.lc);
     }
     c->timer.begin(c->stream);
@@ -1329,20 +1331,20 @@ static okm_status split_launch_sampled(okm_ctx *c, const std::vector<DevSeg> &ps
                  o_cp = pack.add(cp);
     uint8_t *blob;
     unsigned long long *scan_tmp;
-    OKM_TRY(pool_get(c->pool, pack.bytes.size(), &blob));
-    OKM_TRY(pool_get(c->pool, (size_t)nout + 1, &L.d_offs));
-    OKM_TRY(pool_get(c->pool, (size_t)nout, &L.d_ends));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
+    OKM_TRY(pool_get(*c->pool, pack.bytes.size(), &blob));
+    OKM_TRY(pool_get(*c->pool, (size_t)nout + 1, &L.d_offs));
+    OKM_TRY(pool_get(*c->pool, (size_t)nout, &L.d_ends));
+    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nout + 1), &scan_tmp));
     for (void *p : {(void *)blob, (void *)L.d_offs, (void *)L.d_ends, (void *)scan_tmp}) level_bufs.push_back(p);
     DevSeg *d_segs = reinterpret_cast<DevSeg *>(blob + o_segs);
     DevChunk *d_chunks = reinterpret_cast<DevChunk *>(blob + o_chunks);
     DevChunk *d_sample = reinterpret_cast<DevChunk *>(blob + o_sample);
     DevCapParent *d_cp = reinterpret_cast<DevCapParent *>(blob + o_cp);
     L.padded = (uint64_t)limit;
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &L.lk));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &L.lk));
     level_bufs.push_back(L.lk);
     if (weighted) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &L.lc));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(L.padded, 1), &L.lc));
         level_bufs.push_back(L.lc);
     }
     OKM_TRY(h2d(c, blob, pack.bytes.data(), pack.bytes.size()));
@@ -1424,7 +1426,7 @@ static uint32_t log2_floor(uint64_t x) {
 // tables hold one slot per instance).
 static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, uint64_t n, double slack) {
     const uint64_t kb = std::max<uint64_t>(n, 1) * 8 * c->kw, cb = std::max<uint64_t>(n, 1) * 8;
-    const double held = (double)c->pool.size_of(*keys) + (double)c->pool.size_of(*counts);
+    const double held = (double)c->pool->size_of(*keys) + (double)c->pool->size_of(*counts);
     if (held <= slack * (double)(kb + cb) + (64u << 20)) return OKM_OK;
     // arena: the table stays where it is and the allocations' tails go back
     // (counts inside the keys' block, as count_and_compact lays a shared
@@ -1432,11 +1434,11 @@ static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, u
     {
         const size_t kpad = (kb + 255) & ~size_t(255);
         uint8_t *kbase = reinterpret_cast<uint8_t *>(*keys);
-        if (reinterpret_cast<uint8_t *>(*counts) == kbase + kpad && c->pool.size_of(*keys) >= kpad + cb &&
-            c->pool.shrink(*keys, kpad + cb))
+        if (reinterpret_cast<uint8_t *>(*counts) == kbase + kpad && c->pool->size_of(*keys) >= kpad + cb &&
+            c->pool->shrink(*keys, kpad + cb))
             return OKM_OK;
-        if (c->pool.size_of(*keys) && c->pool.size_of(*counts) && c->pool.shrink(*keys, kb) &&
-            c->pool.shrink(*counts, cb))
+        if (c->pool->size_of(*keys) && c->pool->size_of(*counts) && c->pool->shrink(*keys, kb) &&
+            c->pool->shrink(*counts, cb))
             return OKM_OK;
     }
     // keys and counts in ONE block (the counts pointer lies inside it, and the
@@ -1446,15 +1448,15 @@ static okm_status shrink_table(okm_ctx *c, uint64_t **keys, uint64_t **counts, u
     // 3.4 G keys of folded tables in 127 GB of blocks instead of 54 GB)
     const uint64_t kpad = (kb + 255) & ~255ull;
     uint8_t *blk;
-    OKM_TRY(pool_get(c->pool, kpad + cb, &blk));
+    OKM_TRY(pool_get(*c->pool, kpad + cb, &blk));
     uint64_t *nk = reinterpret_cast<uint64_t *>(blk), *nc = reinterpret_cast<uint64_t *>(blk + kpad);
     if (n) {
         HIP_TRY(hipMemcpyAsync(nk, *keys, kb, hipMemcpyDeviceToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(nc, *counts, cb, hipMemcpyDeviceToDevice, c->stream));
     }
     OKM_TRY(sync(c));
-    c->pool.put(*keys);
-    c->pool.put(*counts);
+    c->pool->put(*keys);
+    c->pool->put(*counts);
     *keys = nk;
     *counts = nc;
     return OKM_OK;
@@ -1510,7 +1512,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         const size_t need = std::max<uint64_t>(out_total, 1) * 8 * c->kw;
         size_t best = 0;
         for (auto &r : c->runs) {
-            const size_t b = r.borrowed ? 0 : c->pool.size_of(r.keys);
+            const size_t b = r.borrowed ? 0 : c->pool->size_of(r.keys);
             if (b >= need && (!best || b < best)) best = b, sk = r.keys;
         }
     }
@@ -1523,35 +1525,35 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             if (on) c->input_lost = true;
         }
     } lost{c, false};
-    if (!donated && !in_place && !direct) OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
-    if (!direct) OKM_TRY(pool_get(c->pool, sc_words, &sc));
-    OKM_TRY(pool_get(c->pool, nitems + 1, &n_out));
-    OKM_TRY(pool_get(c->pool, nitems + 1, &dense_off));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    if (!donated && !in_place && !direct) OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(out_total, 1) * c->kw, &sk));
+    if (!direct) OKM_TRY(pool_get(*c->pool, sc_words, &sc));
+    OKM_TRY(pool_get(*c->pool, nitems + 1, &n_out));
+    OKM_TRY(pool_get(*c->pool, nitems + 1, &dense_off));
+    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
     uint32_t *defer = nullptr;             // deferred items (tag kernel)
     unsigned long long *status = nullptr;  // per-item look-back words (direct)
     if (direct)
-        OKM_TRY(pool_get(c->pool, nitems, &status));
+        OKM_TRY(pool_get(*c->pool, nitems, &status));
     else
-        OKM_TRY(pool_get(c->pool, nitems, &defer));
+        OKM_TRY(pool_get(*c->pool, nitems, &defer));
     auto release_own = [&]() {
         for (void *p : {(void *)sk, (void *)sc, (void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)defer,
                         (void *)status})
-            if (p && !(donated && p == (void *)sk)) c->pool.put(p);
+            if (p && !(donated && p == (void *)sk)) c->pool->put(p);
     };
     auto release_level = [&]() {
-        for (void *p : level_bufs) c->pool.put(p);
+        for (void *p : level_bufs) c->pool->put(p);
         level_bufs.clear();
-        c->pool.put(d_segs);
+        c->pool->put(d_segs);
     };
     if (c->hprof.on) {
         uint64_t rb = 0;
         for (auto &r : c->runs) rb += run_device_bytes(c, r);
         size_t lb = 0;
-        for (void *p : level_bufs) lb += c->pool.size_of(p);
+        for (void *p : level_bufs) lb += c->pool->size_of(p);
         fprintf(stderr, "[okm count] %u items, %.3f G keys: in use %.1f GB (runs %.1f, level %.1f, staged counts %.1f, "
-                        "staged keys %.1f GB)\n", nitems, in_total / 1e9, c->pool.in_use() / 1e9, rb / 1e9, lb / 1e9,
-                c->pool.size_of(sc) / 1e9, (sk && !donated ? c->pool.size_of(sk) : 0) / 1e9);
+                        "staged keys %.1f GB)\n", nitems, in_total / 1e9, c->pool->in_use() / 1e9, rb / 1e9, lb / 1e9,
+                c->pool->size_of(sc) / 1e9, (sk && !donated ? c->pool->size_of(sk) : 0) / 1e9);
     }
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
     // items past a device-side count (d_nitems) must scan as empty
@@ -1597,7 +1599,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         lost.on = false;  // (groups never write into a run)
         release_own();
         release_level();
-        c->pool.put(d_items);
+        c->pool->put(d_items);
         if (aborted) *aborted = false;  // (known at the sync: count_grouped recounts every group then)
         c->n_res = 0;
         return OKM_OK;
@@ -1629,10 +1631,10 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         // a count past 2^32 in the u32 staging: count again with u64 counts
         // (the input is intact: staging was separate, nothing was compacted)
         c->hprof.mark("count.narrow_overflow");
-        c->pool.put(sc);
+        c->pool->put(sc);
         sc = nullptr;
         narrow = false;
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(out_total, 1), &sc));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(out_total, 1), &sc));
         HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
         HIP_TRY(hipMemsetAsync(d_nitems ? n_out : n_out + nitems, 0,
                                (d_nitems ? nitems + 1 : 1) * sizeof(unsigned long long), c->stream));
@@ -1647,7 +1649,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     if (hv[1]) {  // give every buffer of the step back before failing (long-lived contexts)
         release_own();
         release_level();
-        c->pool.put(d_items);
+        c->pool->put(d_items);
         return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     }
     const uint64_t nd = hv[0];
@@ -1672,15 +1674,15 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
         // ones coalesce (a fold's table then fits where its batches were)
         for (auto &r : c->runs) {
             if (r.borrowed || r.host) continue;
-            c->pool.put(r.keys);
-            c->pool.put(r.counts);
+            c->pool->put(r.keys);
+            c->pool->put(r.counts);
             r.keys = r.counts = nullptr;
         }
         c->took_runs = true;  // (the runs are released after the count)
     } else if (!dst && !in_place && c->share_result) {  // the smallest level block that holds keys and counts
         size_t best = 0, at = 0;
         for (size_t i = 0; i < level_bufs.size(); ++i) {
-            const size_t b = c->pool.size_of(level_bufs[i]);
+            const size_t b = c->pool->size_of(level_bufs[i]);
             if (b >= need && (!best || b < best)) best = b, at = i;
         }
         if (best) {
@@ -1688,22 +1690,28 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             level_bufs.erase(level_bufs.begin() + at);
         }
     }
-    if (!dst && in_place && !donated && c->share_result) {
+    if (!dst && !donated && c->share_result) {
         // the table stays as the items' sorted runs (okm_ctx::Pending): the
-        // dense copy is made by its first reader (ensure_dense)
+        // dense copy is made by its first reader (ensure_dense).  In place,
+        // the runs lie over the items' keys in the level arrays, which stay;
+        // otherwise in the staging array sk, and the level arrays go now.
         drop_pending(c);
+        if (!in_place) release_level();
         okm_ctx::Pending &p = c->pend;
         p.on = true;
         p.items = d_items;
         p.nitems = nkept;
         p.n_out = n_out;
         p.dense_off = dense_off;
+        p.sk = in_place ? nullptr : sk;
         p.sc = sc;
         p.narrow = narrow;
         p.hold = level_bufs;
-        for (void *q : {(void *)d_segs, (void *)d_items, (void *)n_out, (void *)dense_off, (void *)sc}) p.hold.push_back(q);
+        for (void *q : {(void *)d_segs, (void *)d_items, (void *)n_out, (void *)dense_off, (void *)sc, (void *)p.sk})
+            if (q && !(q == (void *)d_segs && !in_place)) p.hold.push_back(q);
         level_bufs.clear();
         sc = nullptr;
+        sk = nullptr;
         n_out = dense_off = nullptr;
         release_own();
         c->n_res = nd;
@@ -1719,8 +1727,8 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
             c->res_keys = reinterpret_cast<uint64_t *>(blk);
             c->res_counts = reinterpret_cast<uint64_t *>(blk + kpad);  // inside the block: the pool ignores it on put
         } else {
-            OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-            OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+            OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+            OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         }
         c->timer.begin(c->stream);
         launch_compact_items(c->stream, d_items, nkept, n_out, dense_off, sk, sc, c->res_keys, c->res_counts, c->wide,
@@ -1730,7 +1738,7 @@ static okm_status count_and_compact(okm_ctx *c, DevItem *d_items, DevSeg *d_segs
     }
     OKM_TRY(sync(c));  // the result is complete (and a group's buffers may serve the next group)
     if (in_place) release_level();
-    c->pool.put(d_items);
+    c->pool->put(d_items);
     release_own();
     lost.on = false;
     c->took_runs |= donated;
@@ -1757,8 +1765,8 @@ static okm_status partition_pairs(okm_ctx *c, const uint64_t *d_keys, const uint
     for (uint64_t o = 0; o < n; o += kChunkKeys) chunks.push_back(DevChunk{0, 0, o, std::min(kChunkKeys, n - o)});
     DevSeg *d_seg;
     DevChunk *d_chunks;
-    OKM_TRY(pool_get(c->pool, 1, &d_seg));
-    OKM_TRY(pool_get(c->pool, chunks.size(), &d_chunks));
+    OKM_TRY(pool_get(*c->pool, 1, &d_seg));
+    OKM_TRY(pool_get(*c->pool, chunks.size(), &d_chunks));
     HIP_TRY(hipMemcpyAsync(d_seg, &s, sizeof(DevSeg), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice, c->stream));
     OKM_TRY(ensure_hc(c, chunks.size() * (size_t)c->nbins));
@@ -1769,16 +1777,16 @@ static okm_status partition_pairs(okm_ctx *c, const uint64_t *d_keys, const uint
     c->timer.end(c->stream, "part_hist", 8.0 * c->kw * (double)n);
     HIP_TRY(hipGetLastError());
     OKM_TRY(hist_to_offsets(c, c->nbins, run.off));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1) * c->kw, &run.keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(run.off.back(), 1) * c->kw, &run.keys));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(run.off.back(), 1), &run.counts));
     c->timer.begin(c->stream);
     launch_part_scatter(c->stream, d_seg, d_chunks, (uint32_t)chunks.size(), c->nbins, c->HC, c->cursor, run.keys,
                         run.counts, c->wide);
     c->timer.end(c->stream, "part_scatter", (16.0 + 16.0 * c->kw) * (double)n);
     HIP_TRY(hipGetLastError());
     OKM_TRY(sync(c));
-    c->pool.put(d_seg);
-    c->pool.put(d_chunks);
+    c->pool->put(d_seg);
+    c->pool->put(d_chunks);
     return OKM_OK;
 }
 
@@ -1790,13 +1798,13 @@ static okm_status partition_pairs(okm_ctx *c, const uint64_t *d_keys, const uint
 static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_segs, uint32_t nitems, uint64_t in_total,
                                      bool weighted, std::vector<void *> &bufs) {
     unsigned long long *n_out, *dense_off, *scan_tmp;
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &n_out));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &dense_off));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
+    OKM_TRY(pool_get(*c->pool, (size_t)nitems + 1, &n_out));
+    OKM_TRY(pool_get(*c->pool, (size_t)nitems + 1, &dense_off));
+    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nitems + 1), &scan_tmp));
     for (void *p : {(void *)n_out, (void *)dense_off, (void *)scan_tmp, (void *)d_items, (void *)d_segs})
         bufs.push_back(p);
     auto release = [&]() {
-        for (void *p : bufs) c->pool.put(p);
+        for (void *p : bufs) c->pool->put(p);
         bufs.clear();
     };
     HIP_TRY(hipMemsetAsync(c->flag, 0, 2 * sizeof(unsigned long long), c->stream));
@@ -1817,8 +1825,8 @@ static okm_status merge_sorted_items(okm_ctx *c, DevItem *d_items, DevSeg *d_seg
         return fail(OKM_E_DEVICE, "merge_items invariant violated (code " + std::to_string(hv[1]) + ")");
     }
     const uint64_t nd = hv[0];
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-    OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+    OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
     c->timer.begin(c->stream);
     launch_merge_items(c->stream, d_items, nitems, d_segs, n_out, dense_off, c->res_keys, c->res_counts, c->flag,
                        weighted, c->wide, true);
@@ -1845,15 +1853,15 @@ static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_
     bufs.push_back(d_items);
     bufs.push_back(d_segs);
     auto release = [&]() {
-        for (void *p : bufs) c->pool.put(p);
+        for (void *p : bufs) c->pool->put(p);
         bufs.clear();
     };
     unsigned long long *n_out = nullptr, *dense_off = nullptr, *scan_tmp = nullptr;
     uint32_t *defer = nullptr;
-    okm_status st = pool_get(c->pool, (size_t)nitems + 1, &n_out);
-    if (st == OKM_OK) bufs.push_back(n_out), st = pool_get(c->pool, (size_t)nitems + 1, &dense_off);
-    if (st == OKM_OK) bufs.push_back(dense_off), st = pool_get(c->pool, scan_tmp_elems(nitems + 1), &scan_tmp);
-    if (st == OKM_OK) bufs.push_back(scan_tmp), st = pool_get(c->pool, (size_t)nitems, &defer);
+    okm_status st = pool_get(*c->pool, (size_t)nitems + 1, &n_out);
+    if (st == OKM_OK) bufs.push_back(n_out), st = pool_get(*c->pool, (size_t)nitems + 1, &dense_off);
+    if (st == OKM_OK) bufs.push_back(dense_off), st = pool_get(*c->pool, scan_tmp_elems(nitems + 1), &scan_tmp);
+    if (st == OKM_OK) bufs.push_back(scan_tmp), st = pool_get(*c->pool, (size_t)nitems, &defer);
     if (st != OKM_OK) {
         release();
         return st;
@@ -1878,8 +1886,8 @@ static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_
         return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hv[1]) + ")");
     }
     const uint64_t nd = hv[0];
-    st = pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys);
-    if (st == OKM_OK) st = pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts);
+    st = pool_get(*c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys);
+    if (st == OKM_OK) st = pool_get(*c->pool, std::max<uint64_t>(nd, 1), &c->res_counts);
     if (st != OKM_OK) {
         release();
         invalidate_result(c);
@@ -1908,28 +1916,35 @@ static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_
 // key-range children by binary search in each run — no key moves — and each
 // child is one multi-segment item.  *fallback: a child is still too big for
 // one item (a hot key); the caller takes the partitioning path instead.
-static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra);
+static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint32_t> &add_bits);
 
 // All runs sorted (see count_sorted_plan).  A child above one item's capacity
 // (canonical-key density gradients inside an L1 bin, a dense run) re-plans
 // with one more key bit for every part, up to 4 times, before giving up to
 // the partitioning path.
 static okm_status count_sorted(okm_ctx *c, bool *fallback) {
-    for (uint32_t extra = 0;; ++extra) {
-        OKM_TRY(count_sorted_plan(c, fallback, extra));
-        if (!*fallback || extra == 4) return OKM_OK;
+    // per part: key bits added to its split after a plan left a child above
+    // one item (count_sorted_plan) -- only the parts that overflowed, e.g. an
+    // owner's first and last L1 bins, which its key range covers in part
+    std::vector<uint32_t> add_bits(c->nbins, 0);
+    for (uint32_t attempt = 0;; ++attempt) {
+        OKM_TRY(count_sorted_plan(c, fallback, add_bits));
+        if (!*fallback || attempt == 6) return OKM_OK;
         c->hprof.mark("sorted.replan");
     }
 }
 
-static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) {
+static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint32_t> &add_bits) {
     *fallback = false;
     const uint32_t R = (uint32_t)c->runs.size();
     const uint64_t item_max = count_item_capacity();
     const uint32_t capbits = count_dense_bits();
     // children by key bits: half an item on average, so the density gradient
     // inside an L1 bin of canonical keys stays below one item
-    const uint64_t target = item_max / 2;
+#ifndef OKM_SORTED_TARGET_Q
+#define OKM_SORTED_TARGET_Q 2
+#endif
+    const uint64_t target = item_max * OKM_SORTED_TARGET_Q / 4;
     bool weighted = false;
     for (auto &r : c->runs) weighted |= r.counts != nullptr;
     std::vector<DevSortedPart> parts;
@@ -1943,7 +1958,8 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
         uint32_t bits = 0;
         if (len > item_max && c->shift1 > capbits)
             while (bits < 20 && bits < c->shift1 && (len >> bits) > target) ++bits;
-        if (bits) bits = std::min<uint32_t>(std::min<uint32_t>(bits + extra, 20u), c->shift1);
+        if (bits || add_bits[b])
+            bits = std::min<uint32_t>(std::min<uint32_t>(bits + add_bits[b], 20u), c->shift1);
         parts.push_back(DevSortedPart{b, bits, nitems, (uint32_t)parts.size()});
         nitems += 1u << bits;
         in_total += len;
@@ -1971,34 +1987,47 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
     DevSeg *d_rbins, *d_segs;
     DevItem *d_items;
     unsigned long long *itemtot, *offs, *tmp, *flags;
-    OKM_TRY(pool_get(c->pool, parts.size(), &d_parts));
-    OKM_TRY(pool_get(c->pool, rbins.size(), &d_rbins));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems * R, &d_segs));
-    OKM_TRY(pool_get(c->pool, nitems, &d_items));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &itemtot));
-    OKM_TRY(pool_get(c->pool, (size_t)nitems + 1, &offs));
-    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nitems + 1), &tmp));
-    OKM_TRY(pool_get(c->pool, 2, &flags));
-    unsigned long long *bounds;
-    OKM_TRY(pool_get(c->pool, std::max<size_t>((size_t)nitems * R, 1), &bounds));
+    OKM_TRY(pool_get(*c->pool, parts.size(), &d_parts));
+    OKM_TRY(pool_get(*c->pool, rbins.size(), &d_rbins));
+    OKM_TRY(pool_get(*c->pool, (size_t)nitems * R, &d_segs));
+    OKM_TRY(pool_get(*c->pool, nitems, &d_items));
+    OKM_TRY(pool_get(*c->pool, (size_t)nitems + 1, &itemtot));
+    OKM_TRY(pool_get(*c->pool, (size_t)nitems + 1, &offs));
+    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nitems + 1), &tmp));
+    OKM_TRY(pool_get(*c->pool, 2, &flags));
+    unsigned long long *bounds, *part_max;
+    OKM_TRY(pool_get(*c->pool, std::max<size_t>((size_t)nitems * R, 1), &bounds));
+    OKM_TRY(pool_get(*c->pool, parts.size(), &part_max));
     for (void *p : {(void *)d_parts, (void *)d_rbins, (void *)itemtot, (void *)offs, (void *)tmp, (void *)flags,
-                    (void *)bounds})
+                    (void *)bounds, (void *)part_max})
         bufs.push_back(p);
     OKM_TRY(h2d(c, d_parts, parts.data(), parts.size() * sizeof(DevSortedPart)));
     OKM_TRY(h2d(c, d_rbins, rbins.data(), rbins.size() * sizeof(DevSeg)));
     HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(part_max, 0, parts.size() * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(itemtot + nitems, 0, sizeof(unsigned long long), c->stream));
     c->timer.begin(c->stream);
     launch_sorted_items(c->stream, d_parts, (uint32_t)parts.size(), nitems, d_rbins, R, c->shift1, d_items, d_segs,
-                        itemtot, item_max, capbits, flags, c->wide, bounds);
+                        itemtot, item_max, capbits, flags, c->wide, bounds, part_max);
     launch_exclusive_scan(c->stream, itemtot, offs, (uint64_t)nitems + 1, tmp);
     launch_set_out_off(c->stream, d_items, nitems, offs);
     c->timer.end(c->stream, "sorted_items", 0.0);
     HIP_TRY(hipGetLastError());
     unsigned long long hf[2];
     HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
+    std::vector<unsigned long long> pmax(parts.size());
+    HIP_TRY(hipMemcpyAsync(pmax.data(), part_max, pmax.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
     OKM_TRY(sync(c));
     if (hf[0]) {
+        // only the parts with a child above one item split further: by the
+        // bits that bring their largest child below the target
+        for (size_t p = 0; p < parts.size(); ++p) {
+            if (pmax[p] <= item_max) continue;
+            uint32_t more = 1;
+            while (more < 8 && (pmax[p] >> more) > target) ++more;
+            add_bits[parts[p].bin] += more;
+        }
         if (c->hprof.on) {
             uint64_t maxlen = 0, maxbits = 0;
             for (auto &p : parts) maxbits = std::max<uint64_t>(maxbits, p.bits);
@@ -2007,18 +2036,18 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, uint32_t extra) 
                 for (auto &r : c->runs) len += r.len(b);
                 maxlen = std::max(maxlen, len);
             }
-            fprintf(stderr, "[okm sorted] extra %u: %llu children too big (max %llu); %u runs, %zu parts, %u items, "
+            fprintf(stderr, "[okm sorted] %llu children too big (max %llu); %u runs, %zu parts, %u items, "
                             "largest part %llu, max bits %llu\n",
-                    extra, (unsigned long long)hf[0], (unsigned long long)hf[1], R, parts.size(), nitems,
+                    (unsigned long long)hf[0], (unsigned long long)hf[1], R, parts.size(), nitems,
                     (unsigned long long)maxlen, (unsigned long long)maxbits);
             for (auto &r : c->runs)
                 fprintf(stderr, "[okm sorted]   run n=%llu sorted=%d folded=%d borrowed=%d off.back=%llu\n",
                         (unsigned long long)r.n, r.sorted, r.folded, r.borrowed,
                         (unsigned long long)(r.off.empty() ? 0 : r.off.back()));
         }
-        for (void *p : bufs) c->pool.put(p);
-        c->pool.put(d_segs);
-        c->pool.put(d_items);
+        for (void *p : bufs) c->pool->put(p);
+        c->pool->put(d_segs);
+        c->pool->put(d_items);
         *fallback = true;
         return OKM_OK;
     }
@@ -2154,8 +2183,8 @@ static okm_status do_count_runs(okm_ctx *c) {
         // holds): it already is the result — copied, since it may be borrowed
         Run &r = c->runs[0];
         const uint64_t n = r.n;
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1) * c->kw, &c->res_keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(n, 1), &c->res_counts));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(n, 1) * c->kw, &c->res_keys));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(n, 1), &c->res_counts));
         c->timer.begin(c->stream);
         if (n) {
             HIP_TRY(hipMemcpyAsync(c->res_keys, r.keys, n * c->kw * sizeof(uint64_t), hipMemcpyDeviceToDevice,
@@ -2225,8 +2254,8 @@ static okm_status count_spilled(okm_ctx *c) {
             if (r.host) host_pairs += r.off[b1] - r.off[b0];
         uint64_t *uk = nullptr, *uc = nullptr;
         if (host_pairs) {
-            st = pool_get(c->pool, host_pairs * kw, &uk);
-            if (st == OKM_OK && weighted) st = pool_get(c->pool, host_pairs, &uc);
+            st = pool_get(*c->pool, host_pairs * kw, &uk);
+            if (st == OKM_OK && weighted) st = pool_get(*c->pool, host_pairs, &uc);
         }
         std::vector<Run> grp;
         uint64_t at = 0;
@@ -2286,8 +2315,8 @@ static okm_status count_spilled(okm_ctx *c) {
             }
             invalidate_result(c);
         }
-        c->pool.put(uk);
-        c->pool.put(uc);
+        c->pool->put(uk);
+        c->pool->put(uc);
         ++groups;
         b0 = b1;
     }
@@ -2297,8 +2326,8 @@ static okm_status count_spilled(okm_ctx *c) {
     // the result: on the device when it fits beside what is left, else on the host
     const uint64_t nd = hc.size();
     if ((double)nd * (8.0 * kw + 8.0) <= 0.8 * device_room(c)) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * kw, &c->res_keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1) * kw, &c->res_keys));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         if (nd) {
             HIP_TRY(hipMemcpyAsync(c->res_keys, hk.data(), nd * 8 * kw, hipMemcpyHostToDevice, c->stream));
             HIP_TRY(hipMemcpyAsync(c->res_counts, hc.data(), nd * 8, hipMemcpyHostToDevice, c->stream));
@@ -2450,7 +2479,7 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
             for (int attempt = 0;; ++attempt) {
                 unsigned long long *flags;  // [0] children too big, [1] 1: slot overflow | 2: 64-bit counts, [2] max,
                                             // [3] / [4] fan-out jobs (small / large)
-                OKM_TRY(pool_get(c->pool, 5, &flags));
+                OKM_TRY(pool_get(*c->pool, 5, &flags));
                 level_bufs.push_back(flags);
                 HIP_TRY(hipMemsetAsync(flags, 0, 5 * sizeof(unsigned long long), c->stream));
                 Level L;
@@ -2460,22 +2489,22 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 for (uint32_t i = 0; i < parts.size(); ++i)
                     par[i] = DevParent{L.out_base[i], twok - parts[i].consumed - bits[i]};
                 DevParent *d_par;
-                OKM_TRY(pool_get(c->pool, par.size(), &d_par));
+                OKM_TRY(pool_get(*c->pool, par.size(), &d_par));
                 const uint32_t nslots = L.nout << fan.bits;
                 const unsigned long long *d_nitems = nullptr;  // fan-out: items kept, on the device
-                OKM_TRY(pool_get(c->pool, nslots, &d_items));
-                OKM_TRY(pool_get(c->pool, nslots, &d_segs));
+                OKM_TRY(pool_get(*c->pool, nslots, &d_items));
+                OKM_TRY(pool_get(*c->pool, nslots, &d_segs));
                 level_bufs.push_back(d_par);
                 if (fan.bits) {
-                    OKM_TRY(pool_get(c->pool, L.nout, &fan.jobs));
+                    OKM_TRY(pool_get(*c->pool, L.nout, &fan.jobs));
                     level_bufs.push_back(fan.jobs);
                 }
                 OKM_TRY(h2d(c, d_par, par.data(), par.size() * sizeof(DevParent)));
                 // items stage their runs densely: slots = the pass's keys, not the
                 // level's sampled capacity (~1.5x the keys at C2)
                 unsigned long long *doff, *dtmp;
-                OKM_TRY(pool_get(c->pool, (size_t)L.nout + 1, &doff));
-                OKM_TRY(pool_get(c->pool, scan_tmp_elems(L.nout + 1), &dtmp));
+                OKM_TRY(pool_get(*c->pool, (size_t)L.nout + 1, &doff));
+                OKM_TRY(pool_get(*c->pool, scan_tmp_elems(L.nout + 1), &dtmp));
                 level_bufs.push_back(doff);
                 level_bufs.push_back(dtmp);
                 launch_child_offsets(c->stream, L.d_offs, L.d_ends, L.nout, doff, dtmp);
@@ -2485,11 +2514,11 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                 if (fan.bits) {  // oversized children split into a second level array (same offsets), or in place
                     uint64_t *fk = L.lk, *fc = nullptr;
                     if (!fan_in_place) {
-                        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &fk));
+                        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(L.padded, 1) * c->kw, &fk));
                         level_bufs.push_back(fk);
                     }
                     if (L.lc) {
-                        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(L.padded, 1), &fc));
+                        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(L.padded, 1), &fc));
                         level_bufs.push_back(fc);
                     }
                     c->timer.begin(c->stream);
@@ -2500,10 +2529,10 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                     // drop the empty slots, so the count kernels deal real items only
                     DevItem *dense_items;
                     unsigned long long *iflags, *ipos, *itmp;
-                    OKM_TRY(pool_get(c->pool, nslots, &dense_items));
-                    OKM_TRY(pool_get(c->pool, (size_t)nslots + 1, &iflags));
-                    OKM_TRY(pool_get(c->pool, (size_t)nslots + 1, &ipos));
-                    OKM_TRY(pool_get(c->pool, scan_tmp_elems(nslots + 1), &itmp));
+                    OKM_TRY(pool_get(*c->pool, nslots, &dense_items));
+                    OKM_TRY(pool_get(*c->pool, (size_t)nslots + 1, &iflags));
+                    OKM_TRY(pool_get(*c->pool, (size_t)nslots + 1, &ipos));
+                    OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nslots + 1), &itmp));
                     for (void *p : {(void *)d_items, (void *)iflags, (void *)ipos, (void *)itmp}) level_bufs.push_back(p);
                     launch_item_compact(c->stream, d_items, nslots, dense_items, iflags, ipos, itmp);
                     HIP_TRY(hipGetLastError());
@@ -2523,8 +2552,8 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
                     c->info.max_partition = hf[2];
                     return OKM_OK;
                 }
-                c->pool.put(d_items);
-                c->pool.put(d_segs);
+                c->pool->put(d_items);
+                c->pool->put(d_segs);
                 d_items = nullptr;
                 d_segs = nullptr;
                 if (hf[1] & 1) {  // a child outgrew its sampled slot: redo the pass exactly
@@ -2576,14 +2605,14 @@ static okm_status count_parts(okm_ctx *c, std::vector<DevSeg> &segtab, std::vect
     }
     c->info.work_items = nitems;
     if (nitems == 0) {
-        for (void *p : level_bufs) c->pool.put(p);
+        for (void *p : level_bufs) c->pool->put(p);
         c->counted = true;
         c->n_res = 0;
         c->info.distinct = 0;
         return OKM_OK;
     }
-    OKM_TRY(pool_get(c->pool, segtab.size(), &d_segs));
-    OKM_TRY(pool_get(c->pool, nitems, &d_items));
+    OKM_TRY(pool_get(*c->pool, segtab.size(), &d_segs));
+    OKM_TRY(pool_get(*c->pool, nitems, &d_items));
     OKM_TRY(h2d(c, d_segs, segtab.data(), segtab.size() * sizeof(DevSeg)));
     OKM_TRY(h2d(c, d_items, items.data(), nitems * sizeof(DevItem)));
     c->hprof.mark("items.build");
@@ -2682,17 +2711,17 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         bool armed = true;
         ~Guard() {
             if (!armed) return;
-            c->pool.put(d->keys);
-            c->pool.put(d->counts);
+            c->pool->put(d->keys);
+            c->pool->put(d->counts);
             for (auto &t : *tabs) {
-                c->pool.put(t.keys);
-                c->pool.put(t.counts);
+                c->pool->put(t.keys);
+                c->pool->put(t.counts);
             }
         }
     } guard{c, &d, &tabs};
     if (mode == 1) {
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(total, 1), &d.counts));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(total, 1), &d.counts));
     }
     const okm_engine_info info0 = c->info;
     okm_engine_info agg = info0;
@@ -2719,7 +2748,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         unsigned long long *p = nullptr, *d_base = nullptr;
         ~Slots() {
             host_pinned_free(p);
-            c->pool.put(d_base);
+            c->pool->put(d_base);
         }
     } slots{c};
     unsigned long long *&d_base = slots.d_base;
@@ -2727,7 +2756,7 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     bool pipelined = mode == 1 && G > 1;
     if (pipelined) {
         slots.p = static_cast<unsigned long long *>(host_pinned_alloc(G * 8 * sizeof(unsigned long long)));
-        pipelined = slots.p && pool_get(c->pool, 1, &d_base) == OKM_OK;
+        pipelined = slots.p && pool_get(*c->pool, 1, &d_base) == OKM_OK;
         if (pipelined) HIP_TRY(hipMemsetAsync(d_base, 0, sizeof(unsigned long long), c->stream));
     }
     for (int pass = 0; pass < 2; ++pass) {
@@ -2789,8 +2818,8 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     } else {
         nd = 0;
         for (auto &t : tabs) nd += t.n;
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
-        OKM_TRY(pool_get(c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1) * c->kw, &c->res_keys));
+        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(nd, 1), &c->res_counts));
         uint64_t o = 0;
         for (auto &t : tabs) {
             if (t.n) {
@@ -2859,6 +2888,54 @@ static okm_status l1_batch_or_spill(okm_ctx *c, const uint8_t *d_seq, uint64_t n
 }
 
 namespace okm {
+// okm_merge_owned at one rank: the owner's key range is the whole key space
+// and its only slice the local table, so the owner takes that table as it
+// stands (dense, or still the items' sorted runs) instead of copying it
+// (do_count_runs' copy of a single borrowed sorted run).  The two contexts
+// swap their device pools -- one device, and every pool is one arena of
+// that device -- so the table stays where it is and is later returned to
+// the pool that holds it; the local context is left reset (its input runs
+// are released first); *adopted says whether it happened.
+okm_status adopt_result(okm_ctx *owner, okm_ctx *local, bool *adopted) {
+    *adopted = false;
+    if (owner == local || owner->device != local->device || owner->k != local->k || owner->mode != local->mode ||
+        owner->wide != local->wide)
+        return OKM_OK;
+    HIP_TRY(hipSetDevice(local->device));
+    OKM_TRY(do_count(local));
+    if (local->input_lost) return OKM_OK;
+    OKM_TRY(okm_reset(owner));  // (synchronises the owner's stream)
+    OKM_TRY(sync(local));
+    // the counted input is no longer needed (the local is left reset, and no
+    // result ever points into a run: a folded table that became the result
+    // left the run list): its memory goes back before the pools swap
+    release_runs(local, local->runs);
+    std::swap(owner->pool, local->pool);
+    owner->pend = std::move(local->pend);
+    local->pend = okm_ctx::Pending{};
+    owner->res_keys = local->res_keys;
+    owner->res_counts = local->res_counts;
+    owner->res_host = local->res_host;
+    owner->n_res = local->n_res;
+    owner->counted = true;
+    owner->res_is_input = true;  // the table stands for the owner's input (kept on its next add)
+    owner->info = local->info;
+    if (local->res_host) {
+        const uint64_t b = local->n_res * (8 * local->kw + 8);
+        owner->host_bytes += b;
+        local->host_bytes -= std::min(local->host_bytes, b);
+    }
+    local->res_keys = local->res_counts = nullptr;
+    local->res_host = false;
+    local->n_res = 0;
+    local->counted = false;
+    local->res_is_input = false;
+    OKM_TRY(okm_reset(local));
+    owner->hprof.mark("adopt_result");
+    *adopted = true;
+    return OKM_OK;
+}
+
 okm_status result_view(okm_ctx *c, const uint64_t **keys, const uint64_t **counts, uint64_t *n, bool *on_host) {
     OKM_TRY(okm_count(c, nullptr));
     OKM_TRY(ensure_dense(c));
@@ -2962,7 +3039,7 @@ okm_status okm_create(okm_ctx **out, uint8_t k, okm_mode mode, int device, uint6
         delete c;
         return fail(OKM_E_DEVICE, "okm_create: stream/alloc failed");
     }
-    c->pool.attach(device);
+    c->pool->attach(device);
     *out = c;
     return OKM_OK;
 }
@@ -2974,8 +3051,8 @@ void okm_destroy(okm_ctx *c) {
     c->timer.destroy();
     invalidate_result(c);  // host tables are freed here; device memory goes with the arena
     release_runs(c, c->runs);
-    c->pool.detach();
-    c->pool.release_all();
+    c->pool->detach();
+    c->pool->release_all();
     if (c->HC) (void)hipFree(c->HC);
     if (c->Hg) (void)hipFree(c->Hg);
     if (c->cursor) (void)hipFree(c->cursor);
@@ -2995,7 +3072,7 @@ okm_status okm_trim(okm_ctx *c) {
     if (!c) return fail(OKM_E_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
     OKM_TRY(sync(c));
-    c->pool.trim();
+    c->pool->trim();
     return OKM_OK;
 }
 
@@ -3008,7 +3085,7 @@ okm_status okm_reset(okm_ctx *c) {
     c->info = okm_engine_info{};
     c->spills = 0;
     c->folds = 0;
-    c->pool.reset_peak();
+    c->pool->reset_peak();
     c->input_lost = false;
     c->hprof.mark("reset");
     return OKM_OK;
@@ -3098,13 +3175,13 @@ okm_status okm_add_pairs(okm_ctx *c, const uint64_t *keys, const uint64_t *count
     if (!keys) return fail(OKM_E_ARG, "okm_add_pairs: null keys");
     HIP_TRY(hipSetDevice(c->device));
     uint64_t *dk = nullptr, *dc = nullptr;
-    OKM_TRY(pool_get(c->pool, n * c->kw, &dk));
-    if (counts) OKM_TRY(pool_get(c->pool, n, &dc));
+    OKM_TRY(pool_get(*c->pool, n * c->kw, &dk));
+    if (counts) OKM_TRY(pool_get(*c->pool, n, &dc));
     HIP_TRY(hipMemcpyAsync(dk, keys, n * 8 * c->kw, hipMemcpyHostToDevice, c->stream));
     if (counts) HIP_TRY(hipMemcpyAsync(dc, counts, n * 8, hipMemcpyHostToDevice, c->stream));
     okm_status s = okm_add_pairs_device(c, dk, dc, n);
-    c->pool.put(dk);
-    c->pool.put(dc);
+    c->pool->put(dk);
+    c->pool->put(dc);
     return s;
 }
 
@@ -3121,10 +3198,10 @@ static okm_status result_to_device(okm_ctx *c) {
     if (!c->res_host) return OKM_OK;
     const uint64_t n = c->n_res;
     uint64_t *dk = nullptr, *dc = nullptr;
-    okm_status st = pool_get(c->pool, std::max<uint64_t>(n, 1) * c->kw, &dk);
-    if (st == OKM_OK) st = pool_get(c->pool, std::max<uint64_t>(n, 1), &dc);
+    okm_status st = pool_get(*c->pool, std::max<uint64_t>(n, 1) * c->kw, &dk);
+    if (st == OKM_OK) st = pool_get(*c->pool, std::max<uint64_t>(n, 1), &dc);
     if (st != OKM_OK) {
-        c->pool.put(dk);
+        c->pool->put(dk);
         return fail(OKM_E_NOMEM, "the counted table (" + std::to_string(n) +
                                      " entries) lies in host memory and does not fit on the device: read it with "
                                      "okm_fetch_counts / okm_finish_counts");
@@ -3166,9 +3243,9 @@ static okm_status fetch_range(okm_ctx *c, const uint64_t *dk, const uint64_t *dc
     if (min_count > 1) {
         const uint32_t nb = filter_blocks(n);
         unsigned long long *bc, *bo, *tmp;
-        OKM_TRY(pool_get(c->pool, nb + 1, &bc));
-        OKM_TRY(pool_get(c->pool, nb + 1, &bo));
-        OKM_TRY(pool_get(c->pool, scan_tmp_elems(nb + 1), &tmp));
+        OKM_TRY(pool_get(*c->pool, nb + 1, &bc));
+        OKM_TRY(pool_get(*c->pool, nb + 1, &bo));
+        OKM_TRY(pool_get(*c->pool, scan_tmp_elems(nb + 1), &tmp));
         HIP_TRY(hipMemsetAsync(bc, 0, (nb + 1) * sizeof(unsigned long long), c->stream));
         launch_filter_count(c->stream, dc, n, min_count, bc, nb);
         launch_exclusive_scan(c->stream, bc, bo, nb + 1, tmp);
@@ -3177,16 +3254,16 @@ static okm_status fetch_range(okm_ctx *c, const uint64_t *dk, const uint64_t *dc
         OKM_TRY(sync(c));
         cnt = tot;
         if ((keys || counts) && cnt > cap) {
-            c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+            c->pool->put(bc); c->pool->put(bo); c->pool->put(tmp);
             return fail(OKM_E_OVERFLOW, "okm_fetch_counts: buffer too small");
         }
         if (cnt && (keys || counts)) {
-            OKM_TRY(pool_get(c->pool, cnt * c->kw, &tk));
-            OKM_TRY(pool_get(c->pool, cnt, &tc));
+            OKM_TRY(pool_get(*c->pool, cnt * c->kw, &tk));
+            OKM_TRY(pool_get(*c->pool, cnt, &tc));
             launch_filter_scatter(c->stream, dk, dc, n, min_count, bo, tk, tc, c->wide);
             HIP_TRY(hipGetLastError());
         }
-        c->pool.put(bc); c->pool.put(bo); c->pool.put(tmp);
+        c->pool->put(bc); c->pool->put(bo); c->pool->put(tmp);
         src_k = tk;
         src_c = tc;
     } else if ((keys || counts) && cnt > cap) {
@@ -3198,8 +3275,8 @@ static okm_status fetch_range(okm_ctx *c, const uint64_t *dk, const uint64_t *dc
         if (counts) HIP_TRY(hipMemcpyAsync(counts, src_c, cnt * 8, kind, c->stream));
         OKM_TRY(sync(c));
     }
-    if (tk) c->pool.put(tk);
-    if (tc) c->pool.put(tc);
+    if (tk) c->pool->put(tk);
+    if (tc) c->pool->put(tc);
     *m = cnt;
     return OKM_OK;
 }
@@ -3216,8 +3293,8 @@ static okm_status fetch_result(okm_ctx *c, uint64_t min_count, uint64_t *keys, u
     constexpr uint64_t kSlice = uint64_t(1) << 26;
     const uint64_t sl = std::min<uint64_t>(kSlice, c->n_res);
     uint64_t *dk = nullptr, *dc = nullptr;
-    OKM_TRY(pool_get(c->pool, sl * c->kw, &dk));
-    okm_status st = pool_get(c->pool, sl, &dc);
+    OKM_TRY(pool_get(*c->pool, sl * c->kw, &dk));
+    okm_status st = pool_get(*c->pool, sl, &dc);
     uint64_t done = 0;
     for (uint64_t o = 0; o < c->n_res && st == OKM_OK; o += sl) {
         const uint64_t len = std::min(sl, c->n_res - o);
@@ -3233,8 +3310,8 @@ static okm_status fetch_result(okm_ctx *c, uint64_t min_count, uint64_t *keys, u
                          out && counts ? counts + done : nullptr, out ? cap - done : 0, &got, dst_on_device);
         done += got;
     }
-    c->pool.put(dk);
-    c->pool.put(dc);
+    c->pool->put(dk);
+    c->pool->put(dc);
     OKM_TRY(st);
     *n = done;
     return OKM_OK;
@@ -3398,8 +3475,8 @@ okm_status okm_engine_info_get(okm_ctx *c, okm_engine_info *info) {
     if (!c || !info) return fail(OKM_E_ARG, "null argument");
     *info = c->info;
     info->folds = c->folds;
-    info->device_bytes = c->pool.held() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
-    info->device_peak_bytes = c->pool.peak() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    info->device_bytes = c->pool->held() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
+    info->device_peak_bytes = c->pool->peak() + c->HC_cap * 4 + c->Hg_cap * 16 + c->staging_cap;
     info->host_bytes = c->host_bytes;
     info->spills = c->spills;
     return OKM_OK;

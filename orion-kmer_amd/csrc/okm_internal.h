@@ -40,6 +40,9 @@ bool device_over_budget(int device, size_t bytes);
 // host memory when count_spilled left it there (okm_group_write_counts_tsv
 // streams either without moving it).
 okm_status result_view(okm_ctx *c, const uint64_t **keys, const uint64_t **counts, uint64_t *n, bool *on_host);
+// okm_merge_owned at one rank: the owner takes the local context's table
+// without a copy (the two swap device pools); the local is left reset.
+okm_status adopt_result(okm_ctx *owner, okm_ctx *local, bool *adopted);
 
 // Context accessors for the other translation units (okm_probe.hip).
 int ctx_device(const okm_ctx *c);
@@ -257,11 +260,12 @@ struct DevSortedPart {
 // One multi-segment item per child (bounds: nitems * nruns words of scratch):
 // segs[i * nruns + r] = the child's key range
 // in run r (rbins[slot * nruns + r] = the part's range in run r); itemtot[i]
-// = its instances; flags[0] += children still too big, flags[1] = max.
+// = its instances; flags[0] += children still too big, flags[1] = max;
+// part_max[slot] = the part's largest child (per-part replanning).
 void launch_sorted_items(void *stream, const DevSortedPart *parts, uint32_t nparts, uint32_t nitems,
                          const DevSeg *rbins, uint32_t nruns, uint32_t shift1, DevItem *items, DevSeg *segs,
                          unsigned long long *itemtot, uint64_t item_max, uint32_t capbits, unsigned long long *flags,
-                         bool wide, unsigned long long *bounds);
+                         bool wide, unsigned long long *bounds, unsigned long long *part_max);
 void launch_set_out_off(void *stream, DevItem *items, uint32_t nitems, const unsigned long long *off);
 
 // Gather the per-item results into dense arrays given exclusive offsets

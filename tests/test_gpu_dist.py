@@ -56,22 +56,30 @@ def test_merge_owned_single_rank_equals_local(comm1, genome):
     buf.upload(b)
     with okm.KmerCounter(k) as local, okm.KmerCounter(k) as owner:
         local.add_device_batch(buf.address, len(b))
+        lk, lc = local.result(1)  # the local table before the merge
         n = comm1.merge_owned(local, owner)
         gk, gc = owner.result(1)
-        lk, lc = local.result(1)
         t = comm1.last_times()
-        # again: the communicator's buffers are reused, the owner is reset
+        # one rank: the local's table was handed to the owner (okm_engine.hip
+        # adopt_result: no copy) and the local left reset
+        assert local.count() == 0
+        # again, after a new count: the owner is reset, the local's pool swapped back
+        local.add_device_batch(buf.address, len(b))
         assert comm1.merge_owned(local, owner) == n
         g2k, g2c = owner.result(1)
+        # the owner keeps its table as input: one more add merges into it (count.rs:48)
+        owner.add_device_batch(buf.address, len(b))
+        o3k, o3c = owner.result(1)
     buf.free()
     assert n == len(ek)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
     assert np.array_equal(lk, ek) and np.array_equal(lc, ec)
     assert np.array_equal(g2k, ek) and np.array_equal(g2c, ec)
+    assert np.array_equal(o3k, ek) and np.array_equal(o3c, 2 * ec)
     assert t["plan_ms"] >= 0 and t["exchange_ms"] >= 0 and t["merge_ms"] >= 0
 
 
-@pytest.mark.parametrize("piece", [4096, 1 << 20])
+@pytest.mark.parametrize("piece", [4096])  # (1 MiB pieces dropped in round 6: 4 KiB covers more pieces)
 def test_merge_owned_rccl_multi_piece(comm1, monkeypatch, piece):
     """Real RCCL at one rank with every message cut into many pieces
     (test knob piece_bytes): keys, count bytes and escapes of the self slice."""
@@ -124,8 +132,9 @@ def test_comm_init_all_one_device():
     (c,) = okm.Comm.init_all([0])
     with okm.KmerCounter(15) as local, okm.KmerCounter(15) as owner:
         local.add_records([b"ACGTTGCAACGTAGCTAGCTAGGATCGA" * 10])
+        nl = local.count()
         n = c.merge_owned(local, owner)
-        assert n == local.count()
+        assert n == nl == owner.count()  # (one rank: the local's table moved to the owner)
     c.close()
 
 
@@ -154,15 +163,18 @@ def test_merge_owned_wide_rccl(comm1, monkeypatch, piece):
     assert (ec > 255).any()
     buf = okm.DeviceBuffer(len(b))
     buf.upload(b)
-    with okm.KmerCounter(k, wide=True) as local, okm.KmerCounter(k, wide=True) as owner:
-        local.add_device_batch(buf.address, len(b))
-        n = comm1.merge_owned(local, owner)
-        gk, gc = owner.result(1)
+    # owner == local: the table goes through an RCCL self send/recv (K128 word
+    # pairs, cut into pieces by the knob) -- a separate owner would take it
+    # as it stands at one rank (adopt_result)
+    with okm.KmerCounter(k, wide=True) as ctx:
+        ctx.add_device_batch(buf.address, len(b))
+        n = comm1.merge_owned(ctx, ctx)
+        gk, gc = ctx.result(1)
         sent, recv = comm1.last_bytes()
     buf.free()
     assert n == len(ec)
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
-    assert sent == recv == 0  # one rank: the self slice is borrowed, nothing crosses a link
+    assert sent == recv == 0  # one rank: only the self slice, nothing crosses a link
 
 
 def test_merge_owned_into_local_context(comm1):

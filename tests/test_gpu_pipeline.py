@@ -85,7 +85,7 @@ class _Counting:
         return self.comm.last_times()
 
 
-@pytest.mark.parametrize("P,workers", [(2, 1), (8, 1), (2, 2), (3, 3)])
+@pytest.mark.parametrize("P,workers", [(2, 1), (8, 1), (3, 3)])  # ((2, 2) dropped in round 6: (3, 3) covers several workers)
 def test_owned_count_pipeline_loopback_exact(P, workers):
     nsteps, rpr = 4, 40_000
     batches = [[_step_batch(i, r, P, rpr) for i in range(nsteps)] for r in range(P)]
