@@ -459,44 +459,6 @@ __device__ __forceinline__ uint64_t lower_bound_bin(const KT *keys, uint64_t lo,
     return lo;
 }
 
-// lower_bound_bin over [0, n), searched outward from a guess g (galloping):
-// a child's start in a run is near len * c / 2^bits when the keys are spread
-// evenly over the part, so a few probes find it instead of ~log2(n) dependent
-// loads from the whole range's midpoints.
-template <typename KT>
-__device__ __forceinline__ uint64_t lower_bound_bin_from(const KT *keys, uint64_t n, uint32_t shift, uint64_t base,
-                                                         uint64_t target, uint64_t g) {
-    if (n == 0) return 0;
-    auto below = [&](uint64_t j) {
-        return (shift >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(keys[j], shift)) - base < target;
-    };
-    if (g >= n) g = n - 1;
-    uint64_t lo, hi;  // the answer lies in [lo, hi]
-    if (below(g)) {
-        lo = g + 1;
-        uint64_t step = 1, p = g + 1;
-        while (p < n && below(p)) {
-            lo = p + 1;
-            step <<= 1;
-            p = g + step;
-        }
-        hi = p < n ? p : n;
-    } else {
-        hi = g;
-        uint64_t step = 1;
-        bool more = g >= 1;
-        uint64_t p = more ? g - 1 : 0;
-        while (more && !below(p)) {
-            hi = p;
-            step <<= 1;
-            more = g >= step;
-            p = more ? g - step : 0;
-        }
-        lo = more ? p + 1 : 0;
-    }
-    return lower_bound_bin(keys, lo, hi, shift, base, target);
-}
-
 template <typename KT>
 __global__ void k_bin_bounds(const KT *__restrict__ keys, uint64_t n, uint32_t shift, uint32_t nbins,
                              ull *__restrict__ out) {
@@ -542,8 +504,8 @@ __global__ void k_sorted_bounds(const DevSortedPart *__restrict__ parts, uint32_
     const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
     const uint32_t c = i - P.item_base;
     const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
-    bounds[x] = P.bits && c ? lower_bound_bin_from(reinterpret_cast<const KT *>(rb.keys), rb.len, shift1 - P.bits,
-                                                   (uint64_t)P.bin << P.bits, c, (rb.len * c) >> P.bits)
+    bounds[x] = P.bits && c ? lower_bound_bin(reinterpret_cast<const KT *>(rb.keys), 0, rb.len, shift1 - P.bits,
+                                              (uint64_t)P.bin << P.bits, c)
                             : 0;
 }
 
