@@ -70,4 +70,23 @@ __device__ __forceinline__ ull block_excl_scan(ull v, ull *wsum, ull *total) {
     return wbase + inc - v;
 }
 
+// block_excl_scan without the trailing barrier: for callers whose next
+// write to wsum is separated from this scan's reads by a later barrier anyway.
+template <int BLOCK>
+__device__ __forceinline__ ull block_excl_scan_1b(ull v, ull *wsum, ull *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const ull inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = inc;
+    lds_sync();
+    ull wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        const ull s = wsum[w];
+        if (w < wid) wbase += s;
+        tot += s;
+    }
+    *total = tot;
+    return wbase + inc - v;
+}
+
 }  // namespace okm

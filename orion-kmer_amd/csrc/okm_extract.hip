@@ -129,7 +129,6 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(kSca
     __shared__ ull gcur[kMaxL1Bins];         // this block's next output index per bin
     __shared__ uint32_t hist[kMaxL1Bins + 1];
     __shared__ uint32_t lofs[kMaxL1Bins];    // tile-local start of each bin in `stage`
-    __shared__ uint32_t lcur[kMaxL1Bins];
     __shared__ ull wsum[kScatBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t nb = g.nbins;
@@ -148,12 +147,17 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(kSca
     WinWords<kSegS> ww;
     load_windows_clamped<kSegS>(seq, g.n, beg + (uint64_t)t * kSegS, ww);
     const ull capb = (!HC && t < nb) ? cap_end[t] : 0ull;
+    // five barriers per tile instead of seven: each thread clears its own bin's
+    // counter once it has read it (the next tile's atomics are barriers away),
+    // and the offsets scan needs no trailing barrier (its slots are next
+    // written in the next tile)
+    for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
+    lds_sync();
     for (uint64_t t0 = beg; t0 < end; t0 += kTile) {
-        for (uint32_t b = t; b <= nb; b += kScatBlock) hist[b] = 0;
         const uint64_t w0 = t0 + (uint64_t)t * kSegS;
-        lds_sync();
         const bool live = w0 < end;
         uint32_t tile_n;
+        uint32_t hmine;
         {  // one sweep: keys and their within-bin ranks stay in registers
             ull kk[kSegS];
             uint32_t rk[kSegS / 2];  // two within-bin ranks (< 2^15) per word; the bin is recomputed
@@ -171,12 +175,19 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(kSca
             // end is harmless), so the loaded registers need no merge copies
             load_windows_clamped<kSegS>(seq, g.n, w0 + kTile, ww);
             lds_sync();
-            tile_n = tile_offsets<kScatBlock>(t, nb, hist, lofs, lcur, wsum);
+            hmine = t <= nb ? hist[t] : 0u;
+            if (t <= nb) hist[t] = 0;
+            {
+                ull tn;
+                const uint32_t off = (uint32_t)block_excl_scan_1b<kScatBlock>(t < nb ? hmine : 0u, wsum, &tn);
+                if (t < nb) lofs[t] = off;
+                tile_n = (uint32_t)tn;
+            }
             // sampled capacities: issue this tile's claim now, consume it after the staging
             uint32_t ch = 0;
             ull cp;
             if (!HC && t < nb) {
-                ch = hist[t];
+                ch = hmine;
                 cp = atomicAdd(&cursor[t * kL1CurStride], (ull)ch);  // + 0 when empty: no branch
             }
             lds_sync();
@@ -201,7 +212,7 @@ __global__ __launch_bounds__(kScatBlock) __attribute__((amdgpu_waves_per_eu(kSca
             if (gb != ~0ull) out[gb + (j - lofs[b])] = key;
         }
         lds_sync();
-        if (HC && t < nb) gcur[t] += hist[t];
+        if (HC && t < nb) gcur[t] += hmine;
     }
 }
 
