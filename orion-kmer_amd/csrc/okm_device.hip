@@ -492,8 +492,55 @@ __device__ __forceinline__ uint32_t sorted_part_of(const DevSortedPart *__restri
 }
 
 // bounds[i * nruns + r] = where item i's key range starts in run r: one
-// thread per (item, run), so the binary searches over the runs run side by
-// side instead of 2 x nruns of them back to back in one thread per item.
+// thread per (item, run), so the searches over the runs run side by side
+// instead of 2 x nruns of them back to back in one thread per item.  Each
+// search interpolates first: a part's keys are spread smoothly over its key
+// range (canonical-key density varies linearly, not in steps), so two
+// interpolation probes leave a window of ~sqrt(sqrt(n)) keys, where a plain
+// binary search over a 200 K-key slice takes ~18 dependent loads.  After
+// kInterp probes, or once the window is small, bisection finishes (exact
+// whatever the distribution).
+template <typename KT>
+__device__ __forceinline__ uint64_t lower_bound_interp(const KT *keys, uint64_t n, uint32_t shift, uint64_t base,
+                                                       uint64_t target) {
+    constexpr int kInterp = 3;
+    // f(j) = (key_j >> shift) - base >= target; v(j): the key's top bits as a
+    // double (interpolation only: approximate is fine)
+    // (only a guess: f decides, so a key whose top bits do not fit 64 bits
+    // costs probes, never the answer)
+    const uint32_t vs = shift > 20 ? shift - 20 : 0;  // 20 bits below the child index
+    auto v = [&](const KT &k) -> double {
+        return (double)(vs >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(k, vs));
+    };
+    auto f = [&](const KT &k) -> bool {
+        return (shift >= (uint32_t)KeyOps<KT>::kBits ? 0ull : KeyOps<KT>::shr(k, shift)) - base >= target;
+    };
+    uint64_t lo = 0, hi = n;  // answer in [lo, hi]
+    if (n == 0) return 0;
+    const KT k0 = keys[0], k1 = keys[n - 1];
+    if (f(k0)) return 0;
+    if (!f(k1)) return n;
+    // invariants: f(lo) false, f(hi) true; answer in (lo, hi]
+    hi = n - 1;
+    double vlo = v(k0), vhi = v(k1);
+    const double vt = (double)(base + target) * (double)(1ull << (shift - vs));
+#pragma unroll 1
+    for (int it = 0; it < kInterp && hi - lo > 64; ++it) {
+        double fr = vhi > vlo ? (vt - vlo) / (vhi - vlo) : 0.5;
+        fr = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
+        uint64_t m = lo + 1 + (uint64_t)(fr * (double)(hi - lo - 1));
+        if (m >= hi) m = hi - 1;
+        const KT km = keys[m];
+        if (f(km)) { hi = m; vhi = v(km); } else { lo = m; vlo = v(km); }
+    }
+    ++lo;  // answer in [lo, hi]: first true
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (f(keys[mid])) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
 template <typename KT>
 __global__ void k_sorted_bounds(const DevSortedPart *__restrict__ parts, uint32_t nparts, uint32_t nitems,
                                 const DevSeg *__restrict__ rbins, uint32_t nruns, uint32_t shift1,
@@ -504,8 +551,8 @@ __global__ void k_sorted_bounds(const DevSortedPart *__restrict__ parts, uint32_
     const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
     const uint32_t c = i - P.item_base;
     const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
-    bounds[x] = P.bits && c ? lower_bound_bin(reinterpret_cast<const KT *>(rb.keys), 0, rb.len, shift1 - P.bits,
-                                              (uint64_t)P.bin << P.bits, c)
+    bounds[x] = P.bits && c ? lower_bound_interp(reinterpret_cast<const KT *>(rb.keys), rb.len, shift1 - P.bits,
+                                                 (uint64_t)P.bin << P.bits, c)
                             : 0;
 }
 
@@ -516,42 +563,63 @@ __global__ void k_sorted_items(const DevSortedPart *__restrict__ parts, uint32_t
                                uint64_t item_max, uint32_t capbits, ull *__restrict__ flags,
                                const ull *__restrict__ bounds, ull *__restrict__ part_max) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nitems) return;
-    const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
-    const uint32_t c = i - P.item_base;
-    const uint32_t shift = shift1 - P.bits;                 // child = next `bits` key bits
-    const bool last = !P.bits || c + 1 == (1u << P.bits);  // the part's last child ends where its range does
+    // no early exit: the wave reductions at the end need every lane
+    const bool live = i < nitems;
     ull tot = 0;
-    for (uint32_t r = 0; r < nruns; ++r) {
-        const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
-        const uint64_t s0 = bounds[(uint64_t)i * nruns + r];
-        const uint64_t s1 = last ? rb.len : bounds[(uint64_t)(i + 1) * nruns + r];
-        DevSeg sg;
-        sg.keys = rb.keys + s0 * kw;
-        sg.counts = rb.counts ? rb.counts + s0 : nullptr;
-        sg.len = s1 - s0;
-        sg.key_base = 0;
-        sg.out_base = 0;
-        sg.shift = kSingleBin;
-        sg.nlocal = 1;
-        sg.pad = 0;
-        segs[(uint64_t)i * nruns + r] = sg;
-        tot += s1 - s0;
+    uint32_t slot = ~0u;
+    if (live) {
+        const DevSortedPart P = parts[sorted_part_of(parts, nparts, i)];
+        slot = P.slot;
+        const uint32_t c = i - P.item_base;
+        const uint32_t shift = shift1 - P.bits;                 // child = next `bits` key bits
+        const bool last = !P.bits || c + 1 == (1u << P.bits);  // the part's last child ends where its range does
+        for (uint32_t r = 0; r < nruns; ++r) {
+            const DevSeg rb = rbins[(uint64_t)P.slot * nruns + r];
+            const uint64_t s0 = bounds[(uint64_t)i * nruns + r];
+            const uint64_t s1 = last ? rb.len : bounds[(uint64_t)(i + 1) * nruns + r];
+            DevSeg sg;
+            sg.keys = rb.keys + s0 * kw;
+            sg.counts = rb.counts ? rb.counts + s0 : nullptr;
+            sg.len = s1 - s0;
+            sg.key_base = 0;
+            sg.out_base = 0;
+            sg.shift = kSingleBin;
+            sg.nlocal = 1;
+            sg.pad = 0;
+            segs[(uint64_t)i * nruns + r] = sg;
+            tot += s1 - s0;
+        }
+        DevItem it;
+        it.seg_begin = i * nruns;
+        it.seg_count = nruns;
+        it.out_off = 0;  // set from the scan of itemtot (k_set_out_off)
+        it.rem_bits = shift;
+        it.pad = 0;
+        it.total = tot;
+        it.keys0 = segs[(uint64_t)i * nruns].keys;
+        it.counts0 = segs[(uint64_t)i * nruns].counts;
+        items[i] = it;
+        itemtot[i] = tot;
+        if (tot > item_max && shift > capbits) atomicAdd(&flags[0], 1ull);
     }
-    DevItem it;
-    it.seg_begin = i * nruns;
-    it.seg_count = nruns;
-    it.out_off = 0;  // set from the scan of itemtot (k_set_out_off)
-    it.rem_bits = shift;
-    it.pad = 0;
-    it.total = tot;
-    it.keys0 = segs[(uint64_t)i * nruns].keys;
-    it.counts0 = segs[(uint64_t)i * nruns].counts;
-    items[i] = it;
-    itemtot[i] = tot;
-    if (tot > item_max && shift > capbits) atomicAdd(&flags[0], 1ull);
-    atomicMax(&flags[1], tot);
-    atomicMax(&part_max[P.slot], tot);
+    // the maxima: one atomic per wave (per part within it), not per item --
+    // a part's thousand items on one address serialise in L2
+    ull wmax = tot;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const ull o = __shfl_xor(wmax, d, 64);
+        wmax = o > wmax ? o : wmax;
+    }
+    // items are consecutive lanes: a wave whose lane 0 has no item has none
+    const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slot);
+    if (slot0 == ~0u) return;  // wave-uniform
+    const bool one_part = __ballot(live && slot != slot0) == 0;  // wave-uniform
+    if ((threadIdx.x & 63u) == 0) atomicMax(&flags[1], wmax);
+    if (one_part) {
+        if ((threadIdx.x & 63u) == 0) atomicMax(&part_max[slot0], wmax);
+    } else if (live) {
+        atomicMax(&part_max[slot], tot);
+    }
 }
 
 __global__ void k_set_out_off(DevItem *__restrict__ items, uint32_t nitems, const ull *__restrict__ off) {
