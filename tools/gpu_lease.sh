@@ -37,14 +37,21 @@ sq_sum() {  # <json out> <csv...>
     python3 - "$out" "$@" <<'PY'
 import csv, collections, json, sys
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(set)
 for path in sys.argv[2:]:
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"].split("(")[0]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
 keep = ("extract_scatter", "part_scatter", "count_items", "compact_items", "count_direct")
-out = {k: {c: int(v) for c, v in sorted(d.items())} for k, d in sorted(agg.items()) if any(x in k for x in keep)}
-json.dump({"per_dispatch_sum_over_one_step": out}, open(sys.argv[1], "w"), indent=1)
-print(json.dumps(out, indent=1))
+ks = [k for k in sorted(agg) if any(x in k for x in keep)]
+out = {k: {c: int(v) for c, v in sorted(agg[k].items())} for k in ks}
+# the bench command counts a warm-up batch and the step: the sums cover every
+# dispatch of the kernel; `per_dispatch` divides by their number
+per = {k: {c: int(v / max(len(disp[k]), 1)) for c, v in sorted(agg[k].items())} for k in ks}
+json.dump({"sum_over_all_dispatches": out, "dispatches": {k: len(disp[k]) for k in ks}, "per_dispatch": per},
+          open(sys.argv[1], "w"), indent=1)
+print(json.dumps(per, indent=1))
 PY
 }
 
