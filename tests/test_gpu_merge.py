@@ -181,3 +181,68 @@ def test_merge_counts_past_u32(wide):
     if wide:
         gk = gk.reshape(-1, 2)[:, 0]
     assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def _skewed_runs(rng, nruns, n, bits):
+    """Sorted runs whose keys are far from uniform inside an L1 bin: three
+    clusters 2^-9 of a bin wide plus a cubic density ramp (keys crowd the low
+    end).  The item bounds search interpolates before it bisects; on this data
+    the interpolation guesses are poor and the bisection must still land
+    exactly."""
+    top = np.uint64(1) << np.uint64(bits)
+    out = []
+    for r in range(nruns):
+        parts = []
+        for c in (0.1003, 0.5, 0.77):
+            centre = int(c * float(top))
+            parts.append(np.uint64(centre) + rng.integers(0, 1 << (bits - 18), n // 4, dtype=np.uint64))
+        u = rng.random(n // 4)
+        parts.append((u ** 3 * float(top)).astype(np.uint64))
+        keys = np.unique(np.concatenate(parts))
+        keys = keys[keys < top]
+        out.append((keys, rng.integers(1, 100, len(keys)).astype(np.uint64)))
+    return out
+
+
+@pytest.mark.parametrize("merge_kernel", ["", "2"])
+def test_merge_skewed_key_density(merge_kernel):
+    if merge_kernel:
+        testing.set_knob("sorted_path", int(merge_kernel))
+    rng = np.random.default_rng(23)
+    runs = _skewed_runs(rng, 8, 240_000, 62)
+    ek, ec = _expected(runs, True)
+    bufs = []
+    with okm.KmerCounter(31) as m:
+        for keys, counts in runs:
+            bk, bc = _upload(keys), _upload(counts)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(keys))
+        gk, gc = m.result(1)
+    assert np.array_equal(gk, ek) and np.array_equal(gc, ec)
+
+
+def test_merge_skewed_key_density_wide():
+    rng = np.random.default_rng(29)
+    k = 63
+    runs = []
+    for keys, counts in _skewed_runs(rng, 4, 120_000, 62):
+        # the skewed values as the top 62 bits of 126-bit keys (low word random)
+        lo = rng.integers(0, 1 << 62, len(keys), dtype=np.uint64)
+        v = (keys.astype(object) << 64) | lo.astype(object)
+        v = sorted(set(v.tolist()))
+        kk = np.array([[x & ((1 << 64) - 1), x >> 64] for x in v], dtype=np.uint64)
+        runs.append((kk, rng.integers(1, 50, len(v)).astype(np.uint64)))
+    allk = {}
+    for keys, counts in runs:
+        for (lo, hi), c in zip(keys.tolist(), counts.tolist()):
+            key = (hi << 64) | lo
+            allk[key] = allk.get(key, 0) + c
+    bufs = []
+    with okm.KmerCounter(k, wide=True) as m:
+        for keys, counts in runs:
+            bk, bc = _upload(keys.reshape(-1)), _upload(counts)
+            bufs += [bk, bc]
+            m.add_sorted_pairs_device(bk.address, bc.address, len(counts))
+        gk, gc = m.result(1)
+    assert okm.keys128_to_int(gk) == sorted(allk)
+    assert dict(zip(okm.keys128_to_int(gk), gc.tolist())) == allk
