@@ -636,6 +636,9 @@ struct okm_comm {
     DevBuf ksend;  // u64 keys sent from communicator memory (Transport::owned_send_buffers)
     ull *hpin = nullptr;  // pinned landing area for the small readbacks
     size_t hpin_cap = 0;
+    // the agreed histogram over this rank's owner range (zero elsewhere): the
+    // owner's count plans its items from it (set_sorted_hint)
+    std::vector<ull> owned_hist;
     double last_ms[4] = {0, 0, 0, 0};  // plan, exchange, unpack, merge (host wall, last okm_merge_owned)
     uint64_t last_bytes[2] = {0, 0};   // bytes sent / received by the last okm_merge_owned (excl. self)
 };
@@ -772,6 +775,11 @@ okm_status plan_split(okm_comm *m, std::vector<Table> &tabs, uint32_t nb, uint32
     for (size_t i = 0; i < nt; ++i) tabs[i].starts.assign(h_starts + i * (nb + 1), h_starts + (i + 1) * (nb + 1));
     bounds.assign(P + 1, 0);  // (h_starts stays valid: tabs[i].starts copied above)
     owner_bounds(reinterpret_cast<const uint64_t *>(h_sum), nb, (int)P, bounds.data());
+    // what this rank will own, bin by bin (h_sum is the sum over ranks of
+    // every table's pairs, so for several tables an upper bound of each)
+    m->owned_hist.assign(nb, 0);
+    const uint32_t me = (uint32_t)m->rank;
+    std::copy(h_sum + bounds[me], h_sum + bounds[me + 1], m->owned_hist.begin() + bounds[me]);
     return OKM_OK;
 }
 
@@ -1034,8 +1042,10 @@ okm_status move_and_merge(okm_comm *m, Table &t, const std::vector<uint32_t> &bo
     const double t_x = ms_since(t0);
 
     // 5. the owner counts the P sorted slices in place (key-range items); no
-    // collective from here on
+    // collective from here on.  The agreed histogram tells the owner's plan
+    // how dense each part of its range is, so its first split fits.
     OKM_TRY(okm_reset(owner));
+    if (m->owned_hist.size() == nb) set_sorted_hint(owner, m->owned_hist.data(), 31 - __builtin_clz(nb));
     for (uint32_t r = 0; r < P; ++r) {
         if (r == me && self_borrow && self_n) {
             OKM_TRY(okm_add_sorted_pairs_device(owner, dk + kw * cut[me], set ? nullptr : dc + cut[me], self_n));

@@ -447,6 +447,10 @@ struct okm_ctx {
     bool wide = false;   // k > 32: K128 keys (two u64 per key)
     uint32_t kw = 1;     // u64 words per key
 
+    // density hint for the next sorted-run count (set_sorted_hint): pairs per
+    // top-hint_bits key bin; empty = none
+    std::vector<unsigned long long> sorted_hint;
+    uint32_t sorted_hint_bits = 0;
     std::unique_ptr<DevPool> pool{new DevPool};  // heap-held: a merge at one rank hands the whole pool over (adopt_result)
     std::vector<Run> runs;
     KernelTimer timer;
@@ -522,6 +526,13 @@ namespace okm {
 int ctx_device(const okm_ctx *c) { return c->device; }
 bool ctx_is_wide(const okm_ctx *c) { return c->wide; }
 uint32_t ctx_k(const okm_ctx *c) { return c->k; }
+void set_sorted_hint(okm_ctx *c, const unsigned long long *fine, uint32_t fine_bits) {
+    c->sorted_hint.clear();
+    c->sorted_hint_bits = 0;
+    if (!fine || fine_bits > 24) return;
+    c->sorted_hint.assign(fine, fine + (size_t(1) << fine_bits));
+    c->sorted_hint_bits = fine_bits;
+}
 bool ctx_is_set(const okm_ctx *c) { return c->mode == OKM_MODE_SET; }
 
 void *host_pinned_alloc(size_t bytes) {
@@ -1918,6 +1929,30 @@ static okm_status count_sorted_two_pass(okm_ctx *c, DevItem *d_items, DevSeg *d_
 // one item (a hot key); the caller takes the partitioning path instead.
 static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint32_t> &add_bits);
 
+// Split bits for one L1 part from its fine-bin pair counts f[0 .. 2^sub):
+// the fewest bits whose largest child stays within `target`, a child being
+// a window of 2^(sub - bits) fine bins (bits <= sub) or a 2^(bits - sub)-th of
+// one fine bin (keys spread evenly inside a fine bin: canonical-key density
+// changes smoothly, not inside 1/2^16 of the key space).
+static uint32_t hint_part_bits(const unsigned long long *f, uint32_t sub, uint64_t target) {
+    const uint32_t nf = 1u << sub;
+    for (uint32_t bits = 0; bits <= sub; ++bits) {
+        const uint32_t w = nf >> bits;
+        uint64_t worst = 0;
+        for (uint32_t c0 = 0; c0 < nf; c0 += w) {
+            uint64_t sum = 0;
+            for (uint32_t j = 0; j < w; ++j) sum += f[c0 + j];
+            worst = std::max<uint64_t>(worst, sum);
+        }
+        if (worst <= target) return bits;
+    }
+    uint64_t fmax = 0;
+    for (uint32_t j = 0; j < nf; ++j) fmax = std::max<uint64_t>(fmax, f[j]);
+    uint32_t more = 0;
+    while (more < 20 && (fmax + (1ull << more) - 1) >> more > target) ++more;
+    return sub + more;
+}
+
 // All runs sorted (see count_sorted_plan).  A child above one item's capacity
 // (canonical-key density gradients inside an L1 bin, a dense run) re-plans
 // with one more key bit for every part, up to 4 times, before giving up to
@@ -1927,11 +1962,14 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
     // one item (count_sorted_plan) -- only the parts that overflowed, e.g. an
     // owner's first and last L1 bins, which its key range covers in part
     std::vector<uint32_t> add_bits(c->nbins, 0);
+    okm_status st = OKM_OK;
     for (uint32_t attempt = 0;; ++attempt) {
-        OKM_TRY(count_sorted_plan(c, fallback, add_bits));
-        if (!*fallback || attempt == 6) return OKM_OK;
+        st = count_sorted_plan(c, fallback, add_bits);
+        if (st != OKM_OK || !*fallback || attempt == 6) break;
         c->hprof.mark("sorted.replan");
     }
+    set_sorted_hint(c, nullptr, 0);  // one count's
+    return st;
 }
 
 static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint32_t> &add_bits) {
@@ -1947,6 +1985,11 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint
     const uint64_t target = item_max * OKM_SORTED_TARGET_Q / 4;
     bool weighted = false;
     for (auto &r : c->runs) weighted |= r.counts != nullptr;
+    // fine bins per L1 bin of the density hint (-1: no usable hint)
+    const int hint_sub = !c->sorted_hint.empty() && c->sorted_hint_bits >= c->l1_bits &&
+                                 c->sorted_hint_bits <= 2 * c->k
+                             ? (int)(c->sorted_hint_bits - c->l1_bits)
+                             : -1;
     std::vector<DevSortedPart> parts;
     std::vector<DevSeg> rbins;
     uint32_t nitems = 0;
@@ -1956,8 +1999,16 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint
         for (auto &r : c->runs) len += r.len(b);
         if (!len) continue;
         uint32_t bits = 0;
-        if (len > item_max && c->shift1 > capbits)
-            while (bits < 20 && bits < c->shift1 && (len >> bits) > target) ++bits;
+        if (len > item_max && c->shift1 > capbits) {
+            if (hint_sub >= 0)
+                // (the densest child is known, not guessed from the mean:
+                // it may come to 3/4 of an item)
+                bits = hint_part_bits(c->sorted_hint.data() + ((size_t)b << hint_sub), (uint32_t)hint_sub,
+                                      item_max * 3 / 4);
+            else
+                while (bits < 20 && bits < c->shift1 && (len >> bits) > target) ++bits;
+            bits = std::min<uint32_t>(bits, std::min<uint32_t>(20u, c->shift1));
+        }
         if (bits || add_bits[b])
             bits = std::min<uint32_t>(std::min<uint32_t>(bits + add_bits[b], 20u), c->shift1);
         parts.push_back(DevSortedPart{b, bits, nitems, (uint32_t)parts.size()});
@@ -3087,6 +3138,7 @@ okm_status okm_reset(okm_ctx *c) {
     c->folds = 0;
     c->pool->reset_peak();
     c->input_lost = false;
+    set_sorted_hint(c, nullptr, 0);
     c->hprof.mark("reset");
     return OKM_OK;
 }

@@ -48,6 +48,12 @@ okm_status adopt_result(okm_ctx *owner, okm_ctx *local, bool *adopted);
 int ctx_device(const okm_ctx *c);
 bool ctx_is_wide(const okm_ctx *c);  // never a canonical key
 uint32_t ctx_k(const okm_ctx *c);
+// Key density of the next count's sorted runs (okm_merge_owned's owner): pairs
+// per top-`fine_bits` key bin over the whole key space (zero outside the
+// owner's range).  count_sorted_plan sizes each L1 part's split from the
+// densest of its fine bins, so the first plan fits; okm_reset / the count
+// clear it.  fine == nullptr clears.
+void set_sorted_hint(okm_ctx *c, const unsigned long long *fine, uint32_t fine_bits);
 bool ctx_is_set(const okm_ctx *c);
 
 // ----------------------------------------------------------------------------
