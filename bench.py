@@ -255,10 +255,13 @@ def main():
     # library's own stream) into one of two owner contexts.
     S = max(1, args.streams)
 
-    def count_batch(c):
+    def count_batch(c, dense=False):
         c.reset()
         c.add_device_batch(dbuf.address, len(batch))
-        return c.count()
+        n = c.count()
+        if dense:  # the dense (keys, counts) arrays gathered too (okm_result_device)
+            c.result_device()
+        return n
 
     pipe = None
     if dist_on:
@@ -270,7 +273,7 @@ def main():
         ctrs, mergers = [okm.KmerCounter(K, "count", device) for _ in range(S)], []
     ctr = ctrs[0]
 
-    def run_steps(nsteps):
+    def run_steps(nsteps, dense=False):
         """nsteps batches through the path; returns the distinct count (N=1)
         or this rank's owned distinct count of the last merge (N>1)."""
         import threading
@@ -280,7 +283,7 @@ def main():
         if S == 1:
             n = 0
             for _ in range(nsteps):
-                n = count_batch(ctr)
+                n = count_batch(ctr, dense)
             return n
         nxt, lock, res, err = [0], threading.Lock(), [], []
 
@@ -291,7 +294,7 @@ def main():
                         if nxt[0] >= nsteps:
                             return
                         nxt[0] += 1
-                    res.append(count_batch(c))
+                    res.append(count_batch(c, dense))
             except BaseException as e:  # surfaced below
                 err.append(e)
 
@@ -326,6 +329,17 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # The step ends with the sorted table as per-item runs (the dense arrays
+    # are gathered by their first reader).  The same K steps again, each also
+    # gathering the dense (keys, counts) arrays: the conservative rate, for a
+    # caller that wants the flat table every batch.
+    dense_ms = None
+    if not dist_on:
+        barrier_sync()
+        t2 = time.perf_counter()
+        run_steps(args.steps, dense=True)
+        barrier_sync()
+        dense_ms = (time.perf_counter() - t2) / args.steps * 1e3
     # one job alone (one context, one stream, one host thread): the latency of
     # a single batch, beside the throughput of S batches in flight above
     single_ms = None
@@ -429,6 +443,10 @@ def main():
         "single_job": ({"ms_per_step": round(single_ms, 3), "value": round(bases / (single_ms * 1e-3), 1),
                         "note": "one context, one stream, one host thread: a batch's latency; `value` above "
                                 f"is {S} batches in flight"} if single_ms else None),
+        "with_dense_table": ({"ms_per_step": round(dense_ms, 3), "value": round(bases / (dense_ms * 1e-3), 1),
+                              "note": "the same K steps, each also gathering the flat (keys, u64 counts) arrays "
+                                      "(okm_result_device -> k_compact_items) inside the timed region"}
+                             if dense_ms else None),
         "kernels": kernels,
         "engine": info,
     }
