@@ -57,7 +57,11 @@ typedef enum okm_test_knob {
     /* device memory budget of the process's contexts in bytes (as OKM_HBM_CAP)
      * — a small GPU, for the out-of-memory paths */
     OKM_TEST_HBM_BUDGET_BYTES = 15,
-    OKM_TEST_KNOBS = 16
+    /* key-range groups of one batch write the table's keys over the batch's
+     * own L1 run when memory-bounded counting splits them (the default);
+     * 1 also with group_keys' forced groups, 0 never */
+    OKM_TEST_GROUP_OVER = 16,
+    OKM_TEST_KNOBS = 17
 } okm_test_knob;
 
 /* value < 0 unsets the knob (the product default). */

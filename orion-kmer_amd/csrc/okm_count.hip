@@ -922,6 +922,11 @@ __global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu((W && sizeo
                                                     uint64_t *__restrict__ fin_keys, uint64_t *__restrict__ fin_counts,
                                                     const ull *__restrict__ fin_base) {
     if (guard && (guard[0] | guard[1])) return;
+    // a poisoned table base: an earlier pipelined key-range group was
+    // abandoned, so this one is counted again too (nothing may be written;
+    // checked once here -- a per-item check in the write path measured 8 %
+    // slower on C4)
+    if (DIRECT && fin_base && (*fin_base & kBasePoison)) return;
     if (d_nitems) nitems = __builtin_amdgcn_readfirstlane((uint32_t)min((ull)nitems, *d_nitems));
     constexpr int kHB = sizeof(KT) > 8 ? kFullHomeBitsW : kHomeBits;  // full-mode home bits
     // full_item shifts a key by rem_bits - kHB with rem_bits > kDenseBits: the

@@ -671,6 +671,7 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
     if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
     if (d_base) {  // the table's next free entry, known on the device only (pipelined key-range groups)
         const ull b = *d_base;
+        if (b & kBasePoison) return;  // an earlier group was abandoned: it is counted again, and so is this one
         dk += b;
         dc += b;
     }
@@ -732,11 +733,19 @@ __global__ __launch_bounds__(256) void k_compact_items(const DevItem *__restrict
 }
 
 // After a group's compaction: *d_base += the group's distinct keys (the
-// exclusive scan's total), unless the launch was abandoned (guard / err).
+// exclusive scan's total).  An abandoned launch (guard / err) poisons the
+// base instead, so no later group of the same pipelined pass writes into the
+// table (the host counts them again from the first abandoned group, at the
+// base without the poison bit: every group before it is in place).
 __global__ void k_advance_base(ull *__restrict__ d_base, const ull *__restrict__ total, const ull *__restrict__ guard,
                                const ull *__restrict__ err) {
-    if ((guard && (guard[0] | guard[1])) || (err && *err)) return;
-    *d_base += *total;
+    const ull b = *d_base;
+    if (b & kBasePoison) return;
+    if ((guard && (guard[0] | guard[1])) || (err && *err)) {
+        *d_base = b | kBasePoison;
+        return;
+    }
+    *d_base = b + *total;
 }
 
 void launch_advance_base(void *stream, unsigned long long *d_base, const unsigned long long *total,

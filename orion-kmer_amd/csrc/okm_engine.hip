@@ -2700,6 +2700,17 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     const double avail = 0.75 * room;
     uint64_t group_keys = total;
     int mode = 0;  // 0: one group (no grouping)
+    // The table's keys can be written over the batch's own L1 run (below):
+    // one batch run, unweighted, and no run needed after this count
+    // (may_take_runs).  Then only the counts are instance-bound new memory.
+    bool over_ok = false;
+    if (!weighted && c->may_take_runs && c->runs.size() == 1) {
+        const Run &r = c->runs[0];
+        over_ok = !r.sorted && !r.folded && !r.host && !r.borrowed && !r.counts && r.keys &&
+                  c->pool->size_of(r.keys) >= std::max<uint64_t>(total, 1) * 8 * c->kw;
+    }
+    if (test_knob(OKM_TEST_GROUP_OVER) == 0) over_ok = false;
+    bool use_over = false;
     const int64_t ge = test_knob(OKM_TEST_GROUP_KEYS);
     if (ge > 0) {
         group_keys = (uint64_t)ge;
@@ -2719,7 +2730,20 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         const double bound = (double)total * res_key;
         const bool a_fits = room_a >= (double)total * ws_key / 64.0;
         const bool a_last = 2.0 * bound > avail && room_l >= (double)total * ws_key / 256.0;
-        if (a_fits && (bound <= 0.5 * avail || 2.0 * bound > avail)) {
+        // the keys over the run (below): the bound-sized table is its counts
+        // only, so groups get the key array's room too.  Groups of more than
+        // kGroupKeysMax instances gain nothing (a group's fixed cost is
+        // ~0.2 ms) and hold 52 B of working set per instance at k > 32: C4
+        // (5.36 Gbases) runs in 6 groups at 173 GB instead of 18 at 228 GB,
+        // 187 vs 189 ms (profiles/r06_c4_over.txt)
+        constexpr uint64_t kGroupKeysMax = uint64_t(1) << 30;
+        const double room_o = avail - (double)total * 8.0;
+        const bool o_fits = over_ok && room_o >= (double)total * ws_key / 64.0;
+        if (o_fits) {
+            mode = 1;
+            use_over = true;
+            group_keys = std::min<uint64_t>((uint64_t)(room_o / ws_key), kGroupKeysMax);
+        } else if (a_fits && (bound <= 0.5 * avail || 2.0 * bound > avail)) {
             mode = 1;
             group_keys = (uint64_t)(room_a / ws_key);
         } else if (a_last) {
@@ -2735,8 +2759,22 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     // it as one group (the direct count: no staged runs, no compaction pass),
     // and the table then gives its tail back
     const bool direct_one = c->wide && mode == 0 && (double)total * (ws_key + res_key) <= avail;
-    if (direct_one) mode = 1;
+    if (direct_one) {
+        mode = 1;
+        use_over = over_ok;  // (one group: its keys over its own run, read by then)
+    }
     if (mode == 0 || (group_keys >= total && !direct_one)) return count_parts(c, segtab, parts, weighted, cp, nullptr);
+    // The table's keys over the batch's own L1 run: with one batch run, the
+    // groups in key order and the runs no longer needed after this count
+    // (may_take_runs), group g's keys -- at most as many as the instances of
+    // groups 0..g -- end before group g + 1's run starts, and group g's own
+    // run was read by its partition pass before its count writes.  The
+    // instance-bound key array (16 B per instance at k > 32: 85 GB at C4)
+    // is then never allocated.
+    // forced by the test hook too (knob group_over), so the small test
+    // inputs take the path
+    if (mode == 1 && over_ok && test_knob(OKM_TEST_GROUP_OVER) == 1) use_over = true;
+    Run *over = use_over ? &c->runs[0] : nullptr;
     // every group reads the runs: none may hold a group's staged keys
     struct Keep {
         okm_ctx *c;
@@ -2760,9 +2798,10 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         ResDst *d;
         std::vector<Tab> *tabs;
         bool armed = true;
+        bool keys_are_run = false;  // (the run's block: it stays with the run)
         ~Guard() {
             if (!armed) return;
-            c->pool->put(d->keys);
+            if (!keys_are_run) c->pool->put(d->keys);
             c->pool->put(d->counts);
             for (auto &t : *tabs) {
                 c->pool->put(t.keys);
@@ -2771,9 +2810,22 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         }
     } guard{c, &d, &tabs};
     if (mode == 1) {
-        OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
+        if (over) {
+            d.keys = over->keys;
+            guard.keys_are_run = true;
+        } else {
+            OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(total, 1) * c->kw, &d.keys));
+        }
         OKM_TRY(pool_get(*c->pool, std::max<uint64_t>(total, 1), &d.counts));
     }
+    // once a group wrote over the run, a failure leaves no input to count again
+    struct Lost {
+        okm_ctx *c;
+        bool on = false;
+        ~Lost() {
+            if (on) c->input_lost = true;
+        }
+    } lost{c};
     const okm_engine_info info0 = c->info;
     okm_engine_info agg = info0;
     agg.work_items = 0;
@@ -2791,9 +2843,11 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
     // group's with no host sync in between (the table's next entry advances
     // on the device); one sync at the end reads every group's words.  A group
     // whose speculative count was abandoned (a sampled slot overflowed, a
-    // child too big for one item) left nothing in the table and moved nothing:
-    // then every group is counted again, one sync each (the runs are intact:
-    // groups never write into them).
+    // child too big for one item) left nothing in the table and moved nothing,
+    // and poisoned the device-side base, so no later group wrote either: then
+    // the groups from the first abandoned one on are counted again, one sync
+    // each, from the base the groups before it reached (their entries are in
+    // place, and the runs of the groups from there on are intact).
     struct Slots {
         okm_ctx *c;
         unsigned long long *p = nullptr, *d_base = nullptr;
@@ -2810,20 +2864,24 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         pipelined = slots.p && pool_get(*c->pool, 1, &d_base) == OKM_OK;
         if (pipelined) HIP_TRY(hipMemsetAsync(d_base, 0, sizeof(unsigned long long), c->stream));
     }
+    size_t g_from = 0;  // the first group of this pass
     for (int pass = 0; pass < 2; ++pass) {
         bool redo = false;
-        d.off = 0;
+        if (pass == 0) {
+            d.off = 0;
+            agg = info0;
+            agg.work_items = 0;
+            agg.max_partition = 0;
+            ngroups = 0;
+        }
         d.d_base = pipelined ? d_base : nullptr;
-        agg = info0;
-        agg.work_items = 0;
-        agg.max_partition = 0;
-        ngroups = 0;
-        for (size_t g = 0; g < G; ++g) {
+        for (size_t g = g_from; g < G; ++g) {
             std::vector<Part> sub(parts.begin() + cuts[g], parts.begin() + cuts[g + 1]);
             c->info.levels = 0;
             c->info.l2_bits = 0;
             if (pipelined) d.hslot = slots.p + 8 * g;
             OKM_TRY(count_parts(c, segtab, sub, weighted, cp, mode == 1 ? &d : nullptr));
+            lost.on = over != nullptr;  // (this group's keys are written, or queued)
             agg.levels = std::max(agg.levels, c->info.levels);
             agg.l2_bits = std::max(agg.l2_bits, c->info.l2_bits);
             agg.work_items += c->info.work_items;
@@ -2846,22 +2904,34 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
                                c->stream));
         OKM_TRY(sync(c));
         base = c->hres[kHresCount];
+        size_t first_bad = G;
         for (size_t g = 0; g < G; ++g) {
             const unsigned long long *hs = slots.p + 8 * g;
             if (hs[1]) return fail(OKM_E_DEVICE, "count_items invariant violated (code " + std::to_string(hs[1]) + ")");
-            redo |= (hs[2] | hs[3]) != 0;
+            if ((hs[2] | hs[3]) != 0 && first_bad == G) first_bad = g;
             agg.max_partition = std::max<uint64_t>(agg.max_partition, hs[4]);
         }
-        d.off = base;
+        redo = first_bad < G;
+        if (redo != ((base & kBasePoison) != 0))
+            return fail(OKM_E_DEVICE, "pipelined key-range groups: table base and group flags disagree");
+        d.off = base & ~kBasePoison;
         if (!redo) break;
         c->hprof.mark("groups.redo");
-        pipelined = false;  // every group again, one sync each
+        pipelined = false;  // the groups from the first abandoned one, one sync each
+        g_from = first_bad;
+        ngroups = (uint32_t)first_bad;
     }
+    lost.on = false;
     uint64_t nd = d.off;
     if (mode == 1) {
         guard.armed = false;
         c->res_keys = d.keys;
         c->res_counts = d.counts;
+        if (over) {  // the run's block is the table's now; the run is gone (released after the count)
+            over->keys = nullptr;
+            c->took_runs = true;
+            OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, nd, 1.0));
+        }
         if (direct_one) {
             OKM_TRY(shrink_table(c, &c->res_keys, &c->res_counts, nd, 1.0));
             ngroups = 0;  // (one pass: no grouping)

@@ -283,6 +283,9 @@ void launch_compact_items(void *stream, const DevItem *items, uint32_t nitems,
                           uint64_t *dst_keys, uint64_t *dst_counts, bool wide, bool narrow,
                           const unsigned long long *guard = nullptr, const unsigned long long *err = nullptr,
                           const unsigned long long *d_nitems = nullptr, const unsigned long long *d_base = nullptr);
+// Pipelined key-range groups: bit 63 of the device-side table base marks a
+// pass in which a group was abandoned; no later group writes then.
+constexpr unsigned long long kBasePoison = 1ull << 63;
 // d_base (pipelined key-range groups): the compaction writes at dst + *d_base,
 // and launch_advance_base then adds the group's distinct keys (*total) to it
 // -- nothing of either when a guard word or *err is set.

@@ -27,6 +27,7 @@ KNOBS: Dict[str, int] = {
     "gz_strict": 13,
     "no_libdeflate": 14,
     "hbm_budget_bytes": 15,
+    "group_over": 16,
 }
 
 

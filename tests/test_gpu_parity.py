@@ -633,20 +633,27 @@ def test_grouped_count(k, wide, mode, maxb, monkeypatch):
             assert np.array_equal(fk, xk) and np.array_equal(fc, xc), mc
 
 
-@pytest.mark.parametrize("cap,k", [(None, 31), (0.5, 63)])  # (two of the four crossings: suite time, round 6)
-def test_grouped_count_pipelined_and_redo(cap, k):
+@pytest.mark.parametrize("cap,k,over", [(None, 31, False), (0.5, 31, True), (0.5, 63, True)])
+def test_grouped_count_pipelined_and_redo(cap, k, over):
     """Key-range groups in one instance-bound table, pipelined: every group's
     kernels queue behind the previous group's with no host sync and the
     table's next entry advances on the device.  Groups of >= 4 Mi keys take
     the sampled partition placement; with part_cap_permille = 500 their
-    sampled slots overflow, the speculative counts are abandoned, and every
-    group is counted again one sync at a time.  Exact both ways.  k = 63:
-    the count kernel writes the table itself (items in order, each at its
-    look-back prefix: okm_count.hip launch_count_direct), no compaction."""
+    sampled slots overflow, the speculative counts are abandoned (the first
+    abandoned group poisons the device-side table base, so no later group
+    writes), and the groups from the first abandoned one on are counted again
+    one sync at a time.  `over` (knob group_over; otherwise taken when the
+    instance-bound table would leave no room for pipelined groups): the
+    table's keys are written over the batch's own L1 run, group by group in
+    key order (count_grouped), so a group that wrote too early would destroy
+    a later group's input -- exact all ways.  k = 63: the count kernel writes
+    the table itself (items in order, each at its look-back prefix:
+    okm_count.hip launch_count_direct), no compaction."""
     from oracle import OracleCounterWide
     wide = k > 32
     testing.set_knob("group_keys", 5_000_000)
     testing.set_knob("group_exact", 0)
+    testing.set_knob("group_over", 1 if over else -1)
     if cap:
         testing.set_knob("part_cap_permille", round(cap * 1000))
     batch = okm.synth_reads(130_000, 150, genome_len=20_000_000, genome_seed=12, seed=4, sub_rate=0.01)

@@ -677,7 +677,14 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     ap.add_argument("--loopback", type=int, default=0,
                     help="c5: P virtual ranks on one GPU through okm_comm_init_loopback (the distributed compare)")
+    ap.add_argument("--knob", action="append", default=[],
+                    help="NAME=VALUE: an engine test knob for the run (okm.testing; A/B of rare paths)")
     args = ap.parse_args()
+    if args.knob:
+        from okm import testing
+        for kv in args.knob:
+            name, val = kv.split("=", 1)
+            testing.set_knob(name, int(val))
     c5 = wl_c5_dist if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.loopback else wl_c5
     out = {"query": wl_query, "build": wl_build, "wide": wl_wide, "classify": wl_classify,
            "c5": c5, "c3": wl_c3_loop}[args.workload](args)
