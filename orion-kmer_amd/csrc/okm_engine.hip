@@ -2731,12 +2731,13 @@ static okm_status count_grouped(okm_ctx *c, std::vector<DevSeg> &segtab, std::ve
         const bool a_fits = room_a >= (double)total * ws_key / 64.0;
         const bool a_last = 2.0 * bound > avail && room_l >= (double)total * ws_key / 256.0;
         // the keys over the run (below): the bound-sized table is its counts
-        // only, so groups get the key array's room too.  Groups of more than
-        // kGroupKeysMax instances gain nothing (a group's fixed cost is
-        // ~0.2 ms) and hold 52 B of working set per instance at k > 32: C4
-        // (5.36 Gbases) runs in 6 groups at 173 GB instead of 18 at 228 GB,
-        // 187 vs 189 ms (profiles/r06_c4_over.txt)
-        constexpr uint64_t kGroupKeysMax = uint64_t(1) << 30;
+        // only, so groups get the key array's room too.  Groups hold 52 B of
+        // working set per instance at k > 32 and larger ones gain little
+        // (C4, 5.36 Gbases: 18 groups 188 ms at 228.5 GB with a separate key
+        // array; over the run 5 groups of <= 2^30 instances 180-186 ms at
+        // 175 GB, 4 of <= 1.4 G 179-183 ms at 185 GB, 3 of <= 1.8 G 177-180 ms
+        // at 203 GB: profiles/r06_c4_over.txt, r06_c4_groups.txt)
+        constexpr uint64_t kGroupKeysMax = 1400000000ull;
         const double room_o = avail - (double)total * 8.0;
         const bool o_fits = over_ok && room_o >= (double)total * ws_key / 64.0;
         if (o_fits) {
