@@ -185,6 +185,9 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
                                                   uint32_t max_jobs) {
     constexpr int kWaves = FB / 64;
     static_assert(FMAX / FB * 64 <= 4096, "ranks fit 12 bits");
+    // rows of a job held in registers between the passes (unweighted big jobs)
+    // (8 rows of K128 keys: 125 VGPRs; 16 rows spill 50 at the 128-VGPR cap)
+    constexpr int kHold = (!W && FMAX > kFanSmallMax) ? (sizeof(KT) > 8 ? 8 : 12) : 0;
     __shared__ uint16_t brs[FMAX];                // per key: bin << 12 | rank within (wave, bin)
     __shared__ uint32_t wtot[kWaves][kFanBins];   // per (wave, bin): count, then start in the job's range
     __shared__ uint32_t btot[kFanBins];
@@ -201,9 +204,7 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
         const ull lt = (1ull << lane) - 1ull;
         // pass 1: bins and ranks
         uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
-        for (uint32_t u = 0; u < rows; ++u) {
-            const uint64_t idx = (uint64_t)u * FB + t;
-            const KT key = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+        auto rank_row = [&](uint32_t u, const KT &key) {  // (every lane of the wave: ballots)
             const bool v = !KeyOps<KT>::is_empty(key);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(key, shift) & (nb - 1)) : 0u;
             uint32_t br = 0;
@@ -216,6 +217,24 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
                 }
             }
             brs[u * FB + t] = (uint16_t)br;
+        };
+        // the job's first kHold rows stay in registers for pass 2, so only the
+        // rest is read twice (big unweighted jobs: k = 63 children of 16-64 Ki
+        // keys, a third of C4's keys)
+        KT kk[kHold > 0 ? kHold : 1];
+        if (kHold > 0) {
+#pragma unroll
+            for (int u = 0; u < kHold; ++u) {
+                const uint64_t idx = (uint64_t)u * FB + t;
+                kk[u] = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+            }
+#pragma unroll
+            for (int u = 0; u < kHold; ++u)
+                if ((uint32_t)u < rows) rank_row((uint32_t)u, kk[u]);  // block-uniform
+        }
+        for (uint32_t u = kHold; u < rows; ++u) {
+            const uint64_t idx = (uint64_t)u * FB + t;
+            rank_row(u, idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty());
         }
 #pragma unroll
         for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
@@ -261,8 +280,18 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
             atomicMax(&oflags[2], len);
         }
         __syncthreads();
-        // pass 2: every key to its place (keys read again, from L2)
-        for (uint32_t u = 0; u < rows; ++u) {
+        // pass 2: every key to its place (the held rows from registers, the
+        // others read again)
+        if (kHold > 0) {
+#pragma unroll
+            for (int u = 0; u < kHold; ++u) {
+                const uint64_t idx = (uint64_t)u * FB + t;
+                if ((uint32_t)u >= rows || idx >= jb.len || KeyOps<KT>::is_empty(kk[u])) continue;
+                const uint32_t br = brs[u * FB + t];
+                dk[jb.off + wtot[wv][br >> 12] + (br & 0xFFFu)] = kk[u];
+            }
+        }
+        for (uint32_t u = kHold; u < rows; ++u) {
             const uint64_t idx = (uint64_t)u * FB + t;
             if (idx >= jb.len) continue;
             const KT key = sk[jb.off + idx];

@@ -1,5 +1,5 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/c4one
-for r in 1 2; do for n in head main; do
+for r in 1 2 3 4; do for n in head main; do
   if [ "$n" = main ]; then lib=orion-kmer_amd/build/liborion_kmer.so; else lib=orion-kmer_amd/build_$n/liborion_kmer.so; fi
   OKM_LIB=$lib timeout -k 10 300 python tools/bench_paths.py --workload wide --gbases 5.36 --steps 2 --warmup 1 > gpurun_out/c4one/${n}_$r.json 2> gpurun_out/c4one/${n}_$r.log || { echo "$n failed"; exit 1; }
   python3 -c "import json;d=json.load(open('gpurun_out/c4one/${n}_$r.json'));print('$n', d['ms_per_step'], {k:round(v['avg_ms']*v['launches'],1) for k,v in d['kernels'].items() if k in ('count_items','part_scatter','fan_split')}, d['engine']['device_peak_bytes']/1e9)"
