@@ -1964,8 +1964,11 @@ static okm_status count_sorted(okm_ctx *c, bool *fallback) {
     std::vector<uint32_t> add_bits(c->nbins, 0);
     okm_status st = OKM_OK;
     for (uint32_t attempt = 0;; ++attempt) {
+        const std::vector<uint32_t> before = add_bits;
         st = count_sorted_plan(c, fallback, add_bits);
-        if (st != OKM_OK || !*fallback || attempt == 6) break;
+        // no part can split further (its bits are at the cap: keys crowded
+        // into a sliver of the key space): the partitioning path, at once
+        if (st != OKM_OK || !*fallback || attempt == 6 || add_bits == before) break;
         c->hprof.mark("sorted.replan");
     }
     set_sorted_hint(c, nullptr, 0);  // one count's
@@ -2077,7 +2080,10 @@ static okm_status count_sorted_plan(okm_ctx *c, bool *fallback, std::vector<uint
             if (pmax[p] <= item_max) continue;
             uint32_t more = 1;
             while (more < 8 && (pmax[p] >> more) > target) ++more;
-            add_bits[parts[p].bin] += more;
+            // (only while the part's bits can still grow: capped at 20 and at
+            // the key bits below the L1 prefix)
+            const uint32_t cap = std::min<uint32_t>(20u, c->shift1);
+            if (parts[p].bits < cap) add_bits[parts[p].bin] += std::min<uint32_t>(more, cap - parts[p].bits);
         }
         if (c->hprof.on) {
             uint64_t maxlen = 0, maxbits = 0;
