@@ -186,8 +186,9 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
     constexpr int kWaves = FB / 64;
     static_assert(FMAX / FB * 64 <= 4096, "ranks fit 12 bits");
     // rows of a job held in registers between the passes (unweighted big jobs)
-    // (8 rows of K128 keys: 125 VGPRs; 16 rows spill 50 at the 128-VGPR cap)
-    constexpr int kHold = (!W && FMAX > kFanSmallMax) ? (sizeof(KT) > 8 ? 8 : 12) : 0;
+    // (12 rows of K128 keys: 128 VGPRs, no spills, once the rows' loads share
+    // one lane offset; 16 rows spill 24 at the 128-VGPR cap)
+    constexpr int kHold = (!W && FMAX > kFanSmallMax) ? 12 : 0;
     __shared__ uint16_t brs[FMAX];                // per key: bin << 12 | rank within (wave, bin)
     __shared__ uint32_t wtot[kWaves][kFanBins];   // per (wave, bin): count, then start in the job's range
     __shared__ uint32_t btot[kFanBins];
@@ -225,8 +226,11 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
         if (kHold > 0) {
 #pragma unroll
             for (int u = 0; u < kHold; ++u) {
-                const uint64_t idx = (uint64_t)u * FB + t;
-                kk[u] = idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+                // (the row's start and its live lanes are block-uniform: one
+                // lane offset serves every row, no per-row index registers)
+                const int32_t left = __builtin_amdgcn_readfirstlane((int32_t)jb.len - u * FB);
+                const KT *row = sk + jb.off + (uint64_t)u * FB;
+                kk[u] = (int32_t)t < left ? row[t] : KeyOps<KT>::empty();
             }
 #pragma unroll
             for (int u = 0; u < kHold; ++u)
@@ -285,8 +289,7 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
         if (kHold > 0) {
 #pragma unroll
             for (int u = 0; u < kHold; ++u) {
-                const uint64_t idx = (uint64_t)u * FB + t;
-                if ((uint32_t)u >= rows || idx >= jb.len || KeyOps<KT>::is_empty(kk[u])) continue;
+                if (KeyOps<KT>::is_empty(kk[u])) continue;  // (rows past the job's end were loaded empty)
                 const uint32_t br = brs[u * FB + t];
                 dk[jb.off + wtot[wv][br >> 12] + (br & 0xFFFu)] = kk[u];
             }
@@ -309,7 +312,8 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
 // shards, k=63): one 1024-thread workgroup per job holds the job's keys in
 // registers (16 rows), so they are read once — the LDS variants read them
 // twice (ranks first, keys again for the scatter) — and only the per-(wave,
-// bin) counters live in LDS (two workgroups per CU, VGPR-bound).
+// bin) counters live in LDS.  (128 VGPRs, one workgroup per CU; 512-thread
+// workgroups for the jobs of <= 8 Ki keys, two per CU, measured no faster.)
 constexpr int kFanRegBlock = 1024, kFanRegRows = 16, kFanRegMax = kFanRegBlock * kFanRegRows;
 static_assert(kFanRegMax == kFanSmallJob, "the register variant takes every small job");
 
@@ -320,7 +324,8 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
                                                                 DevItem *__restrict__ items,
                                                                 DevSeg *__restrict__ segs, uint64_t item_max,
                                                                 uint32_t capbits, ull *__restrict__ oflags) {
-    constexpr int kWaves = kFanRegBlock / 64;
+    constexpr int RB = kFanRegBlock;
+    constexpr int kWaves = RB / 64;
     __shared__ uint32_t wtot[kWaves][kFanBins];
     __shared__ uint32_t btot[kFanBins];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -334,14 +339,17 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
         uint32_t br[kFanRegRows];  // bin << 16 | rank within (wave, bin); ~0: no key
 #pragma unroll
         for (int u = 0; u < kFanRegRows; ++u) {
-            const uint32_t idx = (uint32_t)u * kFanRegBlock + t;
-            kk[u] = idx < len ? sk[jb.off + idx] : KeyOps<KT>::empty();
+            // (each row's start and live-lane bound are block-uniform: one lane
+            // offset serves every row, no per-row index registers)
+            const int32_t left = __builtin_amdgcn_readfirstlane((int32_t)len - u * RB);
+            const KT *row = sk + jb.off + (uint64_t)u * RB;
+            kk[u] = (int32_t)t < left ? row[t] : KeyOps<KT>::empty();
         }
         uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
 #pragma unroll
         for (int u = 0; u < kFanRegRows; ++u) {
             br[u] = ~0u;
-            if ((uint32_t)u * kFanRegBlock >= len) continue;  // block-uniform
+            if ((uint32_t)u * RB >= len) continue;  // block-uniform
             const bool v = !KeyOps<KT>::is_empty(kk[u]);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(kk[u], shift) & (nb - 1)) : 0u;
 #pragma unroll
