@@ -176,6 +176,29 @@ uint64_t fan_split_max() { return (uint64_t)kFanBigMax; }
 uint64_t fan_split_max_in_place() { return (uint64_t)kFanSmallJob; }
 static_assert(kFanSmallMax == kFanSmallJob, "the job list's small/large cut is the small variants' capacity");
 
+// Rank of a lane's key among the wave's valid keys in the same bin (lane
+// order), and the bins' running counts: one ballot per bin bit (<= 4) instead
+// of one per bin (16), so a row costs ~5 ballots and ~30 VALU instead of 16
+// ballots and ~160.  runv: lane q < kFanBins holds bin q's running count
+// (lanes q >= 2^bits hold nothing meaningful).
+__device__ __forceinline__ uint32_t wave_bin_rank(bool v, uint32_t b, uint32_t bits, uint32_t &runv, uint32_t lane,
+                                                  ull lt) {
+    const ull vm = __ballot(v);
+    ull miss = 0, qmiss = 0;  // lanes whose bin differs from mine / from bin `lane`
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        if (i < bits) {  // block-uniform
+            const ull mi = __ballot(v && ((b >> i) & 1u));
+            miss |= mi ^ (((b >> i) & 1u) ? ~0ull : 0ull);
+            qmiss |= mi ^ (((lane >> i) & 1u) ? ~0ull : 0ull);
+        }
+    }
+    const uint32_t base = (uint32_t)__shfl((int)runv, (int)b, 64);
+    const uint32_t rank = base + (uint32_t)__popcll(vm & ~miss & lt);
+    if (lane < (uint32_t)kFanBins) runv += (uint32_t)__popcll(vm & ~qmiss);
+    return rank;
+}
+
 template <typename KT, bool W, int FB, int FMAX>
 __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ jobs, const ull *__restrict__ flags,
                                                   const KT *__restrict__ sk, const uint64_t *__restrict__ sc,
@@ -204,20 +227,12 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
         const uint32_t rows = (uint32_t)((jb.len + FB - 1) / FB);  // block-uniform
         const ull lt = (1ull << lane) - 1ull;
         // pass 1: bins and ranks
-        uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
+        uint32_t runv = 0;  // lane q: bin q's running count in this wave
         auto rank_row = [&](uint32_t u, const KT &key) {  // (every lane of the wave: ballots)
             const bool v = !KeyOps<KT>::is_empty(key);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(key, shift) & (nb - 1)) : 0u;
-            uint32_t br = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q) {
-                if (q < nb) {  // block-uniform
-                    const ull m = __ballot(v && b == q);
-                    if (v && b == q) br = (q << 12) | (run[q] + (uint32_t)__popcll(m & lt));
-                    run[q] += (uint32_t)__popcll(m);
-                }
-            }
-            brs[u * FB + t] = (uint16_t)br;
+            const uint32_t rank = wave_bin_rank(v, b, jb.bits, runv, lane, lt);
+            brs[u * FB + t] = (uint16_t)(v ? (b << 12) | rank : 0u);
         };
         // the job's first kHold rows stay in registers for pass 2, so only the
         // rest is read twice (big unweighted jobs: k = 63 children of 16-64 Ki
@@ -233,16 +248,16 @@ __global__ __launch_bounds__(FB) void k_fan_split(const DevFanJob *__restrict__ 
                 kk[u] = (int32_t)t < left ? row[t] : KeyOps<KT>::empty();
             }
 #pragma unroll
-            for (int u = 0; u < kHold; ++u)
+            for (int u = 0; u < kHold; ++u) {
                 if ((uint32_t)u < rows) rank_row((uint32_t)u, kk[u]);  // block-uniform
+                __builtin_amdgcn_sched_barrier(0);  // one row's masks live at a time
+            }
         }
         for (uint32_t u = kHold; u < rows; ++u) {
             const uint64_t idx = (uint64_t)u * FB + t;
             rank_row(u, idx < jb.len ? sk[jb.off + idx] : KeyOps<KT>::empty());
         }
-#pragma unroll
-        for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
-            if (lane == 0) wtot[wv][q] = q < nb ? run[q] : 0u;
+        if (lane < (uint32_t)kFanBins) wtot[wv][lane] = lane < nb ? runv : 0u;
         __syncthreads();
         if (t < nb) {
             uint32_t s = 0;
@@ -345,25 +360,18 @@ __global__ __launch_bounds__(kFanRegBlock) void k_fan_split_reg(const DevFanJob 
             const KT *row = sk + jb.off + (uint64_t)u * RB;
             kk[u] = (int32_t)t < left ? row[t] : KeyOps<KT>::empty();
         }
-        uint32_t run[kFanBins] = {};  // wave-uniform running counts per bin
+        uint32_t runv = 0;  // lane q: bin q's running count in this wave
 #pragma unroll
         for (int u = 0; u < kFanRegRows; ++u) {
             br[u] = ~0u;
             if ((uint32_t)u * RB >= len) continue;  // block-uniform
             const bool v = !KeyOps<KT>::is_empty(kk[u]);
             const uint32_t b = v ? (uint32_t)(KeyOps<KT>::shr(kk[u], shift) & (nb - 1)) : 0u;
-#pragma unroll
-            for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q) {
-                if (q < nb) {  // block-uniform
-                    const ull m = __ballot(v && b == q);
-                    if (v && b == q) br[u] = (q << 16) | (run[q] + (uint32_t)__popcll(m & lt));
-                    run[q] += (uint32_t)__popcll(m);
-                }
-            }
+            const uint32_t rank = wave_bin_rank(v, b, jb.bits, runv, lane, lt);
+            if (v) br[u] = (b << 16) | rank;
+            __builtin_amdgcn_sched_barrier(0);  // one row's masks live at a time
         }
-#pragma unroll
-        for (uint32_t q = 0; q < (uint32_t)kFanBins; ++q)
-            if (lane == 0) wtot[wv][q] = q < nb ? run[q] : 0u;
+        if (lane < (uint32_t)kFanBins) wtot[wv][lane] = lane < nb ? runv : 0u;
         __syncthreads();
         if (t < nb) {
             uint32_t s = 0;
